@@ -1,0 +1,206 @@
+"""bench.py — b2p2t_gru+w2v training step on MI355X (BASELINE.json metric:
+"train steps/sec + CTC loss, b2p2t_gru+w2v bs=32 seq=1024 at 1/2/4/8 MI355X").
+
+Workload (BASELINE.json configs[1]): wav2vec2-base architecture (768/12L/12H/3072, random-init,
+hub unreachable), GRU H256x2 bidirectional, fc [] -> 768, bs=32 per GPU, 1024-bin x 256-channel
+synthetic windows (x ~ N(0,1)), train mode (dropout 0.1 / LayerDrop 0.1 as the checkpoint config),
+unfreeze_strategy=brain_encoder (Adam over the brain encoder; the frozen w2v still computes weight
+gradients, as the reference does). One step = forward + backward + DDP gradient all-reduce (N>1)
++ Adam + CTC loss readback (.item(), as the reference's forward does), inputs pre-staged in HBM.
+
+usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
+# train-step FLOPs, base bs=32 L=1024 = 3 x 1738.7 GFLOP forward
+STEP_TFLOP_BASE_BS32 = 5.216
+
+
+def make_config(bs, L):
+    return dict(name="bench_base", seed=42, B=bs, L=L, in_lens=[L] * bs, tgt_range=(60, 120), hidden_size=768,
+                layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2,
+                bidirectional=True, fc_hidden=[], learnable_h0=False, full_grad_max=0, infeasible=False)
+
+
+def build(cfg, device, train_dropouts=True):
+    from tests.helpers import build_model
+    return build_model(cfg, device=device, train_dropouts=train_dropouts)
+
+
+def batch_on(cfg, device):
+    from tests.golden.configs import make_batch
+    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    x, day, il, tgt, tl = make_batch(cfg)
+    b = make_b2t_batch(x, tgt, day, il, tl)
+    return b.cuda() if device != "cpu" else b
+
+
+def cpu_baseline(bs_sample=8, L=1024, bs_metric=32):
+    """The CPU oracle (torch-CPU fp32 restatement, oracle/b2p2t_oracle.py) timed on the host on a
+    bounded sample of the same workload: one warm-up + 2 timed fwd+bwd+Adam steps at bs=bs_sample,
+    scaled linearly to bs_metric."""
+    from oracle.b2p2t_oracle import loss_and_grads, adam_step
+    from tests.helpers import oracle_cfg
+    cfg = make_config(bs_sample, L)
+    ocfg = oracle_cfg(cfg)
+    ocfg.hidden_dropout = ocfg.activation_dropout = ocfg.attention_dropout = ocfg.final_dropout = 0.1
+    ocfg.layerdrop = 0.1
+    model = build(cfg, "cpu")
+    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    from tests.golden.configs import make_batch
+    x, day, il, tgt, tl = make_batch(cfg)
+    b = dict(x=x, day_idxs=day, input_lens=il, target=tgt, target_lens=tl)
+    brain = [k for k in sd if k.startswith("brain_encoder.") and sd[k].is_floating_point()
+             and "gaussian" not in k]
+    state = {k: (torch.zeros_like(sd[k]), torch.zeros_like(sd[k])) for k in brain}
+
+    def step(i):
+        loss, grads = loss_and_grads(sd, b, ocfg, training=True)
+        for k in brain:
+            m, v = state[k]
+            sd[k], m, v = adam_step(sd[k], grads[k], m, v, i + 1, 1e-3)
+            state[k] = (m, v)
+        return float(loss)
+
+    step(0)
+    t0 = time.perf_counter()
+    n = 2
+    for i in range(n):
+        step(i + 1)
+    dt = (time.perf_counter() - t0) / n
+    per_metric_step = dt * bs_metric / bs_sample
+    return {"value": round(1.0 / per_metric_step, 5), "unit": "steps/s", "cores": torch.get_num_threads(),
+            "kind": "port",
+            "sample": f"oracle fwd+bwd+Adam, bs={bs_sample} L={L} train mode, mean of {n} steps after 1 warm-up "
+                      f"({dt:.2f} s/step), scaled x{bs_metric // bs_sample} to bs={bs_metric}"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--bs", type=int, default=32)
+    ap.add_argument("--seq", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    device = f"cuda:{local}"
+    torch.cuda.set_device(local)
+    torch.manual_seed(1234 + rank)
+
+    from wav2vec2forbrain_amd import functional as Fn, _lib
+    from wav2vec2forbrain_amd.optim import HipAdam
+    from wav2vec2forbrain_amd.train.ddp import GradBucketReducer, unused_param_names
+
+    Fn.set_precision("bf16")
+    cfg = make_config(args.bs, args.seq)
+    model = build(cfg, device)
+    model.train()
+    skip = unused_param_names(model)
+    brain_params = [p for n, p in model.named_parameters() if n.startswith("brain_encoder.") and n not in skip]
+    opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
+    reducer = GradBucketReducer(brain_params) if world > 1 else None
+    batch = batch_on(cfg, device)
+
+    def step():
+        opt.zero_grad()
+        out = model(batch)            # forward incl. ctc_loss.item() (reference :94)
+        out.loss.backward()
+        if reducer is not None:
+            reducer.finish()
+        opt.step()
+        return out.metrics["ctc_loss"]
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    _lib.check(_lib.load().b2p_timing_enable(_lib.TIMING_GEMM, 100000), "timing_enable")
+    Fn.set_gemm_timing(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    losses = [step() for _ in range(args.steps)]
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    Fn.set_gemm_timing(False)
+    ms = ctypes_read_timing()
+    _lib.check(_lib.load().b2p_timing_enable(_lib.TIMING_GEMM, 0), "timing_disable")
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    if rank != 0:
+        dist.destroy_process_group() if world > 1 else None
+        return
+    steps_per_s = args.steps / dt * 1.0          # global steps/s (every rank does one step per step)
+    gemm_ms, gemm_n, gemm_flops = ms
+    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    step_tflop = STEP_TFLOP_BASE_BS32 * args.bs / 32 * args.seq / 1024
+    res = {
+        "metric": "train steps/sec + CTC loss, b2p2t_gru+w2v bs=32 seq=1024",
+        "value": round(steps_per_s, 4),
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16",
+        "data": "synthetic (x~N(0,1) 256-ch windows, random-init weights of the wav2vec2-base architecture)",
+        "config": {"workload": "b2p2t_gru+w2v wav2vec2-base (12L/768), GRU H256x2 bidir, train mode, "
+                               "unfreeze=brain_encoder, Adam", "global_batch": args.bs * world,
+                   "per_gpu_batch": args.bs, "seq_len": args.seq, "parallelism": f"dp{world}"},
+        "ctc_loss": round(losses[-1], 5),
+        "samples_per_s": round(steps_per_s * args.bs * world, 2),
+        "step_mfma_frac": round(step_tflop * steps_per_s / BF16_DENSE_PEAK_TFLOPS, 4),
+        "roofline": {"bound": "mfma", "kernel": "b2p_gemm (all GEMM launches of the step)",
+                     "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": None,
+                     "launches": gemm_n, "avg_launch_us": round(gemm_ms * 1e3 / max(gemm_n, 1), 2)},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        res["cpu_baseline"] = cpu_baseline(L=args.seq)
+    print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def ctypes_read_timing():
+    import ctypes
+    from wav2vec2forbrain_amd import _lib
+    ms = ctypes.c_float()
+    n = ctypes.c_int32()
+    fl = ctypes.c_double()
+    _lib.check(_lib.load().b2p_timing_read(_lib.TIMING_GEMM, ctypes.byref(ms), ctypes.byref(n), ctypes.byref(fl)),
+               "timing_read")
+    return ms.value, n.value, fl.value
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+/*
+ * b2p_hip.h — C ABI of the MI355X-native (gfx950 / CDNA4) b2p2t_gru+w2v training-step kernels.
+ *
+ * The reference (yuanhao-chen-nyoeghau/Wav2Vec2ForBrain) is pure Python on PyTorch/HF transformers:
+ * it has no FFI. Its hot path is the per-batch body of Trainer._train_epoch
+ * (src/train/train_loop.py:41-84) calling W2VBrainEncoderModel.forward
+ * (src/model/w2v_custom_feat_extractor.py:65-122). Every entry point below replaces one
+ * third-party operator that path reaches; the reference call site is cited per entry.
+ * The "binding a maintainer would add" is the ctypes layer in
+ * wav2vec2forbrain_amd/_lib.py.
+ *
+ * Conventions
+ *  - raw device pointers (fp32 activations/weights/grads, int64 indices) + explicit sizes;
+ *    the caller (PyTorch caching allocator) owns every buffer, workspaces included;
+ *  - `stream` is a hipStream_t; all work is stream-ordered, no host synchronisation,
+ *    no allocation on the hot path (graph-capturable);
+ *  - return 0 on success, nonzero on error; b2p_last_error() returns the message
+ *    (thread-local, valid until the next failing call on that thread).
+ */
+#ifndef B2P_HIP_H
+#define B2P_HIP_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* b2p_stream_t; /* hipStream_t */
+
+/* ------------------------------------------------------------------ library */
+const char* b2p_last_error(void);
+int b2p_version(void);
+/* optional per-kernel-family HIP-event timing (bench.py roofline): family ids in
+ * wav2vec2forbrain_amd/_lib.py. enable=0 turns it off. */
+int b2p_timing_enable(int family, int max_events);
+int b2p_timing_read(int family, float* total_ms, int* count, double* total_flops);
+
+/* ------------------------------------------------------------------ GEMM
+ * C[z](m,n) = epilogue( alpha * sum_k A[z](m,k) * B[z](k,n) ), bf16 MFMA (fp32 accumulate)
+ * or exact-fp32 MFMA (precision=1). Operands are fp32 in HBM and converted while being
+ * staged into LDS. Replaces every nn.Linear / matmul / conv-as-GEMM of the path:
+ *   nn.Linear (TF w2v q/k/v/out_proj, FFN, lm_head: modeling_wav2vec2.py Wav2Vec2Attention,
+ *   Wav2Vec2FeedForward; src/model/w2v_custom_feat_extractor.py:152;
+ *   src/util/nn_helper.py:31-49 create_fully_connected),
+ *   einsum("btd,bdk->btk") day layer (src/model/b2p2t_model.py:155-158, via gather1 = day_idxs),
+ *   nn.Unfold + GRU input projection (src/model/b2p2t_model.py:162-167 +
+ *   src/model/brain_feature_extractor.py:39-47, via the implicit conv view),
+ *   grouped positional Conv1d (modeling_wav2vec2.py Wav2Vec2PositionalConvEmbedding, implicit
+ *   conv view), attention QK^T / PV (eager_attention_forward).
+ */
+typedef struct {
+  const float* ptr;
+  int64_t ld;            /* elements between consecutive outer indices                 */
+  int64_t bs1, bs2;      /* batch strides for z1 = z / nz2 and z2 = z % nz2            */
+  const int64_t* gather1;/* optional: offset uses gather1[z1] * bs1 instead of z1*bs1  */
+  int32_t inner_is_k;    /* 1: the contiguous dimension is the reduction dimension     */
+  int32_t conv;          /* 1: implicit conv1d view (below)                           */
+  /* implicit conv1d view: logical element (r, j) with r = b*conv_T_out + t and
+   * j = tap*conv_Cg + ch maps to src[b*conv_sample_stride + (t*conv_stride + tap - conv_pad)*ld + ch],
+   * zero when the frame index falls outside [0, conv_T_in). */
+  int32_t conv_T_out, conv_T_in, conv_stride, conv_pad, conv_Cg, _pad0;
+  int64_t conv_sample_stride;
+} b2p_operand;
+
+enum { B2P_ACT_NONE = 0, B2P_ACT_GELU = 1, B2P_ACT_SOFTSIGN = 2, B2P_ACT_SILU = 3 };
+
+typedef struct {
+  float* C;
+  int64_t ldc, cbs1, cbs2;
+  float alpha, beta;          /* beta != 0: C = alpha*acc + beta*C_old                        */
+  const float* bias;          /* [N] added after alpha/beta, or NULL                          */
+  int64_t biasbs1;            /* bias offset per z1 (grouped GEMMs)                           */
+  const int64_t* bias_gather; /* optional: bias offset = bias_gather[z1] * biasbs1 (day bias)  */
+  float* pre_out;             /* optional: store the pre-activation value (layout of C)       */
+  int32_t act;                /* B2P_ACT_* applied after bias                                  */
+  int32_t act_bwd;            /* B2P_ACT_*: multiply by act'(aux) after dropout (backward)     */
+  const float* aux;           /* pre-activation for act_bwd                                    */
+  int64_t ldaux, abs1, abs2;
+  float drop_p;               /* dropout probability (0 = off); mask = f(drop_seed, index)     */
+  int32_t _pad0;
+  uint64_t drop_seed;
+  const float* residual;      /* optional: added last                                          */
+  int64_t ldr, rbs1, rbs2;
+} b2p_epilogue;
+
+typedef struct {
+  int64_t M, N, K;
+  int32_t nz1, nz2;
+  b2p_operand A, B;
+  b2p_epilogue ep;
+  int32_t precision;          /* 0 = bf16 MFMA, 1 = fp32 MFMA (parity mode)                   */
+  int32_t timing_family;      /* tag for b2p_timing_* (0 = untagged)                          */
+  double flops;               /* algorithmic FLOPs of this launch (for timing)                */
+} b2p_gemm_desc;
+
+int b2p_gemm(const b2p_gemm_desc* d, b2p_stream_t stream);
+
+/* ------------------------------------------------------------------ elementwise / reductions */
+/* column sums over rows: out[n] (+)= sum_m X[m*ld + n]; used for bias grads. partial must hold
+ * ceil(M/rows_per_block)*N floats (see b2p_colsum_workspace). */
+int64_t b2p_colsum_workspace(int64_t M, int64_t N);
+int b2p_colsum(const float* X, int64_t M, int64_t N, int64_t ld, float* out, int accumulate,
+               float* partial, b2p_stream_t stream);
+/* batched variant: out[b][n] (+)= sum_m f(X[b*bstride + m*ld + n]); mode 0: x, 1: x^2, 2: x*Y */
+int b2p_colsum_batched(const float* X, const float* Y, int64_t batch, int64_t M, int64_t N, int64_t ld,
+                       int64_t bstride, int mode, float* out, int accumulate, float* partial,
+                       b2p_stream_t stream);
+
+/* dropout (forward and backward use the same mask): y = x * keep(seed, i) / (1-p) */
+int b2p_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, b2p_stream_t stream);
+
+/* LayerNorm over the last dim (transformers Wav2Vec2EncoderLayer.layer_norm / final_layer_norm,
+ * Wav2Vec2Encoder.layer_norm; eps 1e-5). mean/rstd saved for backward. */
+int b2p_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y,
+                      float* mean, float* rstd, int64_t rows, int64_t cols, float eps,
+                      float drop_p, uint64_t drop_seed, b2p_stream_t stream);
+int64_t b2p_layernorm_bwd_workspace(int64_t rows, int64_t cols);
+/* dy is the gradient of the (optionally dropped-out, drop_p/drop_seed) LN output; dx (+)= dx_accum.
+ * If dx_dropped != NULL it also receives dx * mask(in_drop_seed)/(1-in_drop_p): the gradient of
+ * the residual-branch dropout whose output fed this LayerNorm (post-LN encoder layers). */
+int b2p_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
+                      const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                      int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
+                      float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* workspace,
+                      b2p_stream_t stream);
+
+/* Row softmax for attention scores (eager_attention_forward: softmax(QK^T*scale) + dropout).
+ * S rows of length n (row stride ld). Writes P (pre-dropout) and Pd (dropped, scaled). */
+int b2p_softmax_fwd(const float* S, float* P, float* Pd, int64_t rows, int64_t n, int64_t ld,
+                    float drop_p, uint64_t drop_seed, b2p_stream_t stream);
+/* dS = P * (dPd*mask - rowsum(P * dPd*mask)) */
+int b2p_softmax_bwd(const float* P, const float* dPd, float* dS, int64_t rows, int64_t n,
+                    int64_t ld, float drop_p, uint64_t drop_seed, b2p_stream_t stream);
+
+/* elementwise activation backward: dx = dy * act'(pre) (optionally after dropout of dy) */
+int b2p_act_bwd(const float* dy, const float* pre, float* dx, int64_t n, int act,
+                b2p_stream_t stream);
+
+/* ------------------------------------------------------------------ front-end
+ * GaussianSmoothing (src/model/b2p2t_model.py:27-90): depthwise conv1d over time, taps[ntaps],
+ * padding "same" (left (ntaps-1)/2, right ntaps/2) on x (B, L, C) channels-last. */
+int b2p_gauss_smooth(const float* x, const float* taps, int ntaps, float* y, int64_t B,
+                     int64_t L, int64_t C, b2p_stream_t stream);
+/* col2im for Unfold((k,1), stride s) (src/model/b2p2t_model.py:108-113, 162-167) in tap-major
+ * order: dX[b,l,c] = sum_{tap} dA[b, (l-tap)/s, tap*C + c], then (optionally) multiplied by
+ * softsign'(Z[b,l,c]) (src/model/b2p2t_model.py:159). */
+int b2p_unfold_col2im(const float* dA, const float* Z, float* dX, int64_t B, int64_t L,
+                      int64_t C, int64_t T, int ktaps, int stride, b2p_stream_t stream);
+/* day-weight gradient reduction: dW[d] = sum_{b: day[b]==d} dWb[b] (deterministic) */
+int b2p_day_reduce(const float* per_sample, const int64_t* day_idx, int64_t B, int64_t ndays,
+                   int64_t elems, float* out, b2p_stream_t stream);
+
+/* ------------------------------------------------------------------ layout transforms */
+/* out[o][tap*I + i] = in[o][i*ntaps + tap]   (conv weight (O, I, taps) -> tap-major GEMM B)
+ * inverse=1 does the opposite mapping; flip=1 reads tap (ntaps-1-tap). */
+int b2p_conv_weight_permute(const float* in, float* out, int64_t O, int64_t I, int64_t ntaps,
+                            int inverse, b2p_stream_t stream);
+/* grouped conv-transpose weight: out[g][i][k'*Og + o] = w[(g*Og+o)][i][ntaps-1-k'] and inverse */
+int b2p_conv_weight_transpose_flip(const float* w, float* out, int64_t G, int64_t Og, int64_t I,
+                                   int64_t ntaps, b2p_stream_t stream);
+
+/* weight norm over all dims but dim=2 (torch.nn.utils.parametrizations.weight_norm(dim=2),
+ * transformers Wav2Vec2PositionalConvEmbedding): w[o,i,k] = g[k] * v[o,i,k] / ||v[:,:,k]|| */
+int64_t b2p_weight_norm_workspace(int64_t O, int64_t I, int64_t K);
+int b2p_weight_norm_fwd(const float* g, const float* v, float* w, float* norms, int64_t O,
+                        int64_t I, int64_t K, float* workspace, b2p_stream_t stream);
+int b2p_weight_norm_bwd(const float* g, const float* v, const float* norms, const float* dw,
+                        float* dg, float* dv, int64_t O, int64_t I, int64_t K, float* workspace,
+                        b2p_stream_t stream);
+
+/* ------------------------------------------------------------------ GRU recurrence
+ * nn.GRU (src/model/brain_feature_extractor.py:39-47, 56-68), PyTorch gate order (r,z,n),
+ * bidirectional, batch_first, h0 = 0 (or h0 given). gi = x W_ih^T + b_ih precomputed by
+ * b2p_gemm for both directions: gi[b][t][dir*3H + g*H + j]. whh: [2][3H][H], bhh: [2][3H].
+ * Outputs: out[b][t][dir*H + j]; saved gates for backward: rzn [B][T][2][4][H]
+ * (r, z, n, W_hn h + b_hn). */
+int b2p_gru_fwd(const float* gi, const float* whh, const float* bhh, const float* h0,
+                float* out, float* saved, int64_t B, int64_t T, int64_t H, int ndir,
+                b2p_stream_t stream);
+/* BPTT: dout [B][T][ndir*H] -> dgi [B][T][ndir*3H] (= dgh except the n-gate, also returned in
+ * dgh [B][T][ndir*3H]) and, if dh0 != NULL, dh0 [ndir][B][H]. dhbuf: ndir*B*H floats scratch.
+ * Weight grads are GEMMs on (dgh, h_prev), bias grads column sums. */
+int b2p_gru_bwd(const float* dout, const float* whh, const float* out, const float* saved,
+                const float* h0, float* dgi, float* dgh, float* dh0, float* dhbuf, int64_t B,
+                int64_t T, int64_t H, int ndir, b2p_stream_t stream);
+/* h_prev sequence for the weight-gradient GEMM: hp[dir][b][t][j] = h_{t-1} in that direction's
+ * processing order (h0 at the first step). */
+int b2p_gru_hprev(const float* out, const float* h0, float* hp, int64_t B, int64_t T, int64_t H,
+                  int ndir, b2p_stream_t stream);
+
+/* ------------------------------------------------------------------ CTC
+ * log_softmax + nn.CTCLoss(blank=0, reduction="mean", zero_infinity=True)
+ * (src/model/w2v_custom_feat_extractor.py:59, 81-90). logits (B, T, C) batch-first; targets
+ * (B, S) int64 (entries beyond target_len ignored); in_lens int32 (B), tgt_lens int64 (B).
+ * Writes per-sample nll (B; +inf when infeasible), the mean loss (1; infeasible samples count
+ * as 0 = zero_infinity), and grad_logits (B, T, C) = d(mean loss)/d(logits) (zero for
+ * t >= in_len and for infeasible samples). Workspace: b2p_ctc_workspace floats. */
+int64_t b2p_ctc_workspace(int64_t B, int64_t T, int64_t S, int64_t C);
+int b2p_ctc_fwd_bwd(const float* logits, const int64_t* targets, const int32_t* in_lens,
+                    const int64_t* tgt_lens, int64_t B, int64_t T, int64_t S, int64_t C,
+                    int blank, float* nll, float* loss, float* grad_logits, float* workspace,
+                    b2p_stream_t stream);
+
+/* ------------------------------------------------------------------ Adam
+ * torch.optim.Adam (src/experiments/experiment.py:25-28, b2t_gru_w2v_experiment.py:138-145):
+ * L2 weight decay, bias correction, eps outside the sqrt. Multi-tensor: `table` is a device
+ * array of ntensors records {param*, grad*, exp_avg*, exp_avg_sq*, numel} (5 x int64). */
+int b2p_adam_multi(const int64_t* table, int ntensors, int64_t max_numel, float lr, float beta1,
+                   float beta2, float eps, float weight_decay, float bias_c1, float bias_c2_sqrt,
+                   b2p_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* B2P_HIP_H */

@@ -1,0 +1,44 @@
+"""Fixture configurations shared by make_golden.py (reference side) and the tests (build side)."""
+from __future__ import annotations
+
+import torch
+
+CONFIGS = [
+    # tiny: every code path, full gradients stored
+    dict(name="tiny_a", seed=42, B=3, L=96, in_lens=[96, 80, 64], tgt_range=(2, 8), hidden_size=64, layers=2,
+         heads=4, ffn=128, pos_k=16, pos_groups=4, gru_hidden=32, gru_layers=2, bidirectional=True, fc_hidden=[],
+         learnable_h0=False, full_grad_max=65536, infeasible=False),
+    # tiny variant: 3 GRU layers, fc hidden + GELU, learnable h0, one infeasible sample (zero_infinity)
+    dict(name="tiny_b", seed=43, B=2, L=128, in_lens=[128, 128], tgt_range=(3, 9), hidden_size=48, layers=1,
+         heads=3, ffn=96, pos_k=8, pos_groups=2, gru_hidden=16, gru_layers=3, bidirectional=True, fc_hidden=[40],
+         learnable_h0=True, full_grad_max=65536, infeasible=True),
+    # config (1) of BASELINE.json: wav2vec2-base architecture, bs=2, 512-step windows (plumbing case)
+    dict(name="plumbing_base", seed=42, B=2, L=512, in_lens=[512, 384], tgt_range=(20, 50), hidden_size=768,
+         layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2, bidirectional=True,
+         fc_hidden=[], learnable_h0=False, full_grad_max=4096, infeasible=False),
+]
+
+
+def make_batch(cfg):
+    """Synthetic inputs: x ~ N(0,1) (B,L,256); day ~ U{0..23}; targets ~ U{4..31}
+    padded with 0; data seed 0."""
+    g = torch.Generator().manual_seed(0)
+    B, L = cfg["B"], cfg["L"]
+    x = torch.randn(B, L, 256, generator=g)
+    for b, il in enumerate(cfg["in_lens"]):
+        x[b, il:] = 0.0   # zero-padded tail like the collate function
+    day = torch.randint(0, 24, (B,), generator=g)
+    lo, hi = cfg["tgt_range"]
+    tl = torch.randint(lo, hi + 1, (B,), generator=g)
+    S = int(tl.max())
+    tgt = torch.zeros(B, S, dtype=torch.int64)
+    for b in range(B):
+        tgt[b, :tl[b]] = torch.randint(4, 32, (int(tl[b]),), generator=g)
+    if cfg.get("infeasible"):
+        # sample 0: more labels (all equal -> needs 2 frames each) than logit frames
+        T = (cfg["in_lens"][0] - 32) // 4
+        n = min(S, T // 2 + 2)
+        tgt[0, :n] = 7
+        tl[0] = n
+    in_lens = torch.tensor(cfg["in_lens"], dtype=torch.int64)
+    return x, day, in_lens, tgt, tl.to(torch.int64)

@@ -1,0 +1,114 @@
+"""Generates the golden fixtures tests/golden/*.npz by running THE REFERENCE's own model modules
+(/root/reference/src/model/*) on CPU, fp32, deterministic mode (all dropout 0, LayerDrop 0).
+
+Runs only in the build container (it reads /root/reference; never on the GPU box). Stubs, as in
+SURVEY.md 8(c3): torch .cuda() -> identity; Wav2Vec2Config.from_pretrained(<hub name>) -> an
+explicit local config; attention implementation "eager" (transformers 4.35.2 semantics).
+Weights come from wav2vec2forbrain_amd.util.init (deterministic by name), so the fixtures store
+inputs, outputs and gradients, not weights.
+
+usage: python tests/golden/make_golden.py   (from the repo root)
+"""
+from __future__ import annotations
+
+import os
+import sys
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+REF = "/root/reference"
+OUT = os.path.join(REPO, "tests", "golden")
+sys.path.insert(0, REPO)
+from wav2vec2forbrain_amd.util.init import deterministic_state  # noqa: E402
+from tests.golden.configs import CONFIGS, make_batch  # noqa: E402
+
+
+def _import_reference():
+    sys.path.insert(0, REF)
+    sys.dont_write_bytecode = True
+    torch.nn.Module.cuda = lambda self, *a, **k: self
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    import transformers.models.wav2vec2.modeling_wav2vec2 as tfw
+    from src.model import brain_feature_extractor as bfe
+    from src.model import w2v_custom_feat_extractor as w2v
+    from src.args import base_args
+    return tfw, bfe, w2v, base_args
+
+
+def build_reference_model(cfg, tfw, bfe, w2v, base_args):
+    name = "golden/" + cfg["name"]
+    base_args.PRETRAINED_LATENT_SIZES[name] = cfg["hidden_size"]
+    bfe.PRETRAINED_LATENT_SIZES[name] = cfg["hidden_size"]
+    hf = tfw.Wav2Vec2Config(
+        hidden_size=cfg["hidden_size"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"],
+        intermediate_size=cfg["ffn"], hidden_act="gelu", hidden_dropout=0.0, activation_dropout=0.0,
+        attention_dropout=0.0, feat_proj_dropout=0.0, final_dropout=0.0, layerdrop=0.0,
+        num_conv_pos_embeddings=cfg["pos_k"], num_conv_pos_embedding_groups=cfg["pos_groups"], vocab_size=32,
+        do_stable_layer_norm=False)
+    hf._attn_implementation = "eager"
+
+    def fake_from_pretrained(ckpt, **kw):
+        c = tfw.Wav2Vec2Config.from_dict(hf.to_dict())
+        for k, v in kw.items():
+            setattr(c, k, v)
+        c._attn_implementation = "eager"
+        return c
+
+    w2v.Wav2Vec2Config.from_pretrained = staticmethod(fake_from_pretrained)
+    args = bfe.B2P2TBrainFeatureExtractorArgsModel(
+        encoder_gru_hidden_size=cfg["gru_hidden"], encoder_num_gru_layers=cfg["gru_layers"],
+        encoder_bidirectional=cfg["bidirectional"], encoder_fc_hidden_sizes=cfg["fc_hidden"],
+        encoder_learnable_inital_state=cfg["learnable_h0"])
+    brain = bfe.bfe_w_preprocessing_from_config(args, None, name)
+    model = w2v.W2VBrainEncoderModel(w2v.W2VBrainEncoderModelArgs(), brain, name, None, True)
+    return model
+
+
+def run(cfg, modules):
+    tfw, bfe, w2v, base_args = modules
+    torch.manual_seed(0)
+    model = build_reference_model(cfg, tfw, bfe, w2v, base_args)
+    sd = deterministic_state([(n, p.shape) for n, p in model.named_parameters()], seed=cfg["seed"])
+    missing, unexpected = model.load_state_dict(sd, strict=False)
+    assert not unexpected, unexpected
+    assert all(k.endswith("gaussian_smoother.weight") for k in missing), missing
+    model.train()   # deterministic: every dropout and layerdrop is 0
+    from src.datasets.batch_types import B2tSampleBatch
+    x, day, in_lens, tgt, tgt_lens = make_batch(cfg)
+    batch = B2tSampleBatch(x, tgt)
+    batch.day_idxs = day
+    batch.input_lens = in_lens
+    batch.target_lens = tgt_lens
+    out = model.forward(batch)
+    out.loss.backward()
+    res = {"loss": np.array(out.loss.item(), dtype=np.float64),
+           "logits": out.logits.detach().numpy(),
+           "logit_lens": out.logit_lens.numpy(),
+           "x": x.numpy(), "day_idxs": day.numpy(), "input_lens": in_lens.numpy(), "target": tgt.numpy(),
+           "target_lens": tgt_lens.numpy()}
+    names = []
+    gen = torch.Generator().manual_seed(7)
+    for n, p in model.named_parameters():
+        g = p.grad if p.grad is not None else torch.zeros_like(p)
+        names.append(n)
+        res["gnorm/" + n] = np.array(g.double().norm().item())
+        flat = g.reshape(-1)
+        if flat.numel() <= cfg["full_grad_max"]:
+            res["grad/" + n] = g.numpy()
+        else:
+            idx = torch.randint(0, flat.numel(), (1024,), generator=gen)
+            res["gidx/" + n] = idx.numpy()
+            res["gval/" + n] = flat[idx].numpy()
+    res["param_names"] = np.array(names)
+    path = os.path.join(OUT, f"{cfg['name']}.npz")
+    np.savez_compressed(path, **res)
+    print(f"{path}: loss={out.loss.item():.6f}  ({os.path.getsize(path)/1e6:.2f} MB)")
+
+
+if __name__ == "__main__":
+    mods = _import_reference()
+    torch.set_num_threads(8)
+    for c in CONFIGS:
+        run(c, mods)

@@ -1,0 +1,56 @@
+"""C-ABI boundary checks (CPU): the library builds/loads and exports every entry point that
+include/b2p_hip.h declares; the ctypes binding covers the same set; argument validation errors
+surface as RuntimeError without touching a device."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    src = open(os.path.join(ROOT, "include", "b2p_hip.h")).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(b2p_[a-z0-9_]+)\s*\(", src)))
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert "b2p_gemm" in names and "b2p_ctc_fwd_bwd" in names and "b2p_gru_fwd" in names
+    assert len(names) >= 25
+
+
+def test_library_exports_every_declared_symbol():
+    from wav2vec2forbrain_amd import _lib
+    lib = _lib.load()
+    missing = [n for n in _declared() if not hasattr(lib, n)]
+    assert not missing, missing
+
+
+def test_binding_covers_header():
+    from wav2vec2forbrain_amd import _lib
+    assert sorted(_lib.exported_symbols()) == _declared()
+
+
+def test_struct_layout_matches_c():
+    from wav2vec2forbrain_amd import _lib
+    # sizes fixed by the C structs (include/b2p_hip.h), x86-64 SysV alignment
+    assert ctypes.sizeof(_lib.Operand) == 8 * 5 + 4 * 8 + 8
+    assert ctypes.sizeof(_lib.GemmDesc) == 3 * 8 + 8 + 2 * ctypes.sizeof(_lib.Operand) + \
+        ctypes.sizeof(_lib.Epilogue) + 8 + 8
+
+
+def test_argument_validation_without_device():
+    from wav2vec2forbrain_amd import _lib
+    lib = _lib.load()
+    assert lib.b2p_version() >= 1
+    d = _lib.GemmDesc()
+    d.M, d.N, d.K, d.nz1, d.nz2 = 4, 4, 4, 1, 1
+    rc = lib.b2p_gemm(ctypes.byref(d), None)          # NULL operands -> error, no launch
+    assert rc != 0
+    assert b"NULL" in lib.b2p_last_error()
+    with pytest.raises(RuntimeError):
+        _lib.call("b2p_dropout", None, None, 10, 0.5, 1, None)
+    assert lib.b2p_ctc_workspace(2, 10, 3, 32) == 2 * (10 * 32 + 2 * 10 * 7)

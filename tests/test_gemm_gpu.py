@@ -1,0 +1,177 @@
+"""GEMM kernel (b2p_gemm) against plain PyTorch fp32 references: layouts, tails, batching,
+implicit conv/unfold views, epilogues, both MFMA precisions."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+TOL = {"fp32": (2e-5, 2e-5), "bf16": (2e-2, 2e-2)}
+
+
+def _fn():
+    from wav2vec2forbrain_amd import functional as Fn
+    return Fn
+
+
+def _close(out, ref, mode, scale=None):
+    rtol, atol = TOL[mode]
+    scale = scale if scale is not None else ref.abs().max().item() + 1e-6
+    err = (out - ref).abs().max().item()
+    assert err <= atol * scale + rtol * 0, f"max err {err} vs scale {scale} ({mode})"
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (130, 70, 37), (1, 33, 5), (300, 257, 96), (64, 48, 6144)])
+def test_nt_nn_tn(mode, M, N, K):
+    Fn = _fn()
+    torch.manual_seed(0)
+    Kp = (K + 3) // 4 * 4
+    Np = (N + 3) // 4 * 4
+    Mp = (M + 3) // 4 * 4
+    a = torch.randn(M, Kp, device="cuda")
+    w = torch.randn(N, Kp, device="cuda")
+    with Fn.precision(mode):
+        # NT: out = a[:, :K] @ w[:, :K]^T
+        out = torch.empty(M, Np, device="cuda")
+        Fn.gemm(M, N, K, Fn.op(a, 0, Kp, True), Fn.op(w, 0, Kp, True), out, Np)
+        _close(out[:, :N], a[:, :K] @ w[:, :K].t(), mode)
+        # NN: out = a[:, :K] @ b (b: K x N, row-major, ld Np)
+        b = torch.randn(K, Np, device="cuda")
+        out2 = torch.empty(M, Np, device="cuda")
+        Fn.gemm(M, N, K, Fn.op(a, 0, Kp, True), Fn.op(b, 0, Np, False), out2, Np)
+        _close(out2[:, :N], a[:, :K] @ b[:, :N], mode)
+        # TN: out = at^T @ b with at: K x M (ld Mp)
+        at = torch.randn(K, Mp, device="cuda")
+        out3 = torch.empty(M, Np, device="cuda")
+        Fn.gemm(M, N, K, Fn.op(at, 0, Mp, False), Fn.op(b, 0, Np, False), out3, Np)
+        _close(out3[:, :N], at[:, :M].t() @ b[:, :N], mode)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_epilogue(mode):
+    Fn = _fn()
+    torch.manual_seed(1)
+    M, N, K = 200, 96, 64
+    x = torch.randn(M, K, device="cuda")
+    w = torch.randn(N, K, device="cuda") / 8
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda")
+    with Fn.precision(mode):
+        out = torch.empty(M, N, device="cuda")
+        pre = torch.empty(M, N, device="cuda")
+        Fn.mm_nt(x, w, out, bias=bias, act=Fn.ACT["gelu"], pre_out=pre, residual=res)
+        ref_pre = x @ w.t() + bias
+        _close(pre, ref_pre, mode)
+        _close(out, F.gelu(ref_pre) + res, mode, scale=ref_pre.abs().max().item())
+        # beta accumulate + alpha
+        c = torch.randn(M, N, device="cuda")
+        c0 = c.clone()
+        Fn.gemm(M, N, K, Fn.op(x, 0, K, True), Fn.op(w, 0, K, True), c, N, alpha=0.5, beta=2.0)
+        _close(c, 0.5 * (x @ w.t()) + 2.0 * c0, mode, scale=ref_pre.abs().max().item() * 2)
+        # act_bwd: out = acc * gelu'(aux)
+        g = torch.empty(M, N, device="cuda")
+        Fn.gemm(M, N, K, Fn.op(x, 0, K, True), Fn.op(w, 0, K, True), g, N, act_bwd=Fn.ACT["gelu"], aux=ref_pre)
+        pr = ref_pre.clone().requires_grad_(True)
+        (gg,) = torch.autograd.grad(F.gelu(pr), pr, x @ w.t())
+        _close(g, gg, mode, scale=ref_pre.abs().max().item())
+
+
+def test_dropout_epilogue_mask_consistent():
+    Fn = _fn()
+    M, N, K = 256, 128, 32
+    x = torch.randn(M, K, device="cuda")
+    w = torch.randn(N, K, device="cuda")
+    with Fn.precision("fp32"):
+        out = torch.empty(M, N, device="cuda")
+        Fn.gemm(M, N, K, Fn.op(x, 0, K, True), Fn.op(w, 0, K, True), out, N, drop_p=0.25, seed=1234)
+        ref = x @ w.t()
+        kept = out != 0
+        frac = kept.float().mean().item()
+        assert 0.72 < frac < 0.78
+        torch.testing.assert_close(out[kept], ref[kept] / 0.75, rtol=1e-4, atol=1e-4)
+        # same (seed, index) mask from the elementwise dropout kernel
+        y = Fn._dropout_raw(torch.ones(M, N, device="cuda"), 0.25, 1234)
+        assert torch.equal(y != 0, kept)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_batched_attention_layout(mode):
+    Fn = _fn()
+    torch.manual_seed(2)
+    B, T, nh, dh = 3, 37, 4, 16
+    D = nh * dh
+    Tp = (T + 3) // 4 * 4
+    qkv = torch.randn(B * T, 3 * D, device="cuda")
+    S = torch.zeros(B, nh, T, Tp, device="cuda")
+    with Fn.precision(mode):
+        Fn.gemm(T, T, dh, Fn.op(qkv, 0, 3 * D, True, bs1=T * 3 * D, bs2=dh),
+                Fn.op(qkv, D, 3 * D, True, bs1=T * 3 * D, bs2=dh), S, Tp, cbs1=nh * T * Tp, cbs2=T * Tp, nz1=B,
+                nz2=nh, alpha=0.25)
+    q = qkv.view(B, T, 3, nh, dh)[:, :, 0].transpose(1, 2)
+    k = qkv.view(B, T, 3, nh, dh)[:, :, 1].transpose(1, 2)
+    _close(S[..., :T], 0.25 * q @ k.transpose(-1, -2), mode)
+
+
+def test_gather_batch_and_bias():
+    """day-linear: per-sample B operand and bias selected through day_idxs."""
+    Fn = _fn()
+    torch.manual_seed(3)
+    B, L, C, nd = 4, 40, 32, 6
+    xs = torch.randn(B, L, C, device="cuda")
+    W = torch.randn(nd, C, C, device="cuda")
+    bias = torch.randn(nd, 1, C, device="cuda")
+    day = torch.tensor([5, 0, 5, 2], device="cuda")
+    out = torch.empty(B, L, C, device="cuda")
+    with Fn.precision("fp32"):
+        Fn.gemm(L, C, C, Fn.op(xs, 0, C, True, bs1=L * C), Fn.op(W, 0, C, False, bs1=C * C, gather=day), out, C,
+                cbs1=L * C, nz1=B, bias=bias, biasbs1=C, bias_gather=day)
+    ref = torch.einsum("btd,bdk->btk", xs, W[day]) + bias[day]
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_implicit_unfold_views(mode):
+    """nn.Unfold((k,1), stride) + projection as one implicit GEMM, and its transposed use (dW)."""
+    Fn = _fn()
+    from oracle.b2p2t_oracle import unfold
+    torch.manual_seed(4)
+    B, L, C, k, s, N = 3, 72, 16, 8, 4, 40
+    T = (L - k) // s + 1
+    x = torch.randn(B, L, C, device="cuda")
+    w = torch.randn(N, C * k, device="cuda")            # reference layout: col = c*k + tap
+    u = unfold(x.cpu(), k, s).cuda()                     # (B, T, C*k)
+    wp = torch.empty(N, k * C, device="cuda")
+    Fn._lib.call("b2p_conv_weight_permute", w.data_ptr(), wp.data_ptr(), N, C, k, 0, Fn._st())
+    with Fn.precision(mode):
+        out = torch.empty(B * T, N, device="cuda")
+        A = Fn.conv_op(x, 0, C, T, L, s, 0, C, L * C, True)
+        Fn.gemm(B * T, N, k * C, A, Fn.op(wp, 0, k * C, True), out, N)
+        _close(out, (u.view(B * T, -1) @ w.t()), mode)
+        # dW' = dy^T @ unfold(x) (conv view as B operand, inner = n)
+        dy = torch.randn(B * T, N, device="cuda")
+        dwp = torch.empty(N, k * C, device="cuda")
+        Bop = Fn.conv_op(x, 0, C, T, L, s, 0, C, L * C, False)
+        Fn.gemm(N, k * C, B * T, Fn.op(dy, 0, N, False), Bop, dwp, k * C)
+        dw = torch.empty(N, C * k, device="cuda")
+        Fn._lib.call("b2p_conv_weight_permute", dwp.data_ptr(), dw.data_ptr(), N, C, k, 1, Fn._st())
+        _close(dw, dy.t() @ u.view(B * T, -1), mode)
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_grouped_conv_view(mode):
+    """positional conv: Conv1d(D, D, K, padding=K//2, groups=G) minus last frame as a grouped implicit GEMM."""
+    Fn = _fn()
+    torch.manual_seed(5)
+    B, T, D, G, K = 2, 33, 32, 4, 8
+    Og = Ig = D // G
+    x = torch.randn(B, T, D, device="cuda")
+    w = torch.randn(D, Ig, K, device="cuda") / 8
+    wp = torch.empty(D, K * Ig, device="cuda")
+    Fn._lib.call("b2p_conv_weight_permute", w.data_ptr(), wp.data_ptr(), D, Ig, K, 0, Fn._st())
+    ref = F.conv1d(x.transpose(1, 2), w, padding=K // 2, groups=G)[:, :, :-1].transpose(1, 2)
+    with Fn.precision(mode):
+        out = torch.empty(B, T, D, device="cuda")
+        A = Fn.conv_op(x, 0, D, T, T, 1, K // 2, Ig, T * D, True, bs1=Ig)
+        Fn.gemm(B * T, Og, K * Ig, A, Fn.op(wp, 0, K * Ig, True, bs1=Og * K * Ig), out, D, cbs1=Og, nz1=G)
+        _close(out, ref, mode)

@@ -1,0 +1,263 @@
+"""Per-operator parity of the HIP path (functional.*) against the CPU oracle / PyTorch fp32,
+forward and backward, at sizes the oracle finishes in seconds."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _fn():
+    from wav2vec2forbrain_amd import functional as Fn
+    return Fn
+
+
+def _rel(a, b):
+    return (a - b).abs().max().item() / (b.abs().max().item() + 1e-12)
+
+
+def test_layernorm_fwd_bwd():
+    Fn = _fn()
+    torch.manual_seed(0)
+    for cols in (64, 768, 1024):
+        x = torch.randn(37, cols, device="cuda") * 3 + 1
+        g = torch.randn(cols, device="cuda")
+        b = torch.randn(cols, device="cuda")
+        y, mean, rstd = Fn._ln_fwd(x, g, b, 1e-5)
+        xr = x.detach().clone().requires_grad_(True)
+        gr = g.clone().requires_grad_(True)
+        br = b.clone().requires_grad_(True)
+        yr = F.layer_norm(xr, (cols,), gr, br, 1e-5)
+        assert _rel(y, yr) < 1e-5
+        dy = torch.randn_like(y)
+        dx, dg, db, _ = Fn._ln_bwd(dy, x, g, mean, rstd)
+        gx, gg, gb = torch.autograd.grad(yr, (xr, gr, br), dy)
+        assert _rel(dx, gx) < 1e-4 and _rel(dg, gg) < 1e-4 and _rel(db, gb) < 1e-4
+
+
+def test_softmax_fwd_bwd_with_dropout():
+    Fn = _fn()
+    torch.manual_seed(1)
+    rows, n, ld = 50, 249, 252
+    S = torch.randn(rows, ld, device="cuda") * 3
+    P = torch.empty_like(S)
+    Pd = torch.empty_like(S)
+    Fn._lib.call("b2p_softmax_fwd", S.data_ptr(), P.data_ptr(), Pd.data_ptr(), rows, n, ld, 0.1, 77, Fn._st())
+    ref = torch.softmax(S[:, :n], -1)
+    assert _rel(P[:, :n], ref) < 1e-5
+    keep = Pd[:, :n] != 0
+    torch.testing.assert_close(Pd[:, :n][keep], ref[keep] / 0.9, rtol=1e-5, atol=1e-7)
+    dPd = torch.randn(rows, ld, device="cuda")
+    dS = torch.empty_like(S)
+    Fn._lib.call("b2p_softmax_bwd", P.data_ptr(), dPd.data_ptr(), dS.data_ptr(), rows, n, ld, 0.1, 77, Fn._st())
+    sr = S[:, :n].clone().requires_grad_(True)
+    pr = torch.softmax(sr, -1) * keep.float() / 0.9
+    (g,) = torch.autograd.grad(pr, sr, dPd[:, :n])
+    assert _rel(dS[:, :n], g) < 1e-4
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_ctc_vs_torch(seed):
+    Fn = _fn()
+    torch.manual_seed(seed)
+    B, T, C, S = 5, 60, 32, 20
+    logits = torch.randn(B, T, C, device="cuda") * 2
+    tl = torch.randint(0, S + 1, (B,))
+    tgt = torch.randint(1, C, (B, S))
+    il = torch.randint(T // 2, T + 1, (B,)).to(torch.int32)
+    if seed == 2:
+        tl[0], il[0] = 20, 10        # infeasible -> zero_infinity
+        tgt[1, :] = 5                 # repeated labels
+    loss = Fn.ctc_loss(logits, tgt.cuda(), il.cuda(), tl.cuda())
+    lr = logits.detach().cpu().double().requires_grad_(True)
+    ref = F.ctc_loss(lr.log_softmax(-1).transpose(0, 1), tgt, il.long(), tl, blank=0, reduction="mean",
+                     zero_infinity=True)
+    (g,) = torch.autograd.grad(ref, lr)
+    assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item()) + 1e-6
+    lg = logits.clone().requires_grad_(True)
+    Fn.ctc_loss(lg, tgt.cuda(), il.cuda(), tl.cuda()).backward()
+    assert _rel(lg.grad.cpu().double(), g) < 1e-4
+
+
+@pytest.mark.parametrize("unfold", [False, True])
+@pytest.mark.parametrize("h0", [False, True])
+def test_gru_layer(unfold, h0):
+    Fn = _fn()
+    from oracle.b2p2t_oracle import gru_direction, unfold as unfold_ref
+    torch.manual_seed(3)
+    B, H = 5, 32
+    if unfold:
+        L, C, k, s = 60, 16, 8, 4
+        xsrc = torch.randn(B, L, C)
+        x_ref = unfold_ref(xsrc, k, s)
+        x_in = Fn.Unfolded(xsrc.cuda(), k, s)
+    else:
+        T, IN = 23, 48
+        xsrc = torch.randn(B, T, IN)
+        x_ref = xsrc
+        x_in = xsrc.cuda()
+    IN = x_ref.shape[-1]
+    ws = []
+    for d in range(2):
+        ws += [torch.randn(3 * H, IN) / math.sqrt(IN), torch.randn(3 * H, H) / math.sqrt(H), torch.randn(3 * H) * 0.1,
+               torch.randn(3 * H) * 0.1]
+    hz = torch.randn(2, B, H) if h0 else None
+    # reference
+    wr = [w.clone().requires_grad_(True) for w in ws]
+    xr = xsrc.clone().requires_grad_(True)
+    xin_ref = unfold_ref(xr, k, s) if unfold else xr
+    hr = hz.clone().requires_grad_(True) if h0 else None
+    outs = [gru_direction(xin_ref, *wr[4 * d:4 * d + 4], hr[d] if h0 else None, d == 1) for d in range(2)]
+    ref = torch.cat(outs, -1)
+    dout = torch.randn_like(ref)
+    refg = torch.autograd.grad(ref, [xr, *wr] + ([hr] if h0 else []), dout)
+    # HIP
+    with Fn.precision("fp32"):
+        wg = [w.cuda().requires_grad_(True) for w in ws]
+        if unfold:
+            xs = xsrc.cuda().requires_grad_(True)
+            x_in = Fn.Unfolded(xs, k, s)
+        else:
+            xs = xsrc.cuda().requires_grad_(True)
+            x_in = xs
+        hg = hz.cuda().requires_grad_(True) if h0 else None
+        out = Fn.gru_layer(x_in, H, 2, wg, hg)
+        assert _rel(out.cpu(), ref) < 1e-4
+        got = torch.autograd.grad(out, [xs, *wg] + ([hg] if h0 else []), dout.cuda())
+    for a, b in zip(got, refg):
+        assert _rel(a.cpu(), b) < 2e-4
+
+
+def test_front_end():
+    Fn = _fn()
+    from oracle.b2p2t_oracle import gaussian_taps, gaussian_smooth, day_linear_softsign
+    torch.manual_seed(4)
+    B, L, C = 3, 64, 256
+    x = torch.randn(B, L, C)
+    day = torch.tensor([3, 17, 3])
+    W = torch.eye(C).expand(24, C, C).clone() + 0.05 * torch.randn(24, C, C)
+    bias = 0.1 * torch.randn(24, 1, C)
+    for sigma in (0.3, 1.529):
+        taps = gaussian_taps(sigma)
+        Wr, br = W.clone().requires_grad_(True), bias.clone().requires_grad_(True)
+        ref = day_linear_softsign(gaussian_smooth(x, taps), day, Wr, br)
+        ds = torch.randn_like(ref)
+        gW, gb = torch.autograd.grad(ref, (Wr, br), ds)
+        with Fn.precision("fp32"):
+            Wg, bg = W.cuda().requires_grad_(True), bias.cuda().requires_grad_(True)
+            out = Fn.front_end(x.cuda(), day.cuda(), Wg, bg, taps.cuda())
+            assert _rel(out.cpu(), ref) < 1e-5
+            hW, hb = torch.autograd.grad(out, (Wg, bg), ds.cuda())
+        assert _rel(hW.cpu(), gW) < 1e-4 and _rel(hb.cpu(), gb) < 1e-4
+
+
+def test_pos_conv_ln():
+    Fn = _fn()
+    from oracle.b2p2t_oracle import pos_conv, layer_norm, OracleConfig
+    torch.manual_seed(5)
+    B, T, D, G, K = 2, 41, 64, 4, 16
+    cfg = OracleConfig(num_conv_pos_embeddings=K, num_conv_pos_embedding_groups=G)
+    e = torch.randn(B, T, D)
+    g = 1 + 0.1 * torch.randn(1, 1, K)
+    v = torch.randn(D, D // G, K)
+    cb = 0.05 * torch.randn(D)
+    lg, lb = 1 + 0.1 * torch.randn(D), 0.1 * torch.randn(D)
+    ts = [t.clone().requires_grad_(True) for t in (e, g, v, cb, lg, lb)]
+    sd = {"p.conv.parametrizations.weight.original0": ts[1], "p.conv.parametrizations.weight.original1": ts[2],
+          "p.conv.bias": ts[3]}
+    ref = layer_norm(ts[0] + pos_conv(ts[0], sd, "p.", cfg), ts[4], ts[5], 1e-5)
+    dy = torch.randn_like(ref)
+    refg = torch.autograd.grad(ref, ts, dy)
+    with Fn.precision("fp32"):
+        tg = [t.cuda().requires_grad_(True) for t in (e, g, v, cb, lg, lb)]
+        out = Fn.pos_conv_ln(*tg, G, 1e-5, 0.0, False)
+        assert _rel(out.cpu(), ref) < 1e-4
+        got = torch.autograd.grad(out, tg, dy.cuda())
+    for i, (a, b) in enumerate(zip(got, refg)):
+        assert _rel(a.cpu(), b) < 5e-4, i
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_encoder_layer(mode):
+    Fn = _fn()
+    from oracle.b2p2t_oracle import encoder_layer, OracleConfig
+    torch.manual_seed(6)
+    B, T, D, nh, Ff = 2, 45, 64, 4, 128
+    cfg = OracleConfig(hidden_size=D, num_attention_heads=nh, intermediate_size=Ff)
+    names = ["attention.q_proj.weight", "attention.q_proj.bias", "attention.k_proj.weight", "attention.k_proj.bias",
+             "attention.v_proj.weight", "attention.v_proj.bias", "attention.out_proj.weight", "attention.out_proj.bias",
+             "layer_norm.weight", "layer_norm.bias", "feed_forward.intermediate_dense.weight",
+             "feed_forward.intermediate_dense.bias", "feed_forward.output_dense.weight",
+             "feed_forward.output_dense.bias", "final_layer_norm.weight", "final_layer_norm.bias"]
+    shapes = [(D, D), (D,), (D, D), (D,), (D, D), (D,), (D, D), (D,), (D,), (D,), (Ff, D), (Ff,), (D, Ff), (D,), (D,), (D,)]
+    vals = []
+    for n, s in zip(names, shapes):
+        r = torch.randn(*s)
+        vals.append(1 + 0.1 * r if "norm.weight" in n else (0.05 * r if len(s) == 1 else r / math.sqrt(s[1])))
+    x = torch.randn(B, T, D)
+    pr = [v.clone().requires_grad_(True) for v in vals]
+    xr = x.clone().requires_grad_(True)
+    ref = encoder_layer(xr, {"l." + n: p for n, p in zip(names, pr)}, "l.", cfg, False)
+    dy = torch.randn_like(ref)
+    refg = torch.autograd.grad(ref, [xr] + pr, dy)
+    tol = 2e-4 if mode == "fp32" else 3e-2
+    with Fn.precision(mode):
+        pg = [v.cuda().requires_grad_(True) for v in vals]
+        xg = x.cuda().requires_grad_(True)
+        out = Fn.encoder_layer(xg, pg, nh, 1e-5, 0.0, 0.0, 0.0, False)
+        assert _rel(out.cpu(), ref) < tol
+        got = torch.autograd.grad(out, [xg] + pg, dy.cuda())
+    for i, (a, b) in enumerate(zip(got, refg)):
+        if i == 4:   # k_proj bias: gradient is mathematically zero (softmax shift invariance)
+            assert a.abs().max().item() < 1e-3 * refg[0].abs().max().item() + 1e-6
+            continue
+        assert _rel(a.cpu(), b) < tol * 5, (i, _rel(a.cpu(), b))
+
+
+def test_encoder_layer_dropout_train_mode():
+    """train-mode: outputs finite, dropout active, backward consistent with forward masks
+    (finite-difference check of the directional derivative)."""
+    Fn = _fn()
+    torch.manual_seed(7)
+    B, T, D, nh, Ff = 2, 20, 32, 2, 64
+    shapes = [(D, D), (D,), (D, D), (D,), (D, D), (D,), (D, D), (D,), (D,), (D,), (Ff, D), (Ff,), (D, Ff), (D,), (D,), (D,)]
+    ps = [(torch.randn(*s) / math.sqrt(s[-1])).cuda().double().float() for s in shapes]
+    ps[8] = torch.ones(D, device="cuda"); ps[14] = torch.ones(D, device="cuda")
+    x = torch.randn(B, T, D, device="cuda")
+    cfg_seeds = (11, 12, 13, 14)
+    cfg = (nh, 1e-5, 0.1, 0.1, 0.1, cfg_seeds)
+    with Fn.precision("fp32"):
+        xg = x.clone().requires_grad_(True)
+        out = Fn._EncoderLayer.apply(xg, cfg, *ps)
+        dy = torch.randn_like(out)
+        (gx,) = torch.autograd.grad(out, xg, dy)
+        d = torch.randn_like(x)
+        eps = 1e-2
+        fp = Fn._EncoderLayer.apply(x + eps * d, cfg, *ps)
+        fm = Fn._EncoderLayer.apply(x - eps * d, cfg, *ps)
+        fd = ((fp - fm) * dy).sum() / (2 * eps)
+        an = (gx * d).sum()
+    assert torch.isfinite(out).all()
+    assert abs(fd.item() - an.item()) <= 2e-2 * abs(an.item()) + 1e-3
+
+
+def test_adam_matches_torch():
+    from wav2vec2forbrain_amd.optim import HipAdam
+    torch.manual_seed(8)
+    shapes = [(300, 70), (5,), (24, 1, 256)]
+    ps1 = [torch.nn.Parameter(torch.randn(*s, device="cuda")) for s in shapes]
+    ps2 = [torch.nn.Parameter(p.detach().clone()) for p in ps1]
+    o1 = torch.optim.Adam(ps1, lr=1e-3, weight_decay=0.01, eps=1e-8)
+    o2 = HipAdam(ps2, lr=1e-3, weight_decay=0.01, eps=1e-8)
+    for step in range(5):
+        gs = [torch.randn_like(p) for p in ps1]
+        for p, g in zip(ps1, gs):
+            p.grad = g.clone()
+        for p, g in zip(ps2, gs):
+            p.grad = g.clone()
+        o1.step()
+        o2.step()
+    for a, b in zip(ps1, ps2):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)

@@ -1,0 +1,51 @@
+"""Pins the CPU oracle (oracle/b2p2t_oracle.py) against golden vectors produced by the reference's
+own modules (tests/golden/make_golden.py), plus the build's module tree against the reference
+state_dict (key names and shapes). CPU only."""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import CFG, load_fixture, oracle_cfg, oracle_state, batch_dict, build_model
+
+
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base"])
+def test_state_dict_keys_match_reference(name):
+    fx = load_fixture(name)
+    model = build_model(CFG[name], device="cpu")
+    ours = [n for n, _ in model.named_parameters()]
+    assert ours == list(fx["param_names"])
+
+
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base"])
+def test_oracle_matches_reference_golden(name):
+    cfg = CFG[name]
+    fx = load_fixture(name)
+    torch.set_num_threads(8)
+    from oracle.b2p2t_oracle import loss_and_grads, forward_loss
+    sd = oracle_state(cfg)
+    b = batch_dict(cfg)
+    assert np.array_equal(b["x"].numpy(), fx["x"])
+    loss, grads = loss_and_grads(sd, b, oracle_cfg(cfg))
+    assert abs(float(loss) - float(fx["loss"])) <= 2e-5 * abs(float(fx["loss"])), (float(loss), float(fx["loss"]))
+    gmax = max(float(fx["gnorm/" + n]) for n in fx["param_names"])
+    for n in fx["param_names"]:
+        g = grads[n]
+        ref_norm = float(fx["gnorm/" + n])
+        # gradients that are mathematically ~0 (e.g. attention key bias) are compared absolutely
+        assert abs(float(g.double().norm()) - ref_norm) <= 1e-4 * ref_norm + 1e-6 * gmax, n
+        atol = 1e-6 * gmax
+        if "grad/" + n in fx:
+            np.testing.assert_allclose(g.numpy(), fx["grad/" + n], rtol=1e-3, atol=atol, err_msg=n)
+        else:
+            v = g.reshape(-1)[torch.from_numpy(fx["gidx/" + n])].numpy()
+            np.testing.assert_allclose(v, fx["gval/" + n], rtol=1e-3, atol=atol, err_msg=n)
+
+
+def test_oracle_logits_match_reference():
+    cfg = CFG["tiny_a"]
+    fx = load_fixture("tiny_a")
+    from oracle.b2p2t_oracle import forward_loss
+    sd = oracle_state(cfg)
+    loss, aux = forward_loss(sd, batch_dict(cfg), oracle_cfg(cfg), return_all=True)
+    np.testing.assert_allclose(aux["logits"].detach().numpy(), fx["logits"], rtol=1e-4, atol=1e-5)
+    np.testing.assert_array_equal(aux["logit_lens"].numpy(), fx["logit_lens"])

@@ -1,0 +1,137 @@
+"""ctypes binding of libb2p_hip.so (the C ABI declared in include/b2p_hip.h).
+
+This is the binding a maintainer of the reference would add: the reference is Python, so its
+"FFI" is ctypes over a C-ABI shared library. torch is imported first so the
+HIP runtime it loaded (libamdhip64.so.7) is the one the library binds to; tensors cross the
+boundary as raw device pointers and every call is issued on torch's current HIP stream.
+
+There is no fallback: if the library is missing or fails to load, importing the product path
+raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede loading the HIP library: shared runtime)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libb2p_hip.so")
+
+c_i64 = ctypes.c_int64
+c_i32 = ctypes.c_int32
+c_f32 = ctypes.c_float
+c_f64 = ctypes.c_double
+c_u64 = ctypes.c_uint64
+c_p = ctypes.c_void_p
+
+
+class Operand(ctypes.Structure):
+    _fields_ = [
+        ("ptr", c_p), ("ld", c_i64), ("bs1", c_i64), ("bs2", c_i64), ("gather1", c_p),
+        ("inner_is_k", c_i32), ("conv", c_i32),
+        ("conv_T_out", c_i32), ("conv_T_in", c_i32), ("conv_stride", c_i32), ("conv_pad", c_i32),
+        ("conv_Cg", c_i32), ("_pad0", c_i32), ("conv_sample_stride", c_i64),
+    ]
+
+
+class Epilogue(ctypes.Structure):
+    _fields_ = [
+        ("C", c_p), ("ldc", c_i64), ("cbs1", c_i64), ("cbs2", c_i64),
+        ("alpha", c_f32), ("beta", c_f32), ("bias", c_p), ("biasbs1", c_i64), ("bias_gather", c_p), ("pre_out", c_p),
+        ("act", c_i32), ("act_bwd", c_i32), ("aux", c_p), ("ldaux", c_i64), ("abs1", c_i64),
+        ("abs2", c_i64), ("drop_p", c_f32), ("_pad0", c_i32), ("drop_seed", c_u64),
+        ("residual", c_p), ("ldr", c_i64), ("rbs1", c_i64), ("rbs2", c_i64),
+    ]
+
+
+class GemmDesc(ctypes.Structure):
+    _fields_ = [
+        ("M", c_i64), ("N", c_i64), ("K", c_i64), ("nz1", c_i32), ("nz2", c_i32),
+        ("A", Operand), ("B", Operand), ("ep", Epilogue),
+        ("precision", c_i32), ("timing_family", c_i32), ("flops", c_f64),
+    ]
+
+
+# name -> (restype, argtypes)
+_SIGS = {
+    "b2p_last_error": (ctypes.c_char_p, []),
+    "b2p_version": (c_i32, []),
+    "b2p_timing_enable": (c_i32, [c_i32, c_i32]),
+    "b2p_timing_read": (c_i32, [c_i32, ctypes.POINTER(c_f32), ctypes.POINTER(c_i32), ctypes.POINTER(c_f64)]),
+    "b2p_gemm": (c_i32, [ctypes.POINTER(GemmDesc), c_p]),
+    "b2p_colsum_workspace": (c_i64, [c_i64, c_i64]),
+    "b2p_colsum": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_p]),
+    "b2p_colsum_batched": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32, c_p, c_p]),
+    "b2p_dropout": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_p]),
+    "b2p_layernorm_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_u64, c_p]),
+    "b2p_layernorm_bwd_workspace": (c_i64, [c_i64, c_i64]),
+    "b2p_layernorm_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_f32, c_u64,
+                                  c_p, c_f32, c_u64, c_p, c_p]),
+    "b2p_softmax_fwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_u64, c_p]),
+    "b2p_softmax_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_u64, c_p]),
+    "b2p_act_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p]),
+    "b2p_gauss_smooth": (c_i32, [c_p, c_p, c_i32, c_p, c_i64, c_i64, c_i64, c_p]),
+    "b2p_unfold_col2im": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_p]),
+    "b2p_day_reduce": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p]),
+    "b2p_conv_weight_permute": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_conv_weight_transpose_flip": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
+    "b2p_weight_norm_workspace": (c_i64, [c_i64, c_i64, c_i64]),
+    "b2p_weight_norm_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p]),
+    "b2p_weight_norm_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p]),
+    "b2p_gru_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_gru_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_gru_hprev": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_ctc_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
+    "b2p_ctc_fwd_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "b2p_adam_multi": (c_i32, [c_p, c_i32, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_p]),
+}
+
+# timing families (b2p_timing_*)
+TIMING_GEMM = 1
+
+_lib = None
+
+
+def load() -> ctypes.CDLL:
+    """Loads the HIP library (raises if absent: there is no CPU fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(
+            f"{LIB_PATH} not found: build it with `python -m wav2vec2forbrain_amd.build_lib` "
+            "(or __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    for name, (res, args) in _SIGS.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def exported_symbols() -> list[str]:
+    return list(_SIGS)
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = load().b2p_last_error().decode(errors="replace")
+        raise RuntimeError(f"b2p HIP library error in {what}: {msg} (rc={rc})")
+
+
+def call(name: str, *args) -> None:
+    """Calls a status-returning entry point and raises RuntimeError on failure."""
+    rc = getattr(load(), name)(*args)
+    check(rc, name)
+
+
+def stream_ptr() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def ptr(t) -> int | None:
+    if t is None:
+        return None
+    return t.data_ptr()

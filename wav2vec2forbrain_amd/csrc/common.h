@@ -1,0 +1,87 @@
+// Shared device/host helpers for the b2p2t HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <string>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+
+// ---------------------------------------------------------------------------
+// error reporting: every C-ABI entry returns 0 on success, nonzero on failure
+// and leaves a message retrievable through b2p_last_error().
+// ---------------------------------------------------------------------------
+void b2p_set_error(const char* fmt, ...);
+
+#define B2P_CHECK_ARG(cond, ...)                 \
+  do {                                           \
+    if (!(cond)) {                               \
+      b2p_set_error(__VA_ARGS__);                \
+      return 1;                                  \
+    }                                            \
+  } while (0)
+
+#define B2P_CHECK_HIP(expr)                                                   \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) {                                                   \
+      b2p_set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),   \
+                    __FILE__, __LINE__);                                      \
+      return 2;                                                               \
+    }                                                                         \
+  } while (0)
+
+#define B2P_CHECK_LAUNCH() B2P_CHECK_HIP(hipGetLastError())
+
+// ---------------------------------------------------------------------------
+// device math
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float b2p_gelu(float x) {
+  // exact erf GELU (transformers ACT2FN["gelu"] == torch.nn.functional.gelu)
+  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+}
+__device__ __forceinline__ float b2p_gelu_grad(float x) {
+  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
+  const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);
+  return cdf + x * pdf;
+}
+__device__ __forceinline__ float b2p_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float b2p_silu(float x) { return x * b2p_sigmoid(x); }
+__device__ __forceinline__ float b2p_silu_grad(float x) {
+  const float s = b2p_sigmoid(x);
+  return s * (1.0f + x * (1.0f - s));
+}
+
+// Counter-based dropout mask (stateless, so backward regenerates the forward
+// mask from (seed, element index) instead of storing it). splitmix64 finaliser.
+__device__ __forceinline__ uint32_t b2p_hash(uint64_t seed, uint64_t idx) {
+  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z = z ^ (z >> 31);
+  return (uint32_t)(z >> 32);
+}
+// keep-probability threshold: keep iff hash >= thr, thr = round(p * 2^32)
+__device__ __forceinline__ bool b2p_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
+  return b2p_hash(seed, idx) >= thr;
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+static inline uint32_t b2p_dropout_threshold(float p) {
+  if (p <= 0.f) return 0u;
+  double t = (double)p * 4294967296.0;
+  if (t >= 4294967295.0) return 0xFFFFFFFFu;
+  return (uint32_t)t;
+}

@@ -1,0 +1,596 @@
+// HBM-bound kernels of the path: column reductions, dropout, LayerNorm, attention softmax,
+// activation backward, front-end smoothing / col2im, weight layout transforms, weight norm.
+// All fp32, float4-vectorised along the contiguous dimension where the layout allows.
+#include "common.h"
+#include "../../include/b2p_hip.h"
+
+namespace {
+constexpr int kColsumRows = 64;   // rows summed per block in phase 1
+
+// out[b][n] (+)= sum_m f(X[b][m][n]) ; mode 0: x, 1: x*x, 2: x*Y
+__global__ void colsum_p1(const float* __restrict__ X, const float* __restrict__ Y, int64_t M,
+                          int64_t N, int64_t ld, int64_t bstride, int mode, float* __restrict__ part,
+                          int nblk) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int blk = blockIdx.y, b = blockIdx.z;
+  if (n >= N) return;
+  const int64_t m0 = (int64_t)blk * kColsumRows;
+  const int64_t m1 = m0 + kColsumRows < M ? m0 + kColsumRows : M;
+  const float* xp = X + b * bstride + n;
+  const float* yp = Y ? Y + b * bstride + n : nullptr;
+  float s = 0.f;
+  for (int64_t m = m0; m < m1; ++m) {
+    const float x = xp[m * ld];
+    s += mode == 0 ? x : (mode == 1 ? x * x : x * yp[m * ld]);
+  }
+  part[((int64_t)b * nblk + blk) * N + n] = s;
+}
+
+__global__ void colsum_p2(const float* __restrict__ part, int nblk, int64_t N, float* __restrict__ out,
+                          int accumulate) {
+  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (n >= N) return;
+  const float* p = part + (int64_t)b * nblk * N + n;
+  float s = 0.f;
+  for (int i = 0; i < nblk; ++i) s += p[(int64_t)i * N];
+  float* o = out + (int64_t)b * N + n;
+  *o = accumulate ? *o + s : s;
+}
+
+int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_t N, int64_t ld,
+                int64_t bstride, int mode, float* out, int accumulate, float* part, hipStream_t st) {
+  if (M <= 0 || N <= 0 || batch <= 0) return 0;
+  const int nblk = (int)((M + kColsumRows - 1) / kColsumRows);
+  dim3 g1((unsigned)((N + 255) / 256), nblk, (unsigned)batch);
+  hipLaunchKernelGGL(colsum_p1, g1, dim3(256), 0, st, X, Y, M, N, ld, bstride, mode, part, nblk);
+  dim3 g2((unsigned)((N + 255) / 256), (unsigned)batch);
+  hipLaunchKernelGGL(colsum_p2, g2, dim3(256), 0, st, part, nblk, N, out, accumulate);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+// ------------------------------------------------------------------ dropout
+__global__ void dropout_k(const float* __restrict__ x, float* __restrict__ y, int64_t n, uint32_t thr,
+                          float scale, uint64_t seed) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  y[i] = b2p_keep(seed, (uint64_t)i, thr) ? x[i] * scale : 0.f;
+}
+
+// ------------------------------------------------------------------ LayerNorm
+// one wave per row; cols <= 64 * 4 * LN_MAXV
+constexpr int LN_MAXV = 4;
+__global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                const float* __restrict__ beta, float* __restrict__ y,
+                                                float* __restrict__ mean, float* __restrict__ rstd,
+                                                int64_t rows, int cols, float eps, uint32_t thr, float dscale,
+                                                uint64_t seed, float drop_p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nv = cols >> 2;
+  const float4* xr = reinterpret_cast<const float4*>(x + row * cols);
+  float4 v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) { v[i] = xr[c]; s += v[i].x + v[i].y + v[i].z + v[i].w; }
+  }
+  const float mu = warp_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+      const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
+      q += a * a + b * b + cc * cc + d * d;
+    }
+  }
+  const float var = warp_sum(q) / cols;
+  const float rs = rsqrtf(var + eps);
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+  const float4* g4 = reinterpret_cast<const float4*>(gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(beta);
+  float4* yr = reinterpret_cast<float4*>(y + row * cols);
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+      const float4 g = g4[c], bb = b4[c];
+      float4 o;
+      o.x = (v[i].x - mu) * rs * g.x + bb.x;
+      o.y = (v[i].y - mu) * rs * g.y + bb.y;
+      o.z = (v[i].z - mu) * rs * g.z + bb.z;
+      o.w = (v[i].w - mu) * rs * g.w + bb.w;
+      if (drop_p > 0.f) {
+        const uint64_t base = (uint64_t)row * cols + 4 * c;
+        o.x = b2p_keep(seed, base + 0, thr) ? o.x * dscale : 0.f;
+        o.y = b2p_keep(seed, base + 1, thr) ? o.y * dscale : 0.f;
+        o.z = b2p_keep(seed, base + 2, thr) ? o.z * dscale : 0.f;
+        o.w = b2p_keep(seed, base + 3, thr) ? o.w * dscale : 0.f;
+      }
+      yr[c] = o;
+    }
+  }
+}
+
+constexpr int LN_BWD_ROWS = 32;   // rows per block (8 per wave)
+__global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, const float* __restrict__ x,
+                                                const float* __restrict__ gamma, const float* __restrict__ mean,
+                                                const float* __restrict__ rstd, float* __restrict__ dx,
+                                                const float* __restrict__ dx_accum, float* __restrict__ part,
+                                                int64_t rows, int cols, uint32_t thr, float dscale, uint64_t seed,
+                                                float drop_p, float* __restrict__ dxd, uint32_t thr2, float dscale2,
+                                                uint64_t seed2) {
+  __shared__ float red[4][2][LN_MAXV * 256];   // not all used; cols <= 2048
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nv = cols >> 2;
+  const float4* g4 = reinterpret_cast<const float4*>(gamma);
+  float4 dg[LN_MAXV], db[LN_MAXV];
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) { dg[i] = make_float4(0, 0, 0, 0); db[i] = make_float4(0, 0, 0, 0); }
+  for (int rr = 0; rr < LN_BWD_ROWS / 4; ++rr) {
+    const int64_t row = (int64_t)blockIdx.x * LN_BWD_ROWS + wave * (LN_BWD_ROWS / 4) + rr;
+    if (row >= rows) break;
+    const float mu = mean[row], rs = rstd[row];
+    const float4* xr = reinterpret_cast<const float4*>(x + row * cols);
+    const float4* dyr = reinterpret_cast<const float4*>(dy + row * cols);
+    float4 xh[LN_MAXV], gg[LN_MAXV];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nv) {
+        float4 d = dyr[c];
+        if (drop_p > 0.f) {
+          const uint64_t base = (uint64_t)row * cols + 4 * c;
+          d.x = b2p_keep(seed, base + 0, thr) ? d.x * dscale : 0.f;
+          d.y = b2p_keep(seed, base + 1, thr) ? d.y * dscale : 0.f;
+          d.z = b2p_keep(seed, base + 2, thr) ? d.z * dscale : 0.f;
+          d.w = b2p_keep(seed, base + 3, thr) ? d.w * dscale : 0.f;
+        }
+        const float4 xv = xr[c], g = g4[c];
+        xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
+        gg[i] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
+        s1 += gg[i].x + gg[i].y + gg[i].z + gg[i].w;
+        s2 += gg[i].x * xh[i].x + gg[i].y * xh[i].y + gg[i].z * xh[i].z + gg[i].w * xh[i].w;
+        dg[i].x += d.x * xh[i].x; dg[i].y += d.y * xh[i].y; dg[i].z += d.z * xh[i].z; dg[i].w += d.w * xh[i].w;
+        db[i].x += d.x; db[i].y += d.y; db[i].z += d.z; db[i].w += d.w;
+      }
+    }
+    s1 = warp_sum(s1) / cols;
+    s2 = warp_sum(s2) / cols;
+    float4* dxr = reinterpret_cast<float4*>(dx + row * cols);
+    const float4* acc = dx_accum ? reinterpret_cast<const float4*>(dx_accum + row * cols) : nullptr;
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nv) {
+        float4 o;
+        o.x = rs * (gg[i].x - s1 - xh[i].x * s2);
+        o.y = rs * (gg[i].y - s1 - xh[i].y * s2);
+        o.z = rs * (gg[i].z - s1 - xh[i].z * s2);
+        o.w = rs * (gg[i].w - s1 - xh[i].w * s2);
+        if (acc) { const float4 a = acc[c]; o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w; }
+        dxr[c] = o;
+        if (dxd) {   // gradient of the dropout that produced this LN's input (residual branch)
+          const uint64_t base = (uint64_t)row * cols + 4 * c;
+          float4 q;
+          q.x = b2p_keep(seed2, base + 0, thr2) ? o.x * dscale2 : 0.f;
+          q.y = b2p_keep(seed2, base + 1, thr2) ? o.y * dscale2 : 0.f;
+          q.z = b2p_keep(seed2, base + 2, thr2) ? o.z * dscale2 : 0.f;
+          q.w = b2p_keep(seed2, base + 3, thr2) ? o.w * dscale2 : 0.f;
+          reinterpret_cast<float4*>(dxd + row * cols)[c] = q;
+        }
+      }
+    }
+  }
+  // block reduction of dgamma/dbeta partials
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+      reinterpret_cast<float4*>(red[wave][0])[c] = dg[i];
+      reinterpret_cast<float4*>(red[wave][1])[c] = db[i];
+    }
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < cols; c += 256) {
+    const float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
+    const float b = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
+    part[(int64_t)blockIdx.x * 2 * cols + c] = a;
+    part[(int64_t)blockIdx.x * 2 * cols + cols + c] = b;
+  }
+}
+
+__global__ void ln_bwd_reduce(const float* __restrict__ part, int nblk, int cols, float* __restrict__ dgamma,
+                              float* __restrict__ dbeta) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= 2 * cols) return;
+  float s = 0.f;
+  for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * 2 * cols + c];
+  if (c < cols) { if (dgamma) dgamma[c] = s; }
+  else { if (dbeta) dbeta[c - cols] = s; }
+}
+
+// ------------------------------------------------------------------ attention softmax
+// one wave per row, row length n <= 64*8
+constexpr int SM_MAXE = 8;
+__global__ void __launch_bounds__(256) softmax_fwd_k(const float* __restrict__ S, float* __restrict__ P,
+                                                     float* __restrict__ Pd, int64_t rows, int n, int64_t ld,
+                                                     uint32_t thr, float dscale, uint64_t seed, float drop_p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* sr = S + row * ld;
+  float v[SM_MAXE];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < SM_MAXE; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < n ? sr[c] : -INFINITY;
+    mx = fmaxf(mx, v[i]);
+  }
+  mx = warp_max(mx);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < SM_MAXE; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < n ? __expf(v[i] - mx) : 0.f;
+    s += v[i];
+  }
+  const float inv = 1.0f / warp_sum(s);
+  float* pr = P + row * ld;
+  float* pdr = Pd + row * ld;
+#pragma unroll
+  for (int i = 0; i < SM_MAXE; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n) {
+      const float p = v[i] * inv;
+      pr[c] = p;
+      if (drop_p > 0.f) pdr[c] = b2p_keep(seed, (uint64_t)row * n + c, thr) ? p * dscale : 0.f;
+      else pdr[c] = p;
+    } else if (c < ld) {
+      pr[c] = 0.f;
+      pdr[c] = 0.f;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) softmax_bwd_k(const float* __restrict__ P, const float* __restrict__ dPd,
+                                                     float* __restrict__ dS, int64_t rows, int n, int64_t ld,
+                                                     uint32_t thr, float dscale, uint64_t seed, float drop_p) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const float* pr = P + row * ld;
+  const float* gr = dPd + row * ld;
+  float p[SM_MAXE], g[SM_MAXE];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < SM_MAXE; ++i) {
+    const int c = lane + 64 * i;
+    p[i] = c < n ? pr[c] : 0.f;
+    float gv = c < n ? gr[c] : 0.f;
+    if (drop_p > 0.f && c < n) gv = b2p_keep(seed, (uint64_t)row * n + c, thr) ? gv * dscale : 0.f;
+    g[i] = gv;
+    s += p[i] * gv;
+  }
+  s = warp_sum(s);
+  float* dr = dS + row * ld;
+#pragma unroll
+  for (int i = 0; i < SM_MAXE; ++i) {
+    const int c = lane + 64 * i;
+    if (c < n) dr[c] = p[i] * (g[i] - s);
+    else if (c < ld) dr[c] = 0.f;
+  }
+}
+
+__global__ void act_bwd_k(const float* __restrict__ dy, const float* __restrict__ pre, float* __restrict__ dx,
+                          int64_t n, int act) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float x = pre[i];
+  float g = 1.f;
+  if (act == B2P_ACT_GELU) g = b2p_gelu_grad(x);
+  else if (act == B2P_ACT_SOFTSIGN) { const float d = 1.f + fabsf(x); g = 1.f / (d * d); }
+  else if (act == B2P_ACT_SILU) g = b2p_silu_grad(x);
+  dx[i] = dy[i] * g;
+}
+
+// ------------------------------------------------------------------ front-end
+__global__ void gauss_k(const float* __restrict__ x, const float* __restrict__ taps, int ntaps,
+                        float* __restrict__ y, int64_t B, int64_t L, int64_t C4) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * L * C4) return;
+  const int64_t c4 = i % C4;
+  const int64_t l = (i / C4) % L;
+  const int64_t b = i / (C4 * L);
+  const int left = (ntaps - 1) / 2;
+  const float4* xb = reinterpret_cast<const float4*>(x) + b * L * C4 + c4;
+  float4 acc = make_float4(0, 0, 0, 0);
+  for (int j = 0; j < ntaps; ++j) {
+    const int64_t src = l + j - left;
+    if (src < 0 || src >= L) continue;
+    const float w = taps[j];
+    const float4 v = xb[src * C4];
+    acc.x += w * v.x; acc.y += w * v.y; acc.z += w * v.z; acc.w += w * v.w;
+  }
+  reinterpret_cast<float4*>(y)[i] = acc;
+}
+
+__global__ void col2im_k(const float* __restrict__ dA, const float* __restrict__ Z, float* __restrict__ dX,
+                         int64_t B, int64_t L, int64_t C4, int64_t T, int ktaps, int stride) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * L * C4) return;
+  const int64_t c4 = i % C4;
+  const int64_t l = (i / C4) % L;
+  const int64_t b = i / (C4 * L);
+  const int64_t C = C4 * 4;
+  const int64_t rowlen = (int64_t)ktaps * C;
+  float4 acc = make_float4(0, 0, 0, 0);
+  // taps with (l - tap) % stride == 0
+  int tap0 = (int)(l % stride);
+  for (int tap = tap0; tap < ktaps; tap += stride) {
+    const int64_t t = (l - tap) / stride;
+    if (l - tap < 0) break;
+    if (t >= T) continue;
+    const float4 v = reinterpret_cast<const float4*>(dA + (b * T + t) * rowlen + (int64_t)tap * C)[c4];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  if (Z) {
+    const float4 z = reinterpret_cast<const float4*>(Z)[i];
+    float d;
+    d = 1.f + fabsf(z.x); acc.x /= d * d;
+    d = 1.f + fabsf(z.y); acc.y /= d * d;
+    d = 1.f + fabsf(z.z); acc.z /= d * d;
+    d = 1.f + fabsf(z.w); acc.w /= d * d;
+  }
+  reinterpret_cast<float4*>(dX)[i] = acc;
+}
+
+__global__ void day_reduce_k(const float* __restrict__ ps, const int64_t* __restrict__ day, int64_t B,
+                             int64_t ndays, int64_t elems, float* __restrict__ out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= ndays * elems) return;
+  const int64_t d = i / elems, e = i % elems;
+  float s = 0.f;
+  for (int64_t b = 0; b < B; ++b)
+    if (day[b] == d) s += ps[b * elems + e];
+  out[i] = s;
+}
+
+// ------------------------------------------------------------------ weight layouts
+__global__ void conv_perm_k(const float* __restrict__ in, float* __restrict__ out, int64_t O, int64_t I,
+                            int64_t K, int inverse) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= O * I * K) return;
+  // canonical index: (o, i, k) with k fastest in the reference layout
+  const int64_t k = idx % K, i = (idx / K) % I, o = idx / (K * I);
+  const int64_t ref = idx;
+  const int64_t perm = o * I * K + k * I + i;
+  if (inverse) out[ref] = in[perm];
+  else out[perm] = in[ref];
+}
+
+__global__ void conv_tflip_k(const float* __restrict__ w, float* __restrict__ out, int64_t G, int64_t Og,
+                             int64_t I, int64_t K) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= G * Og * I * K) return;
+  // w layout: [(g*Og+o)][i][k]
+  const int64_t k = idx % K, i = (idx / K) % I, o = (idx / (K * I)) % Og, g = idx / (K * I * Og);
+  const int64_t kp = K - 1 - k;
+  out[((g * I + i) * K + kp) * Og + o] = w[idx];
+}
+
+__global__ void wn_fwd_k(const float* __restrict__ g, const float* __restrict__ v, const float* __restrict__ sq,
+                         float* __restrict__ w, float* __restrict__ norms, int64_t n, int64_t K) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  const int64_t k = idx % K;
+  const float nm = sqrtf(sq[k]);
+  if (idx < K) norms[idx] = sqrtf(sq[idx]);
+  w[idx] = g[k] * v[idx] / nm;
+}
+
+__global__ void wn_bwd_k(const float* __restrict__ g, const float* __restrict__ v, const float* __restrict__ norms,
+                         const float* __restrict__ dw, const float* __restrict__ dwv, float* __restrict__ dg,
+                         float* __restrict__ dv, int64_t n, int64_t K) {
+  const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= n) return;
+  const int64_t k = idx % K;
+  const float nm = norms[k];
+  const float dgk = dwv[k] / nm;                 // sum(dw * v) / ||v||
+  if (idx < K) dg[idx] = dwv[idx] / norms[idx];
+  const float gk = g[k];
+  // dv = (g/n) * (dw - (v/n) * dg)
+  dv[idx] = gk / nm * (dw[idx] - v[idx] / nm * dgk);
+}
+
+inline unsigned nblocks(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
+}  // namespace
+
+// =====================================================================================
+extern "C" int64_t b2p_colsum_workspace(int64_t M, int64_t N) {
+  return ((M + kColsumRows - 1) / kColsumRows) * N;
+}
+
+extern "C" int b2p_colsum(const float* X, int64_t M, int64_t N, int64_t ld, float* out, int accumulate,
+                          float* partial, b2p_stream_t stream) {
+  B2P_CHECK_ARG(X && out && partial, "colsum: NULL pointer");
+  return colsum_impl(X, nullptr, 1, M, N, ld, 0, 0, out, accumulate, partial, (hipStream_t)stream);
+}
+
+extern "C" int b2p_colsum_batched(const float* X, const float* Y, int64_t batch, int64_t M, int64_t N,
+                                  int64_t ld, int64_t bstride, int mode, float* out, int accumulate,
+                                  float* partial, b2p_stream_t stream) {
+  B2P_CHECK_ARG(X && out && partial, "colsum_batched: NULL pointer");
+  B2P_CHECK_ARG(mode != 2 || Y, "colsum_batched: mode 2 needs Y");
+  return colsum_impl(X, Y, batch, M, N, ld, bstride, mode, out, accumulate, partial, (hipStream_t)stream);
+}
+
+extern "C" int b2p_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && y, "dropout: NULL pointer");
+  B2P_CHECK_ARG(p >= 0.f && p < 1.f, "dropout: p must be in [0,1)");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(dropout_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, x, y, n,
+                     b2p_dropout_threshold(p), p > 0.f ? 1.f / (1.f - p) : 1.f, seed);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean,
+                                 float* rstd, int64_t rows, int64_t cols, float eps, float drop_p,
+                                 uint64_t drop_seed, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: NULL pointer");
+  B2P_CHECK_ARG(cols % 4 == 0 && cols <= 64 * 4 * LN_MAXV, "layernorm_fwd: cols must be %%4 and <= 1024");
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(ln_fwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, y,
+                     mean, rstd, rows, (int)cols, eps, b2p_dropout_threshold(drop_p),
+                     drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, drop_seed, drop_p);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t b2p_layernorm_bwd_workspace(int64_t rows, int64_t cols) {
+  return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 2 * cols;
+}
+
+extern "C" int b2p_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
+                                 const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                                 int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
+                                 float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* workspace,
+                                 b2p_stream_t stream) {
+  B2P_CHECK_ARG(dy && x && gamma && mean && rstd && dx && workspace, "layernorm_bwd: NULL pointer");
+  B2P_CHECK_ARG(cols % 4 == 0 && cols <= 64 * 4 * LN_MAXV, "layernorm_bwd: cols must be %%4 and <= 1024");
+  if (rows <= 0) return 0;
+  const int nblk = (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(ln_bwd_k, dim3(nblk), dim3(256), 0, st, dy, x, gamma, mean, rstd, dx, dx_accum, workspace,
+                     rows, (int)cols, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
+                     drop_seed, drop_p, dx_dropped, b2p_dropout_threshold(in_drop_p),
+                     in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed);
+  hipLaunchKernelGGL(ln_bwd_reduce, dim3(nblocks(2 * cols)), dim3(256), 0, st, workspace, nblk, (int)cols,
+                     dgamma, dbeta);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_softmax_fwd(const float* S, float* P, float* Pd, int64_t rows, int64_t n, int64_t ld,
+                               float drop_p, uint64_t drop_seed, b2p_stream_t stream) {
+  B2P_CHECK_ARG(S && P && Pd, "softmax_fwd: NULL pointer");
+  B2P_CHECK_ARG(n > 0 && n <= 64 * SM_MAXE && ld >= n && ld <= 64 * SM_MAXE, "softmax_fwd: row length must be <= 512");
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(softmax_fwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, S, P, Pd, rows,
+                     (int)n, ld, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
+                     drop_seed, drop_p);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_softmax_bwd(const float* P, const float* dPd, float* dS, int64_t rows, int64_t n, int64_t ld,
+                               float drop_p, uint64_t drop_seed, b2p_stream_t stream) {
+  B2P_CHECK_ARG(P && dPd && dS, "softmax_bwd: NULL pointer");
+  B2P_CHECK_ARG(n > 0 && n <= 64 * SM_MAXE && ld >= n && ld <= 64 * SM_MAXE, "softmax_bwd: row length must be <= 512");
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(softmax_bwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, P, dPd, dS, rows,
+                     (int)n, ld, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
+                     drop_seed, drop_p);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_act_bwd(const float* dy, const float* pre, float* dx, int64_t n, int act, b2p_stream_t stream) {
+  B2P_CHECK_ARG(dy && pre && dx, "act_bwd: NULL pointer");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(act_bwd_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, dy, pre, dx, n, act);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_gauss_smooth(const float* x, const float* taps, int ntaps, float* y, int64_t B, int64_t L,
+                                int64_t C, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && taps && y, "gauss_smooth: NULL pointer");
+  B2P_CHECK_ARG(C % 4 == 0 && ntaps > 0, "gauss_smooth: C must be %%4");
+  const int64_t n = B * L * (C / 4);
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(gauss_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, x, taps, ntaps, y, B, L, C / 4);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_unfold_col2im(const float* dA, const float* Z, float* dX, int64_t B, int64_t L, int64_t C,
+                                 int64_t T, int ktaps, int stride, b2p_stream_t stream) {
+  B2P_CHECK_ARG(dA && dX, "unfold_col2im: NULL pointer");
+  B2P_CHECK_ARG(C % 4 == 0 && stride > 0 && ktaps > 0, "unfold_col2im: bad geometry");
+  const int64_t n = B * L * (C / 4);
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(col2im_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, dA, Z, dX, B, L, C / 4, T,
+                     ktaps, stride);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_day_reduce(const float* per_sample, const int64_t* day_idx, int64_t B, int64_t ndays,
+                              int64_t elems, float* out, b2p_stream_t stream) {
+  B2P_CHECK_ARG(per_sample && day_idx && out, "day_reduce: NULL pointer");
+  const int64_t n = ndays * elems;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(day_reduce_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, per_sample, day_idx, B,
+                     ndays, elems, out);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_conv_weight_permute(const float* in, float* out, int64_t O, int64_t I, int64_t ntaps,
+                                       int inverse, b2p_stream_t stream) {
+  B2P_CHECK_ARG(in && out && in != out, "conv_weight_permute: bad pointers");
+  const int64_t n = O * I * ntaps;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(conv_perm_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, in, out, O, I, ntaps,
+                     inverse);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_conv_weight_transpose_flip(const float* w, float* out, int64_t G, int64_t Og, int64_t I,
+                                              int64_t ntaps, b2p_stream_t stream) {
+  B2P_CHECK_ARG(w && out && w != out, "conv_weight_transpose_flip: bad pointers");
+  const int64_t n = G * Og * I * ntaps;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(conv_tflip_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, w, out, G, Og, I, ntaps);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+// workspace: K floats (sum of squares) + colsum partials
+extern "C" int64_t b2p_weight_norm_workspace(int64_t O, int64_t I, int64_t K) {
+  return K + b2p_colsum_workspace(O * I, K);
+}
+
+extern "C" int b2p_weight_norm_fwd(const float* g, const float* v, float* w, float* norms, int64_t O, int64_t I,
+                                   int64_t K, float* workspace, b2p_stream_t stream) {
+  B2P_CHECK_ARG(g && v && w && norms && workspace, "weight_norm_fwd: NULL pointer");
+  hipStream_t st = (hipStream_t)stream;
+  float* sq = workspace;
+  if (colsum_impl(v, nullptr, 1, O * I, K, K, 0, 1, sq, 0, workspace + K, st)) return 1;
+  const int64_t n = O * I * K;
+  hipLaunchKernelGGL(wn_fwd_k, dim3(nblocks(n)), dim3(256), 0, st, g, v, sq, w, norms, n, K);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_weight_norm_bwd(const float* g, const float* v, const float* norms, const float* dw, float* dg,
+                                   float* dv, int64_t O, int64_t I, int64_t K, float* workspace,
+                                   b2p_stream_t stream) {
+  B2P_CHECK_ARG(g && v && norms && dw && dg && dv && workspace, "weight_norm_bwd: NULL pointer");
+  hipStream_t st = (hipStream_t)stream;
+  float* dwv = workspace;
+  if (colsum_impl(dw, v, 1, O * I, K, K, 0, 2, dwv, 0, workspace + K, st)) return 1;
+  const int64_t n = O * I * K;
+  hipLaunchKernelGGL(wn_bwd_k, dim3(nblocks(n)), dim3(256), 0, st, g, v, norms, dw, dwv, dg, dv, n, K);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}

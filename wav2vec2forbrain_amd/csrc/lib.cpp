@@ -1,0 +1,100 @@
+// Library-level C ABI: error reporting, version, launch timing.
+#include <hip/hip_runtime.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <mutex>
+#include <vector>
+#include "../../include/b2p_hip.h"
+#include "timing.h"
+
+static thread_local char g_err[1024] = "";
+
+void b2p_set_error(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(g_err, sizeof(g_err), fmt, ap);
+  va_end(ap);
+}
+
+extern "C" const char* b2p_last_error(void) { return g_err; }
+extern "C" int b2p_version(void) { return 1; }
+
+// ------------------------------------------------------------------ timing
+namespace {
+constexpr int kFamilies = 16;
+struct Family {
+  bool on = false;
+  int max = 0;
+  int used = 0;  // event pairs recorded
+  std::vector<hipEvent_t> ev;  // 2 per launch
+  std::vector<double> flops;
+};
+Family g_fam[kFamilies];
+std::mutex g_mu;
+}  // namespace
+
+void b2p_timing_begin(int family, hipStream_t st) {
+  if (family <= 0 || family >= kFamilies) return;
+  Family& f = g_fam[family];
+  if (!f.on || f.used >= f.max) return;
+  hipEventRecord(f.ev[2 * f.used], st);
+}
+
+void b2p_timing_end(int family, hipStream_t st, double flops) {
+  if (family <= 0 || family >= kFamilies) return;
+  Family& f = g_fam[family];
+  if (!f.on || f.used >= f.max) return;
+  hipEventRecord(f.ev[2 * f.used + 1], st);
+  f.flops[f.used] = flops;
+  ++f.used;
+}
+
+extern "C" int b2p_timing_enable(int family, int max_events) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (family <= 0 || family >= kFamilies) {
+    b2p_set_error("timing: family %d out of range", family);
+    return 1;
+  }
+  Family& f = g_fam[family];
+  for (auto e : f.ev) hipEventDestroy(e);
+  f.ev.clear();
+  f.flops.clear();
+  f.used = 0;
+  f.on = max_events > 0;
+  f.max = max_events > 0 ? max_events : 0;
+  if (!f.on) return 0;
+  f.ev.resize(2 * (size_t)f.max);
+  f.flops.resize(f.max);
+  for (auto& e : f.ev) {
+    if (hipEventCreate(&e) != hipSuccess) {
+      b2p_set_error("timing: hipEventCreate failed");
+      return 2;
+    }
+  }
+  return 0;
+}
+
+extern "C" int b2p_timing_read(int family, float* total_ms, int* count, double* total_flops) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (family <= 0 || family >= kFamilies) {
+    b2p_set_error("timing: family %d out of range", family);
+    return 1;
+  }
+  Family& f = g_fam[family];
+  float tot = 0.f;
+  double fl = 0.0;
+  for (int i = 0; i < f.used; ++i) {
+    if (hipEventSynchronize(f.ev[2 * i + 1]) != hipSuccess) {
+      b2p_set_error("timing: event sync failed");
+      return 2;
+    }
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, f.ev[2 * i], f.ev[2 * i + 1]);
+    tot += ms;
+    fl += f.flops[i];
+  }
+  if (total_ms) *total_ms = tot;
+  if (count) *count = f.used;
+  if (total_flops) *total_flops = fl;
+  return 0;
+}

@@ -1,0 +1,746 @@
+"""Autograd-visible operators of the b2p2t_gru+w2v training step, each a thin host wrapper over
+the C ABI of libb2p_hip.so (include/b2p_hip.h). No operator here computes on the CPU or falls
+back to a PyTorch kernel: tensors must be fp32 CUDA(HIP) tensors and every FLOP of the forward
+and backward runs in the hand-written gfx950 kernels. PyTorch supplies device memory (caching
+allocator), the stream and autograd bookkeeping only.
+
+Operators (reference call sites in each docstring):
+  front_end        Gaussian smoothing + day linear + softsign          (b2p2t_model.py:138-167)
+  gru_layer        bidirectional GRU layer, optional implicit Unfold     (brain_feature_extractor.py:56-68)
+  linear           nn.Linear (+ activation)                              (nn_helper.py:31-49, lm_head)
+  dropout          nn.Dropout with a stateless, regenerable mask
+  pos_conv_ln      pos-conv embedding + residual + LayerNorm + dropout   (TF Wav2Vec2Encoder.forward)
+  encoder_layer    post-LN transformer layer                              (TF Wav2Vec2EncoderLayer)
+  ctc_loss         log_softmax + CTCLoss(blank=0, mean, zero_infinity)   (w2v_custom_feat_extractor.py:81-90)
+"""
+from __future__ import annotations
+
+import contextlib
+import ctypes
+import math
+import threading
+
+import torch
+
+from . import _lib
+from ._lib import GemmDesc, Operand, Epilogue
+
+ACT = {"none": 0, None: 0, "gelu": 1, "softsign": 2, "silu": 3, "swish": 3}
+
+_state = threading.local()
+
+
+def _prec() -> int:
+    return getattr(_state, "prec", 0)
+
+
+@contextlib.contextmanager
+def precision(mode: str):
+    """'bf16' (default: bf16 MFMA, fp32 accumulate) or 'fp32' (exact-fp32 MFMA parity mode)."""
+    old = _prec()
+    _state.prec = {"bf16": 0, "fp32": 1}[mode]
+    try:
+        yield
+    finally:
+        _state.prec = old
+
+
+def set_precision(mode: str) -> None:
+    _state.prec = {"bf16": 0, "fp32": 1}[mode]
+
+
+_GEMM_TIMING = [0]
+
+
+def set_gemm_timing(on: bool) -> None:
+    """Tag every GEMM launch for HIP-event timing (bench.py roofline; b2p_timing_enable first)."""
+    _GEMM_TIMING[0] = _lib.TIMING_GEMM if on else 0
+
+
+# ------------------------------------------------------------------ dropout seeds
+class _SeedStream:
+    """64-bit seeds for the stateless dropout masks, drawn from a CPU generator so that a run is
+    reproducible from torch.manual_seed (the reference seeds torch at src/experiments/experiment.py:34)."""
+
+    def __init__(self):
+        self.gen = None
+
+    def next(self) -> int:
+        if self.gen is None:
+            self.gen = torch.Generator()
+            self.gen.manual_seed(torch.initial_seed() & 0xFFFFFFFFFFFF)
+        return int(torch.randint(0, 2 ** 62, (1,), generator=self.gen).item())
+
+    def reseed(self, seed: int) -> None:
+        self.gen = torch.Generator()
+        self.gen.manual_seed(seed)
+
+
+SEEDS = _SeedStream()
+
+
+def _chk(t: torch.Tensor, name: str) -> None:
+    if not t.is_cuda:
+        raise RuntimeError(f"{name}: expected a HIP device tensor (the product path has no CPU fallback)")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name}: expected float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name}: expected a contiguous tensor")
+
+
+def _p(t, off: int = 0):
+    return None if t is None else t.data_ptr() + 4 * off
+
+
+def _st():
+    return _lib.stream_ptr()
+
+
+# ------------------------------------------------------------------ GEMM plumbing
+def op(t, off=0, ld=0, k_inner=True, bs1=0, bs2=0, gather=None):
+    o = Operand()
+    o.ptr = _p(t, off)
+    o.ld = ld
+    o.bs1 = bs1
+    o.bs2 = bs2
+    o.gather1 = None if gather is None else gather.data_ptr()
+    o.inner_is_k = 1 if k_inner else 0
+    o.conv = 0
+    return o
+
+
+def conv_op(t, off, ld, T_out, T_in, stride, pad, Cg, sample_stride, k_inner=True, bs1=0, bs2=0):
+    o = op(t, off, ld, k_inner, bs1, bs2)
+    o.conv = 1
+    o.conv_T_out = T_out
+    o.conv_T_in = T_in
+    o.conv_stride = stride
+    o.conv_pad = pad
+    o.conv_Cg = Cg
+    o.conv_sample_stride = sample_stride
+    return o
+
+
+def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1, nz2=1, alpha=1.0,
+         beta=0.0, bias=None, biasbs1=0, bias_gather=None, pre_out=None, act=0, act_bwd=0, aux=None, ldaux=0, abs1=0, abs2=0,
+         drop_p=0.0, seed=0, residual=None, r_off=0, ldr=0, rbs1=0, rbs2=0, timing=0):
+    d = GemmDesc()
+    d.M, d.N, d.K = M, N, K
+    d.nz1, d.nz2 = nz1, nz2
+    d.A = A
+    d.B = B
+    e = Epilogue()
+    e.C = _p(C, c_off)
+    e.ldc, e.cbs1, e.cbs2 = ldc, cbs1, cbs2
+    e.alpha, e.beta = alpha, beta
+    e.bias = _p(bias)
+    e.biasbs1 = biasbs1
+    e.bias_gather = None if bias_gather is None else bias_gather.data_ptr()
+    e.pre_out = _p(pre_out, c_off) if pre_out is not None else None
+    e.act, e.act_bwd = act, act_bwd
+    e.aux = _p(aux, c_off) if aux is not None else None
+    e.ldaux, e.abs1, e.abs2 = ldaux or ldc, abs1 or cbs1, abs2 or cbs2
+    e.drop_p = drop_p
+    e.drop_seed = seed
+    e.residual = _p(residual, r_off) if residual is not None else None
+    e.ldr, e.rbs1, e.rbs2 = ldr or ldc, rbs1 or cbs1, rbs2 or cbs2
+    d.ep = e
+    d.precision = _prec()
+    d.timing_family = timing or _GEMM_TIMING[0]
+    d.flops = 2.0 * M * N * K * nz1 * nz2
+    _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
+
+
+def mm_nt(x, W, out, bias=None, act=0, pre_out=None, drop_p=0.0, seed=0, residual=None, alpha=1.0, beta=0.0,
+          timing=0):
+    """out[M,N] = epi(x[M,K] @ W[N,K]^T) (nn.Linear forward)."""
+    M, K = x.shape[-2] if x.dim() > 1 else 1, x.shape[-1]
+    M = x.numel() // K
+    N = W.shape[0]
+    gemm(M, N, K, op(x, 0, K, True), op(W, 0, W.shape[1], True), out, N, bias=bias, act=act, pre_out=pre_out,
+         drop_p=drop_p, seed=seed, residual=residual, alpha=alpha, beta=beta, timing=timing)
+
+
+def mm_nn(a, W, out, act_bwd=0, aux=None, drop_p=0.0, seed=0, residual=None, alpha=1.0, beta=0.0):
+    """out[M,N] = epi(a[M,K] @ W[K,N]) (nn.Linear input gradient, W = weight [out,in])."""
+    K, N = W.shape[0], W.shape[1]
+    M = a.numel() // K
+    gemm(M, N, K, op(a, 0, K, True), op(W, 0, N, False), out, N, act_bwd=act_bwd, aux=aux, drop_p=drop_p,
+         seed=seed, residual=residual, alpha=alpha, beta=beta)
+
+
+def mm_tn(dy, x, out, beta=0.0):
+    """out[N,K] = dy[M,N]^T @ x[M,K] (nn.Linear weight gradient)."""
+    N = dy.shape[-1]
+    K = x.shape[-1]
+    M = dy.numel() // N
+    gemm(N, K, M, op(dy, 0, N, False), op(x, 0, K, False), out, K, beta=beta)
+
+
+_WS = {}
+
+
+def _colsum_ws(M, N, device):
+    n = int(_lib.load().b2p_colsum_workspace(M, N))
+    return torch.empty(max(n, 1), device=device, dtype=torch.float32)
+
+
+def colsum(x2d_ptr_tensor, M, N, out, ld=None, accumulate=False):
+    ws = _colsum_ws(M, N, out.device)
+    _lib.call("b2p_colsum", _p(x2d_ptr_tensor), M, N, ld or N, _p(out), int(accumulate), _p(ws), _st())
+
+
+def colsum_batched(x, batch, M, N, out, ld=None, bstride=None, mode=0, y=None):
+    ws = torch.empty(max(int(_lib.load().b2p_colsum_workspace(M, N)) * batch, 1), device=out.device)
+    _lib.call("b2p_colsum_batched", _p(x), _p(y), batch, M, N, ld or N, bstride if bstride is not None else M * N,
+              mode, _p(out), 0, _p(ws), _st())
+
+
+def _dropout_raw(x, p, seed, out=None):
+    out = torch.empty_like(x) if out is None else out
+    _lib.call("b2p_dropout", _p(x), _p(out), x.numel(), float(p), seed, _st())
+    return out
+
+
+def _act_bwd(dy, pre, act, out=None):
+    out = torch.empty_like(dy) if out is None else out
+    _lib.call("b2p_act_bwd", _p(dy), _p(pre), _p(out), dy.numel(), act, _st())
+    return out
+
+
+def _ln_fwd(x2d, g, b, eps, drop_p=0.0, seed=0):
+    rows, cols = x2d.shape
+    y = torch.empty_like(x2d)
+    mean = torch.empty(rows, device=x2d.device)
+    rstd = torch.empty(rows, device=x2d.device)
+    _lib.call("b2p_layernorm_fwd", _p(x2d), _p(g), _p(b), _p(y), _p(mean), _p(rstd), rows, cols, float(eps),
+              float(drop_p), seed, _st())
+    return y, mean, rstd
+
+
+def _ln_bwd(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, seed=0, in_drop_p=-1.0,
+            in_seed=0):
+    rows, cols = x.shape
+    dx = torch.empty_like(x)
+    dg = torch.empty(cols, device=x.device) if need_params else None
+    db = torch.empty(cols, device=x.device) if need_params else None
+    ws = torch.empty(int(_lib.load().b2p_layernorm_bwd_workspace(rows, cols)), device=x.device)
+    dxd = torch.empty_like(x) if in_drop_p >= 0.0 else None
+    _lib.call("b2p_layernorm_bwd", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows, cols,
+              _p(dx_accum), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed, _p(ws), _st())
+    return dx, dg, db, dxd
+
+
+# =====================================================================================
+# front end: GaussianSmoothing -> day linear (+bias) -> softsign
+# =====================================================================================
+class _FrontEnd(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, day_idxs, day_weights, day_bias, taps):
+        _chk(x, "front_end.x")
+        _chk(day_weights, "front_end.day_weights")
+        B, L, C = x.shape
+        xs = torch.empty_like(x)
+        _lib.call("b2p_gauss_smooth", _p(x), _p(taps), taps.numel(), _p(xs), B, L, C, _st())
+        z = torch.empty_like(x)
+        s = torch.empty_like(x)
+        # z[b] = xs[b] @ W[day[b]] + bias[day[b]] ; s = softsign(z)   (einsum "btd,bdk->btk")
+        gemm(L, C, C, op(xs, 0, C, True, bs1=L * C), op(day_weights, 0, C, False, bs1=C * C, gather=day_idxs),
+             s, C, cbs1=L * C, nz1=B, bias=day_bias, biasbs1=C, bias_gather=day_idxs, pre_out=z,
+             act=ACT["softsign"])
+        ctx.save_for_backward(xs, z, day_idxs, day_weights)
+        ctx.n_days = day_weights.shape[0]
+        return s
+
+    @staticmethod
+    def backward(ctx, ds):
+        xs, z, day_idxs, day_weights = ctx.saved_tensors
+        ds = ds.contiguous()
+        B, L, C = xs.shape
+        dz = _act_bwd(ds, z, ACT["softsign"])
+        dW = dbias = None
+        if ctx.needs_input_grad[2]:
+            per = torch.empty(B, C, C, device=xs.device)
+            # per[b] = xs[b]^T @ dz[b]   (K = L), then summed per day (deterministic)
+            gemm(C, C, L, op(xs, 0, C, False, bs1=L * C), op(dz, 0, C, False, bs1=L * C), per, C, cbs1=C * C, nz1=B)
+            dW = torch.empty_like(day_weights)
+            _lib.call("b2p_day_reduce", _p(per), _p(day_idxs), B, ctx.n_days, C * C, _p(dW), _st())
+        if ctx.needs_input_grad[3]:
+            per_b = torch.empty(B, C, device=xs.device)
+            colsum_batched(dz, B, L, C, per_b)
+            dbias = torch.empty(ctx.n_days, 1, C, device=xs.device)
+            _lib.call("b2p_day_reduce", _p(per_b), _p(day_idxs), B, ctx.n_days, C, _p(dbias), _st())
+        return None, None, dW, dbias, None
+
+
+def front_end(x, day_idxs, day_weights, day_bias, taps):
+    """b2p2t_model.py:150-159: permute -> GaussianSmoothing -> einsum(btd,bdk) + day_bias -> Softsign.
+    Returns the (B, L, 256) softsign output (the Unfold is implicit in the GRU layer-0 projection)."""
+    return _FrontEnd.apply(x.contiguous(), day_idxs.to(torch.int64).contiguous(), day_weights, day_bias, taps)
+
+
+# =====================================================================================
+# GRU layer (both directions)
+# =====================================================================================
+class Unfolded:
+    """Lazy nn.Unfold((k,1), stride) view of a (B, L, C) tensor (b2p2t_model.py:108-113, 162-167):
+    logically (B, T, C*k) with T = (L-k)//stride + 1. Never materialised on the product path; the
+    GRU layer-0 projection reads it as an implicit-GEMM operand."""
+
+    def __init__(self, src: torch.Tensor, kernel: int, stride: int):
+        self.src = src
+        self.kernel = kernel
+        self.stride = stride
+        B, L, C = src.shape
+        self.T = (L - kernel) // stride + 1
+        self.shape = (B, self.T, C * kernel)
+
+    def materialize(self) -> torch.Tensor:
+        """Reference layout (feature index c*k + tap); for inspection/tests only."""
+        B, L, C = self.src.shape
+        idx = torch.arange(self.T, device=self.src.device)[:, None] * self.stride + torch.arange(self.kernel, device=self.src.device)[None, :]
+        win = self.src[:, idx, :]                      # (B, T, k, C)
+        return win.permute(0, 1, 3, 2).reshape(B, self.T, C * self.kernel)
+
+
+def _stack2(a, b):
+    return a.unsqueeze(0) if b is None else torch.stack([a, b], 0)
+
+
+class _GRULayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, unf_meta, H, ndir, h0, *weights):
+        # weights: per direction (w_ih, w_hh, b_ih, b_hh)  (b_* may be None)
+        dev = x.device
+        if unf_meta is not None:
+            ktaps, stride = unf_meta
+            B, L, C = x.shape
+            T = (L - ktaps) // stride + 1
+            IN = C * ktaps
+        else:
+            B, T, IN = x.shape
+        G3 = 3 * H
+        wih = [weights[4 * d + 0] for d in range(ndir)]
+        whh = [weights[4 * d + 1] for d in range(ndir)]
+        bih = [weights[4 * d + 2] for d in range(ndir)]
+        bhh = [weights[4 * d + 3] for d in range(ndir)]
+        for w in wih + whh:
+            _chk(w, "gru.weight")
+        gi = torch.empty(B, T, ndir * G3, device=dev)
+        if unf_meta is not None:
+            # tap-major weight copy: W'[n][tap*C + c] = W[n][c*k + tap] for both directions
+            wperm = torch.empty(ndir * G3, IN, device=dev)
+            for d in range(ndir):
+                _lib.call("b2p_conv_weight_permute", _p(wih[d]), _p(wperm, d * G3 * IN), G3, C, ktaps, 0, _st())
+            bias_cat = torch.cat([b if b is not None else torch.zeros(G3, device=dev) for b in bih]) \
+                if any(b is not None for b in bih) else None
+            A = conv_op(x, 0, C, T, L, stride, 0, C * ktaps, L * C, True)
+            A.conv_Cg = C  # inner j = tap*C + c
+            gemm(B * T, ndir * G3, IN, A, op(wperm, 0, IN, True), gi, ndir * G3, bias=bias_cat)
+        else:
+            _chk(x, "gru.x")
+            wperm = None
+            for d in range(ndir):
+                gemm(B * T, G3, IN, op(x, 0, IN, True), op(wih[d], 0, IN, True), gi, ndir * G3, c_off=d * G3,
+                     bias=bih[d])
+        whh_s = torch.stack(whh, 0).contiguous()
+        bhh_s = torch.stack(bhh, 0).contiguous() if bhh[0] is not None else None
+        out = torch.empty(B, T, ndir * H, device=dev)
+        saved = torch.empty(B, T, ndir, 4, H, device=dev)
+        if h0 is not None:
+            _chk(h0, "gru.h0")
+        _lib.call("b2p_gru_fwd", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved), B, T, H, ndir, _st())
+        ctx.save_for_backward(x, out, saved, whh_s, h0, wperm, *wih)
+        ctx.meta = (unf_meta, H, ndir, B, T, IN, bih[0] is not None, bhh[0] is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        x, out, saved, whh_s, h0, wperm, *wih = ctx.saved_tensors
+        unf_meta, H, ndir, B, T, IN, has_bih, has_bhh = ctx.meta
+        dev = out.device
+        dout = dout.contiguous()
+        G3 = 3 * H
+        dgi = torch.empty(B, T, ndir * G3, device=dev)
+        dgh = torch.empty(B, T, ndir * G3, device=dev)
+        dhbuf = torch.empty(ndir, B, H, device=dev)
+        dh0 = torch.empty(ndir, B, H, device=dev) if (h0 is not None and ctx.needs_input_grad[4]) else None
+        _lib.call("b2p_gru_bwd", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi), _p(dgh), _p(dh0),
+                  _p(dhbuf), B, T, H, ndir, _st())
+        grads = [None] * (4 * ndir)
+        # recurrent weights: dW_hh[d] = dgh[:, :, d]^T @ hprev[d]
+        hp = torch.empty(ndir, B, T, H, device=dev)
+        _lib.call("b2p_gru_hprev", _p(out), _p(h0), _p(hp), B, T, H, ndir, _st())
+        for d in range(ndir):
+            if ctx.needs_input_grad[5 + 4 * d + 1]:
+                dwhh = torch.empty(G3, H, device=dev)
+                gemm(G3, H, B * T, op(dgh, d * G3, ndir * G3, False), op(hp, d * B * T * H, H, False), dwhh, H)
+                grads[4 * d + 1] = dwhh
+            if has_bhh and ctx.needs_input_grad[5 + 4 * d + 3]:
+                db = torch.empty(G3, device=dev)
+                colsum(_view_off(dgh, d * G3), B * T, G3, db, ld=ndir * G3)
+                grads[4 * d + 3] = db
+            if has_bih and ctx.needs_input_grad[5 + 4 * d + 2]:
+                db = torch.empty(G3, device=dev)
+                colsum(_view_off(dgi, d * G3), B * T, G3, db, ld=ndir * G3)
+                grads[4 * d + 2] = db
+        dx = None
+        if unf_meta is not None:
+            ktaps, stride = unf_meta
+            _, L, C = x.shape
+            if any(ctx.needs_input_grad[5 + 4 * d] for d in range(ndir)):
+                dwp = torch.empty(ndir * G3, IN, device=dev)
+                Bop = conv_op(x, 0, C, T, L, stride, 0, C, L * C, False)
+                gemm(ndir * G3, IN, B * T, op(dgi, 0, ndir * G3, False), Bop, dwp, IN)
+                for d in range(ndir):
+                    dw = torch.empty(G3, IN, device=dev)
+                    _lib.call("b2p_conv_weight_permute", _p(dwp, d * G3 * IN), _p(dw), G3, C, ktaps, 1, _st())
+                    grads[4 * d] = dw
+            if ctx.needs_input_grad[0]:
+                dA = torch.empty(B * T, IN, device=dev)
+                gemm(B * T, IN, ndir * G3, op(dgi, 0, ndir * G3, True), op(wperm, 0, IN, False), dA, IN)
+                dx = torch.empty(B, L, C, device=dev)
+                _lib.call("b2p_unfold_col2im", _p(dA), None, _p(dx), B, L, C, T, ktaps, stride, _st())
+        else:
+            for d in range(ndir):
+                if ctx.needs_input_grad[5 + 4 * d]:
+                    dw = torch.empty(G3, IN, device=dev)
+                    gemm(G3, IN, B * T, op(dgi, d * G3, ndir * G3, False), op(x, 0, IN, False), dw, IN)
+                    grads[4 * d] = dw
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty(B, T, IN, device=dev)
+                for d in range(ndir):
+                    gemm(B * T, IN, G3, op(dgi, d * G3, ndir * G3, True), op(wih[d], 0, IN, False), dx, IN,
+                         beta=0.0 if d == 0 else 1.0)
+        return (dx, None, None, None, dh0, *grads)
+
+
+class _OffsetView:
+    """Pointer + offset stand-in for the colsum helper (avoids non-contiguous torch views)."""
+
+    def __init__(self, t, off):
+        self.t, self.off = t, off
+
+    def data_ptr(self):
+        return self.t.data_ptr() + 4 * self.off
+
+
+def _view_off(t, off):
+    return _OffsetView(t, off)
+
+
+def gru_layer(x, H, ndir, weights, h0=None):
+    """One nn.GRU layer (both directions) — brain_feature_extractor.py:39-47,61-65.
+    x: (B,T,IN) tensor or Unfolded; weights: [w_ih, w_hh, b_ih, b_hh] per direction."""
+    if isinstance(x, Unfolded):
+        return _GRULayer.apply(x.src, (x.kernel, x.stride), H, ndir, h0, *weights)
+    return _GRULayer.apply(x, None, H, ndir, h0, *weights)
+
+
+# =====================================================================================
+# Linear / dropout
+# =====================================================================================
+class _Linear(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, W, b, act):
+        _chk(x, "linear.x")
+        _chk(W, "linear.W")
+        N, K = W.shape
+        out = torch.empty(*x.shape[:-1], N, device=x.device)
+        pre = torch.empty_like(out) if act else None
+        mm_nt(x, W, out, bias=b, act=act, pre_out=pre)
+        ctx.save_for_backward(x, W, pre)
+        ctx.act = act
+        ctx.has_b = b is not None
+        return out
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, W, pre = ctx.saved_tensors
+        dy = dy.contiguous()
+        N, K = W.shape
+        if ctx.act:
+            dy = _act_bwd(dy, pre, ctx.act)
+        dx = dW = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            mm_nn(dy, W, dx)
+        if ctx.needs_input_grad[1]:
+            dW = torch.empty_like(W)
+            mm_tn(dy, x, dW)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            db = torch.empty(N, device=x.device)
+            colsum(dy, dy.numel() // N, N, db)
+        return dx, dW, db, None
+
+
+def linear(x, W, b=None, act=0):
+    return _Linear.apply(x.contiguous(), W, b, act)
+
+
+class _Dropout(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, p, seed):
+        ctx.p, ctx.seed = p, seed
+        return _dropout_raw(x.contiguous(), p, seed)
+
+    @staticmethod
+    def backward(ctx, dy):
+        return _dropout_raw(dy.contiguous(), ctx.p, ctx.seed), None, None
+
+
+def dropout(x, p, training):
+    if not training or p <= 0.0:
+        return x
+    return _Dropout.apply(x, float(p), SEEDS.next())
+
+
+# =====================================================================================
+# Wav2Vec2 positional conv embedding + residual + LayerNorm + dropout
+# =====================================================================================
+class _PosConvLN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, seed):
+        _chk(e, "pos_conv.x")
+        B, T, D = e.shape
+        O, Ig, K = wv.shape            # (D, D/groups, k)
+        dev = e.device
+        ws = torch.empty(int(_lib.load().b2p_weight_norm_workspace(O, Ig, K)), device=dev)
+        w = torch.empty_like(wv)
+        norms = torch.empty(K, device=dev)
+        _lib.call("b2p_weight_norm_fwd", _p(wg), _p(wv), _p(w), _p(norms), O, Ig, K, _p(ws), _st())
+        wp = torch.empty(O, K * Ig, device=dev)         # wp[o][tap*Ig + i]
+        _lib.call("b2p_conv_weight_permute", _p(w), _p(wp), O, Ig, K, 0, _st())
+        pre = torch.empty_like(e)
+        xsum = torch.empty_like(e)
+        pad = K // 2
+        Og = O // groups
+        A = conv_op(e, 0, D, T, T, 1, pad, Ig, T * D, True, bs1=Ig)
+        gemm(B * T, Og, K * Ig, A, op(wp, 0, K * Ig, True, bs1=Og * K * Ig), xsum, D, cbs1=Og, nz1=groups,
+             bias=cbias, biasbs1=Og, pre_out=pre, act=ACT["gelu"], residual=e, rbs1=Og, ldr=D)
+        y, mean, rstd = _ln_fwd(xsum.view(B * T, D), ln_g, ln_b, eps, drop_p, seed)
+        ctx.save_for_backward(e, wg, wv, w, norms, pre, xsum, ln_g, mean, rstd)
+        ctx.meta = (groups, drop_p, seed, B, T, D, O, Ig, K)
+        return y.view(B, T, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        e, wg, wv, w, norms, pre, xsum, ln_g, mean, rstd = ctx.saved_tensors
+        groups, drop_p, seed, B, T, D, O, Ig, K = ctx.meta
+        dev = e.device
+        dy = dy.contiguous().view(B * T, D)
+        dxsum, dlg, dlb, _ = _ln_bwd(dy, xsum.view(B * T, D), ln_g, mean, rstd, True, None, drop_p, seed)
+        dpre = _act_bwd(dxsum, pre.view(B * T, D), ACT["gelu"])
+        Og = O // groups
+        pad = K // 2
+        dcb = torch.empty(O, device=dev)
+        colsum(dpre, B * T, D, dcb)
+        dg = dv = None
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            # dwp[g*Og+o][tap*Ig+i] = sum_r dpre[r][g*Og+o] * e[b, t+tap-pad, g*Ig+i]
+            dwp = torch.empty(O, K * Ig, device=dev)
+            Bop = conv_op(e, 0, D, T, T, 1, pad, Ig, T * D, False, bs1=Ig)
+            gemm(Og, K * Ig, B * T, op(dpre, 0, D, False, bs1=Og), Bop, dwp, K * Ig, cbs1=Og * K * Ig, nz1=groups)
+            dw = torch.empty_like(wv)
+            _lib.call("b2p_conv_weight_permute", _p(dwp), _p(dw), O, Ig, K, 1, _st())
+            ws = torch.empty(int(_lib.load().b2p_weight_norm_workspace(O, Ig, K)), device=dev)
+            dg = torch.empty_like(wg)
+            dv = torch.empty_like(wv)
+            _lib.call("b2p_weight_norm_bwd", _p(wg), _p(wv), _p(norms), _p(dw), _p(dg), _p(dv), O, Ig, K, _p(ws),
+                      _st())
+        de = None
+        if ctx.needs_input_grad[0]:
+            # de[b,s,g*Ig+i] = dxsum + sum_{k',o} dpre[b, s+k'-(K-1-pad), g*Og+o] * wt[g][i][k'*Og+o]
+            wt = torch.empty(groups, Ig, K * Og, device=dev)
+            _lib.call("b2p_conv_weight_transpose_flip", _p(w), _p(wt), groups, Og, Ig, K, _st())
+            de = torch.empty(B, T, D, device=dev)
+            A = conv_op(dpre, 0, D, T, T, 1, K - 1 - pad, Og, T * D, True, bs1=Og)
+            gemm(B * T, Ig, K * Og, A, op(wt, 0, K * Og, True, bs1=Ig * K * Og), de, D, cbs1=Ig, nz1=groups,
+                 residual=dxsum, rbs1=Ig, ldr=D)
+        return de, dg, dv, dcb, dlg, dlb, None, None, None, None
+
+
+def pos_conv_ln(e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, training):
+    p = drop_p if training else 0.0
+    return _PosConvLN.apply(e.contiguous(), wg, wv, cbias, ln_g, ln_b, groups, eps, p, SEEDS.next() if p > 0 else 0)
+
+
+# =====================================================================================
+# post-LN transformer encoder layer (Wav2Vec2EncoderLayer)
+# =====================================================================================
+class _EncoderLayer(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, cfg, wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
+        nh, eps, p_attn, p_hid, p_act, seeds = cfg
+        _chk(x, "encoder_layer.x")
+        B, T, D = x.shape
+        dh = D // nh
+        NT = B * T
+        F = w1.shape[0]
+        dev = x.device
+        Tp = (T + 3) // 4 * 4
+        scale = dh ** -0.5
+        x2 = x.view(NT, D)
+        qkv = torch.empty(NT, 3 * D, device=dev)
+        for i, (w, b) in enumerate(((wq, bq), (wk, bk), (wv, bv))):
+            gemm(NT, D, D, op(x2, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=b)
+        # scores S[b,h] = Q K^T * scale
+        S = torch.empty(B, nh, T, Tp, device=dev)
+        gemm(T, T, dh, op(qkv, 0, 3 * D, True, bs1=T * 3 * D, bs2=dh), op(qkv, D, 3 * D, True, bs1=T * 3 * D, bs2=dh),
+             S, Tp, cbs1=nh * T * Tp, cbs2=T * Tp, nz1=B, nz2=nh, alpha=scale)
+        P = torch.empty_like(S)
+        Pd = torch.empty_like(S) if p_attn > 0 else P
+        _lib.call("b2p_softmax_fwd", _p(S), _p(P), _p(Pd), B * nh * T, T, Tp, float(p_attn), seeds[0], _st())
+        del S
+        # O[b,t,h,:] = Pd[b,h] @ V[b,:,h,:]
+        O = torch.empty(NT, D, device=dev)
+        gemm(T, dh, T, op(Pd, 0, Tp, True, bs1=nh * T * Tp, bs2=T * Tp),
+             op(qkv, 2 * D, 3 * D, False, bs1=T * 3 * D, bs2=dh), O, D, cbs1=T * D, cbs2=dh, nz1=B, nz2=nh)
+        # y1 = x + dropout(O Wo^T + bo)
+        y1 = torch.empty(NT, D, device=dev)
+        gemm(NT, D, D, op(O, 0, D, True), op(wo, 0, D, True), y1, D, bias=bo, drop_p=p_hid, seed=seeds[1],
+             residual=x2)
+        x1, m1, r1 = _ln_fwd(y1, g1, be1, eps)
+        # FFN: f = dropout(gelu(x1 W1^T + b1)); y2 = x1 + dropout(f W2^T + b2)
+        pre = torch.empty(NT, F, device=dev)
+        f = torch.empty(NT, F, device=dev)
+        gemm(NT, F, D, op(x1, 0, D, True), op(w1, 0, D, True), f, F, bias=b1, pre_out=pre, act=ACT["gelu"],
+             drop_p=p_act, seed=seeds[2])
+        y2 = torch.empty(NT, D, device=dev)
+        gemm(NT, D, F, op(f, 0, F, True), op(w2, 0, F, True), y2, D, bias=b2, drop_p=p_hid, seed=seeds[3],
+             residual=x1)
+        out, m2, r2 = _ln_fwd(y2, g2, be2, eps)
+        ctx.save_for_backward(x, qkv, P, Pd if p_attn > 0 else None, O, y1, x1, m1, r1, pre, f, y2, m2, r2,
+                              wq, wk, wv, wo, g1, w1, w2, g2)
+        ctx.cfg = cfg
+        ctx.has_b = [b is not None for b in (bq, bk, bv, bo, b1, b2)]
+        return out.view(B, T, D)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x, qkv, P, Pd, O, y1, x1, m1, r1, pre, f, y2, m2, r2, wq, wk, wv, wo, g1, w1, w2, g2) = ctx.saved_tensors
+        nh, eps, p_attn, p_hid, p_act, seeds = ctx.cfg
+        if Pd is None:
+            Pd = P
+        B, T, D = x.shape
+        dh = D // nh
+        NT = B * T
+        F = w1.shape[0]
+        dev = x.device
+        Tp = P.shape[-1]
+        scale = dh ** -0.5
+        ng = ctx.needs_input_grad
+        dout = dout.contiguous().view(NT, D)
+        x2 = x.view(NT, D)
+        # LN2 backward -> dy2 ; dz2 = dropout-mask(dy2) (output dropout of the FFN)
+        dy2, dg2, dbe2, dz2 = _ln_bwd(dout, y2, g2, m2, r2, True, in_drop_p=p_hid, in_seed=seeds[3])
+        dw2 = torch.empty_like(w2) if ng[14] else None
+        if dw2 is not None:
+            mm_tn(dz2, f, dw2)
+        db2 = torch.empty(D, device=dev) if ng[15] else None
+        if db2 is not None:
+            colsum(dz2, NT, D, db2)
+        # dpre = (dz2 W2) * mask_act * gelu'(pre)
+        dpre = torch.empty(NT, F, device=dev)
+        gemm(NT, F, D, op(dz2, 0, D, True), op(w2, 0, F, False), dpre, F, drop_p=p_act, seed=seeds[2],
+             act_bwd=ACT["gelu"], aux=pre)
+        dw1 = torch.empty_like(w1) if ng[12] else None
+        if dw1 is not None:
+            mm_tn(dpre, x1, dw1)
+        db1 = torch.empty(F, device=dev) if ng[13] else None
+        if db1 is not None:
+            colsum(dpre, NT, F, db1)
+        # dx1 = dpre W1 + dy2
+        dx1 = torch.empty(NT, D, device=dev)
+        gemm(NT, D, F, op(dpre, 0, F, True), op(w1, 0, D, False), dx1, D, residual=dy2)
+        del dpre
+        # LN1 backward -> dy1 ; dz1 = dropout-mask(dy1) (attention output dropout)
+        dy1, dg1, dbe1, dz1 = _ln_bwd(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1])
+        dwo = torch.empty_like(wo) if ng[8] else None
+        if dwo is not None:
+            mm_tn(dz1, O, dwo)
+        dbo = torch.empty(D, device=dev) if ng[9] else None
+        if dbo is not None:
+            colsum(dz1, NT, D, dbo)
+        dO = torch.empty(NT, D, device=dev)
+        mm_nn(dz1, wo, dO)
+        # attention backward
+        dPd = torch.empty(B, nh, T, Tp, device=dev)
+        gemm(T, T, dh, op(dO, 0, D, True, bs1=T * D, bs2=dh), op(qkv, 2 * D, 3 * D, True, bs1=T * 3 * D, bs2=dh),
+             dPd, Tp, cbs1=nh * T * Tp, cbs2=T * Tp, nz1=B, nz2=nh)
+        dqkv = torch.empty(NT, 3 * D, device=dev)
+        # dV = Pd^T dO
+        gemm(T, dh, T, op(Pd, 0, Tp, False, bs1=nh * T * Tp, bs2=T * Tp), op(dO, 0, D, False, bs1=T * D, bs2=dh),
+             dqkv, 3 * D, c_off=2 * D, cbs1=T * 3 * D, cbs2=dh, nz1=B, nz2=nh)
+        dS = torch.empty_like(dPd)
+        _lib.call("b2p_softmax_bwd", _p(P), _p(dPd), _p(dS), B * nh * T, T, Tp, float(p_attn), seeds[0], _st())
+        del dPd
+        # dQ = dS K * scale ; dK = dS^T Q * scale
+        gemm(T, dh, T, op(dS, 0, Tp, True, bs1=nh * T * Tp, bs2=T * Tp),
+             op(qkv, D, 3 * D, False, bs1=T * 3 * D, bs2=dh), dqkv, 3 * D, c_off=0, cbs1=T * 3 * D, cbs2=dh,
+             nz1=B, nz2=nh, alpha=scale)
+        gemm(T, dh, T, op(dS, 0, Tp, False, bs1=nh * T * Tp, bs2=T * Tp),
+             op(qkv, 0, 3 * D, False, bs1=T * 3 * D, bs2=dh), dqkv, 3 * D, c_off=D, cbs1=T * 3 * D, cbs2=dh,
+             nz1=B, nz2=nh, alpha=scale)
+        del dS
+        grads_w = []
+        for i, w in enumerate((wq, wk, wv)):
+            gw = gb = None
+            if ng[2 + 2 * i]:
+                gw = torch.empty_like(w)
+                gemm(D, D, NT, op(dqkv, i * D, 3 * D, False), op(x2, 0, D, False), gw, D)
+            if ctx.has_b[i] and ng[3 + 2 * i]:
+                gb = torch.empty(D, device=dev)
+                colsum(_view_off(dqkv, i * D), NT, D, gb, ld=3 * D)
+            grads_w += [gw, gb]
+        dx = None
+        if ng[0]:
+            dx = torch.empty(NT, D, device=dev)
+            for i, w in enumerate((wq, wk, wv)):
+                gemm(NT, D, D, op(dqkv, i * D, 3 * D, True), op(w, 0, D, False), dx, D,
+                     residual=dy1 if i == 0 else None, beta=0.0 if i == 0 else 1.0)
+            dx = dx.view(B, T, D)
+        return (dx, None, *grads_w, dwo, dbo, dg1, dbe1, dw1, db1, dw2, db2, dg2, dbe2)
+
+
+def encoder_layer(x, params, nh, eps, p_attn, p_hid, p_act, training):
+    if not training:
+        p_attn = p_hid = p_act = 0.0
+    seeds = tuple(SEEDS.next() for _ in range(4)) if training else (0, 0, 0, 0)
+    cfg = (nh, eps, float(p_attn), float(p_hid), float(p_act), seeds)
+    return _EncoderLayer.apply(x.contiguous(), cfg, *params)
+
+
+# =====================================================================================
+# CTC
+# =====================================================================================
+class _CTC(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, in_lens, tgt_lens, blank):
+        _chk(logits, "ctc.logits")
+        B, T, C = logits.shape
+        S = targets.shape[1]
+        dev = logits.device
+        ws = torch.empty(int(_lib.load().b2p_ctc_workspace(B, T, S, C)), device=dev)
+        nll = torch.empty(B, device=dev)
+        loss = torch.empty((), device=dev)
+        grad = torch.empty_like(logits)
+        _lib.call("b2p_ctc_fwd_bwd", _p(logits), targets.data_ptr(), in_lens.data_ptr(), tgt_lens.data_ptr(), B, T,
+                  S, C, blank, _p(nll), _p(loss), _p(grad), _p(ws), _st())
+        ctx.save_for_backward(grad)
+        ctx.nll = nll
+        return loss
+
+    @staticmethod
+    def backward(ctx, gout):
+        (grad,) = ctx.saved_tensors
+        return grad * gout, None, None, None, None
+
+
+def ctc_loss(logits, targets, in_lens, tgt_lens, blank=0):
+    """log_softmax(logits) -> nn.CTCLoss(blank, reduction='mean', zero_infinity=True);
+    logits (B,T,C) batch-first. targets int64 (B,S); in_lens int32; tgt_lens int64."""
+    targets = targets.to(torch.int64).contiguous()
+    in_lens = in_lens.to(torch.int32).contiguous()
+    tgt_lens = tgt_lens.to(torch.int64).contiguous()
+    return _CTC.apply(logits.contiguous(), targets, in_lens, tgt_lens, blank)
