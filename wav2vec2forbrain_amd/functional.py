@@ -27,11 +27,17 @@ from ._lib import GemmDesc, Operand, Epilogue
 
 ACT = {"none": 0, None: 0, "gelu": 1, "softsign": 2, "silu": 3, "swish": 3}
 
-_state = threading.local()
+class _State:
+    # process-global (autograd runs backward on its own worker thread, so a thread-local
+    # setting would not reach the backward GEMMs)
+    prec = 0
+
+
+_state = _State()
 
 
 def _prec() -> int:
-    return getattr(_state, "prec", 0)
+    return _state.prec
 
 
 @contextlib.contextmanager

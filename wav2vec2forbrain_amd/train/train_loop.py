@@ -1,0 +1,128 @@
+"""Trainer — mirrors reference src/train/train_loop.py:14-220 (the per-batch body :41-84 is the
+hot path; W&B logging is not available offline and is omitted). Data-parallel when
+torch.distributed is initialised: gradients of the optimised parameters are all-reduced by
+train.ddp.GradBucketReducer overlapped with backward."""
+from __future__ import annotations
+
+import os
+import uuid
+from typing import Literal, cast
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+from ..datasets.batch_types import SampleBatch
+from .ddp import GradBucketReducer, unused_param_names
+from .evaluator import EpochResult
+
+
+class Trainer:
+    def __init__(self, experiment):
+        self.experiment = experiment
+        self.config = experiment.base_config
+        self.dataloader_train = experiment.dataloader_train
+        self.dataloader_val = experiment.dataloader_val
+        self.dataloader_test = experiment.dataloader_test
+        self.model = experiment.model
+        self.optimizer = experiment.create_optimizer()
+        self.scheduler = experiment.get_scheduler(self.optimizer)
+        self.reducer = None
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            skip = unused_param_names(self.model)
+            opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
+            params = [p for n, p in self.model.named_parameters() if id(p) in opt_ids and n not in skip]
+            self.reducer = GradBucketReducer(params)
+
+    def _log_intermediate(self, batch: int, n_batches: int, evaluator):
+        print(f"Batch {batch + 1}/{n_batches} loss: {evaluator.get_latest_loss():.2f} "
+              f"running: {evaluator.get_running_loss():.2f}\r", end="")
+
+    def train_step(self, batch: SampleBatch):
+        """One step of the reference loop body (:42-79): zero_grad, (no-op noise), forward,
+        backward, [DP all-reduce], optional clip, optimizer step."""
+        self.optimizer.zero_grad()
+        if self.config.whiteNoiseSD > 0:       # reference :46-52: computed and discarded
+            _ = torch.randn(batch.input.shape, device=batch.input.device) * self.config.whiteNoiseSD
+        if self.config.constantOffsetSD > 0:   # reference :54-62: computed and discarded
+            inp = batch.input
+            _ = torch.randn([inp.shape[0], 1, inp.shape[2]], device=inp.device) * self.config.constantOffsetSD
+        with torch.enable_grad():
+            outputs = self.model.forward(batch)
+        loss = cast(torch.Tensor, outputs.loss)
+        loss.backward()
+        if self.reducer is not None:
+            self.reducer.finish()
+        if self.config.gradient_clipping is not None:
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.gradient_clipping)
+        self.optimizer.step()
+        return outputs
+
+    def _train_epoch(self, data_loader):
+        self.model.train()
+        evaluator = self.experiment.create_evaluator("train")
+        for i, batch in enumerate(data_loader):
+            batch = cast(SampleBatch, batch).cuda()
+            outputs = self.train_step(batch)
+            evaluator.track_batch(outputs, batch)
+            if i % self.config.log_every_n_batches == self.config.log_every_n_batches - 1:
+                self._log_intermediate(i, len(data_loader), evaluator)
+        results = evaluator.evaluate()
+        evaluator.clean_up()
+        return results
+
+    def _evaluate_epoch(self, mode: Literal["val", "test"]):
+        dataloader = self.dataloader_val if mode == "val" else self.dataloader_test
+        self.model.eval()
+        evaluator = self.experiment.create_evaluator(mode)
+        for i, batch in enumerate(dataloader):
+            batch = cast(SampleBatch, batch).cuda()
+            with torch.no_grad():
+                outputs = self.model.forward(batch)
+            evaluator.track_batch(outputs, batch)
+        results = evaluator.evaluate()
+        evaluator.clean_up()
+        return results
+
+    def train(self):
+        history = []
+        best = float("inf" if self.config.minimize_best_model_metric else "-inf")
+        best_path = os.path.join(self.experiment.cache_dir, "model_checkpoints", str(uuid.uuid4()), "best_model.pt")
+        os.makedirs(os.path.dirname(best_path), exist_ok=True)
+
+        def metric(r: EpochResult):
+            return r.get_average_loss() if self.config.best_model_metric == "loss" else r.metrics[self.config.best_model_metric]
+
+        saved = False
+        for epoch in range(self.config.epochs):
+            print(f"\nEpoch {epoch + 1}/{self.config.epochs}")
+            train_losses = self._train_epoch(self.dataloader_train)
+            val_losses = self._evaluate_epoch("val")
+            self.scheduler.step()
+            print(f"\nFinished Epoch {epoch + 1}/{self.config.epochs} train loss: {train_losses.get_average_loss()} "
+                  f"val loss: {val_losses.get_average_loss()}")
+            history.append((train_losses, val_losses))
+            if self.config.return_best_model:
+                cur = metric(val_losses)
+                better = cur < best if self.config.minimize_best_model_metric else cur > best
+                if better:
+                    best = cur
+                    torch.save(self.model.state_dict(), best_path)
+                    saved = True
+            if self.config.early_stopping_patience is not None and len(history) >= self.config.early_stopping_patience:
+                hist = [metric(v) for _, v in history][-self.config.early_stopping_patience:]
+                if self.config.minimize_best_model_metric:
+                    hist[0] -= self.config.early_stopping_delta
+                else:
+                    hist[0] += self.config.early_stopping_delta
+                bi = np.argmin(hist) if self.config.minimize_best_model_metric else np.argmax(hist)
+                if bi == 0:
+                    print(f"\nEarly stopping after {epoch} epochs")
+                    break
+        if self.config.return_best_model and saved:
+            self.model.load_state_dict(torch.load(best_path, weights_only=True))
+            os.remove(best_path)
+            os.rmdir(os.path.dirname(best_path))
+        test_losses = self._evaluate_epoch("test")
+        print(f"\nTest loss: {test_losses.get_average_loss()}")
+        return self.model, (history, test_losses)
