@@ -30,6 +30,9 @@ typedef void* b2p_stream_t; /* hipStream_t */
 /* ------------------------------------------------------------------ library */
 const char* b2p_last_error(void);
 int b2p_version(void);
+/* sizeof(b2p_operand), sizeof(b2p_epilogue), sizeof(b2p_gemm_desc): lets a binding verify its
+ * struct layouts against the compiled library. */
+int b2p_abi_sizes(int64_t* out3);
 /* optional per-kernel-family HIP-event timing (bench.py roofline): family ids in
  * wav2vec2forbrain_amd/_lib.py. enable=0 turns it off. */
 int b2p_timing_enable(int family, int max_events);
@@ -91,6 +94,12 @@ typedef struct {
   int32_t precision;          /* 0 = bf16 MFMA, 1 = fp32 MFMA (parity mode)                   */
   int32_t timing_family;      /* tag for b2p_timing_* (0 = untagged)                          */
   double flops;               /* algorithmic FLOPs of this launch (for timing)                */
+  /* split-K (deterministic): ksplit > 1 slices K into kchunk-sized ranges (multiple of 32) whose
+   * fp32 partials go to workspace (>= ksplit*nz1*nz2*M*N floats) and are summed in slice order by
+   * a reduce kernel; epilogue limited to alpha/beta. For under-filled grids (weight gradients). */
+  int32_t ksplit, kchunk;
+  float* workspace;
+  int64_t workspace_floats;
 } b2p_gemm_desc;
 
 int b2p_gemm(const b2p_gemm_desc* d, b2p_stream_t stream);
@@ -117,12 +126,13 @@ int b2p_layernorm_fwd(const float* x, const float* gamma, const float* beta, flo
 int64_t b2p_layernorm_bwd_workspace(int64_t rows, int64_t cols);
 /* dy is the gradient of the (optionally dropped-out, drop_p/drop_seed) LN output; dx (+)= dx_accum.
  * If dx_dropped != NULL it also receives dx * mask(in_drop_seed)/(1-in_drop_p): the gradient of
- * the residual-branch dropout whose output fed this LayerNorm (post-LN encoder layers). */
+ * the residual-branch dropout whose output fed this LayerNorm (post-LN encoder layers), and, if
+ * dbias_in != NULL, its column sums (= the bias gradient of the Linear feeding that dropout). */
 int b2p_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
                       const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
                       int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
-                      float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* workspace,
-                      b2p_stream_t stream);
+                      float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
+                      float* workspace, b2p_stream_t stream);
 
 /* Row softmax for attention scores (eager_attention_forward: softmax(QK^T*scale) + dropout).
  * S rows of length n (row stride ld). Writes P (pre-dropout) and Pd (dropped, scaled). */

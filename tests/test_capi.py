@@ -35,11 +35,14 @@ def test_binding_covers_header():
 
 
 def test_struct_layout_matches_c():
+    import numpy as np
     from wav2vec2forbrain_amd import _lib
-    # sizes fixed by the C structs (include/b2p_hip.h), x86-64 SysV alignment
-    assert ctypes.sizeof(_lib.Operand) == 8 * 5 + 4 * 8 + 8
-    assert ctypes.sizeof(_lib.GemmDesc) == 3 * 8 + 8 + 2 * ctypes.sizeof(_lib.Operand) + \
-        ctypes.sizeof(_lib.Epilogue) + 8 + 8
+    out = np.zeros(3, dtype=np.int64)
+    _lib.call("b2p_abi_sizes", out.ctypes.data)
+    assert list(out) == [ctypes.sizeof(_lib.Operand), ctypes.sizeof(_lib.Epilogue), ctypes.sizeof(_lib.GemmDesc)]
+    for cls in (_lib.Operand, _lib.Epilogue, _lib.GemmDesc):
+        for name, _ in cls._fields_:
+            assert getattr(cls, name).offset % 4 == 0
 
 
 def test_argument_validation_without_device():

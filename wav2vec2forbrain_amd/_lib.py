@@ -50,6 +50,7 @@ class GemmDesc(ctypes.Structure):
         ("M", c_i64), ("N", c_i64), ("K", c_i64), ("nz1", c_i32), ("nz2", c_i32),
         ("A", Operand), ("B", Operand), ("ep", Epilogue),
         ("precision", c_i32), ("timing_family", c_i32), ("flops", c_f64),
+        ("ksplit", c_i32), ("kchunk", c_i32), ("workspace", c_p), ("workspace_floats", c_i64),
     ]
 
 
@@ -57,6 +58,7 @@ class GemmDesc(ctypes.Structure):
 _SIGS = {
     "b2p_last_error": (ctypes.c_char_p, []),
     "b2p_version": (c_i32, []),
+    "b2p_abi_sizes": (c_i32, [c_p]),
     "b2p_timing_enable": (c_i32, [c_i32, c_i32]),
     "b2p_timing_read": (c_i32, [c_i32, ctypes.POINTER(c_f32), ctypes.POINTER(c_i32), ctypes.POINTER(c_f64)]),
     "b2p_gemm": (c_i32, [ctypes.POINTER(GemmDesc), c_p]),
@@ -67,7 +69,7 @@ _SIGS = {
     "b2p_layernorm_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_u64, c_p]),
     "b2p_layernorm_bwd_workspace": (c_i64, [c_i64, c_i64]),
     "b2p_layernorm_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_f32, c_u64,
-                                  c_p, c_f32, c_u64, c_p, c_p]),
+                                  c_p, c_f32, c_u64, c_p, c_p, c_p]),
     "b2p_softmax_fwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_u64, c_p]),
     "b2p_softmax_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_u64, c_p]),
     "b2p_act_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p]),

@@ -5,25 +5,31 @@
 #include "../../include/b2p_hip.h"
 
 namespace {
-constexpr int kColsumRows = 64;   // rows summed per block in phase 1
+constexpr int kColsumRows = 256;  // rows per block in phase 1 (64 columns x 4 row lanes)
 
-// out[b][n] (+)= sum_m f(X[b][m][n]) ; mode 0: x, 1: x*x, 2: x*Y
-__global__ void colsum_p1(const float* __restrict__ X, const float* __restrict__ Y, int64_t M,
-                          int64_t N, int64_t ld, int64_t bstride, int mode, float* __restrict__ part,
-                          int nblk) {
-  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// part[b][blk][n] = sum_{m in block rows} f(X[b][m][n]) ; mode 0: x, 1: x*x, 2: x*Y
+__global__ void __launch_bounds__(256) colsum_p1(const float* __restrict__ X, const float* __restrict__ Y,
+                                                 int64_t M, int64_t N, int64_t ld, int64_t bstride, int mode,
+                                                 float* __restrict__ part, int nblk) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + c;
   const int blk = blockIdx.y, b = blockIdx.z;
-  if (n >= N) return;
   const int64_t m0 = (int64_t)blk * kColsumRows;
   const int64_t m1 = m0 + kColsumRows < M ? m0 + kColsumRows : M;
-  const float* xp = X + b * bstride + n;
-  const float* yp = Y ? Y + b * bstride + n : nullptr;
   float s = 0.f;
-  for (int64_t m = m0; m < m1; ++m) {
-    const float x = xp[m * ld];
-    s += mode == 0 ? x : (mode == 1 ? x * x : x * yp[m * ld]);
+  if (n < N) {
+    const float* xp = X + b * bstride + n;
+    const float* yp = Y ? Y + b * bstride + n : nullptr;
+#pragma unroll 8
+    for (int64_t m = m0 + rl; m < m1; m += 4) {
+      const float x = xp[m * ld];
+      s += mode == 0 ? x : (mode == 1 ? x * x : x * yp[m * ld]);
+    }
   }
-  part[((int64_t)b * nblk + blk) * N + n] = s;
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) part[((int64_t)b * nblk + blk) * N + n] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
 __global__ void colsum_p2(const float* __restrict__ part, int nblk, int64_t N, float* __restrict__ out,
@@ -42,7 +48,7 @@ int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_
                 int64_t bstride, int mode, float* out, int accumulate, float* part, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   const int nblk = (int)((M + kColsumRows - 1) / kColsumRows);
-  dim3 g1((unsigned)((N + 255) / 256), nblk, (unsigned)batch);
+  dim3 g1((unsigned)((N + 63) / 64), nblk, (unsigned)batch);
   hipLaunchKernelGGL(colsum_p1, g1, dim3(256), 0, st, X, Y, M, N, ld, bstride, mode, part, nblk);
   dim3 g2((unsigned)((N + 255) / 256), (unsigned)batch);
   hipLaunchKernelGGL(colsum_p2, g2, dim3(256), 0, st, part, nblk, N, out, accumulate);
@@ -116,7 +122,7 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
   }
 }
 
-constexpr int LN_BWD_ROWS = 32;   // rows per block (8 per wave)
+constexpr int LN_BWD_ROWS = 128;  // rows per block (32 per wave)
 __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, const float* __restrict__ x,
                                                 const float* __restrict__ gamma, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, float* __restrict__ dx,
@@ -124,13 +130,15 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
                                                 int64_t rows, int cols, uint32_t thr, float dscale, uint64_t seed,
                                                 float drop_p, float* __restrict__ dxd, uint32_t thr2, float dscale2,
                                                 uint64_t seed2) {
-  __shared__ float red[4][2][LN_MAXV * 256];   // not all used; cols <= 2048
+  __shared__ float red[4][3][LN_MAXV * 256];   // cols <= 1024
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = cols >> 2;
   const float4* g4 = reinterpret_cast<const float4*>(gamma);
-  float4 dg[LN_MAXV], db[LN_MAXV];
+  float4 dg[LN_MAXV], db[LN_MAXV], dd[LN_MAXV];
 #pragma unroll
-  for (int i = 0; i < LN_MAXV; ++i) { dg[i] = make_float4(0, 0, 0, 0); db[i] = make_float4(0, 0, 0, 0); }
+  for (int i = 0; i < LN_MAXV; ++i) {
+    dg[i] = make_float4(0, 0, 0, 0); db[i] = make_float4(0, 0, 0, 0); dd[i] = make_float4(0, 0, 0, 0);
+  }
   for (int rr = 0; rr < LN_BWD_ROWS / 4; ++rr) {
     const int64_t row = (int64_t)blockIdx.x * LN_BWD_ROWS + wave * (LN_BWD_ROWS / 4) + rr;
     if (row >= rows) break;
@@ -183,6 +191,7 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
           q.z = b2p_keep(seed2, base + 2, thr2) ? o.z * dscale2 : 0.f;
           q.w = b2p_keep(seed2, base + 3, thr2) ? o.w * dscale2 : 0.f;
           reinterpret_cast<float4*>(dxd + row * cols)[c] = q;
+          dd[i].x += q.x; dd[i].y += q.y; dd[i].z += q.z; dd[i].w += q.w;
         }
       }
     }
@@ -194,25 +203,27 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
     if (c < nv) {
       reinterpret_cast<float4*>(red[wave][0])[c] = dg[i];
       reinterpret_cast<float4*>(red[wave][1])[c] = db[i];
+      reinterpret_cast<float4*>(red[wave][2])[c] = dd[i];
     }
   }
   __syncthreads();
   for (int c = threadIdx.x; c < cols; c += 256) {
-    const float a = red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c];
-    const float b = red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c];
-    part[(int64_t)blockIdx.x * 2 * cols + c] = a;
-    part[(int64_t)blockIdx.x * 2 * cols + cols + c] = b;
+#pragma unroll
+    for (int q = 0; q < 3; ++q)
+      part[((int64_t)blockIdx.x * 3 + q) * cols + c] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
   }
 }
 
 __global__ void ln_bwd_reduce(const float* __restrict__ part, int nblk, int cols, float* __restrict__ dgamma,
-                              float* __restrict__ dbeta) {
+                              float* __restrict__ dbeta, float* __restrict__ dbias_in) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= 2 * cols) return;
+  if (c >= 3 * cols) return;
+  const int q = c / cols, cc = c - q * cols;
+  float* dst = q == 0 ? dgamma : (q == 1 ? dbeta : dbias_in);
+  if (!dst) return;
   float s = 0.f;
-  for (int i = 0; i < nblk; ++i) s += part[(int64_t)i * 2 * cols + c];
-  if (c < cols) { if (dgamma) dgamma[c] = s; }
-  else { if (dbeta) dbeta[c - cols] = s; }
+  for (int i = 0; i < nblk; ++i) s += part[((int64_t)i * 3 + q) * cols + cc];
+  dst[cc] = s;
 }
 
 // ------------------------------------------------------------------ attention softmax
@@ -455,14 +466,14 @@ extern "C" int b2p_layernorm_fwd(const float* x, const float* gamma, const float
 }
 
 extern "C" int64_t b2p_layernorm_bwd_workspace(int64_t rows, int64_t cols) {
-  return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 2 * cols;
+  return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 3 * cols;
 }
 
 extern "C" int b2p_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
                                  const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
                                  int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
-                                 float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* workspace,
-                                 b2p_stream_t stream) {
+                                 float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
+                                 float* workspace, b2p_stream_t stream) {
   B2P_CHECK_ARG(dy && x && gamma && mean && rstd && dx && workspace, "layernorm_bwd: NULL pointer");
   B2P_CHECK_ARG(cols % 4 == 0 && cols <= 64 * 4 * LN_MAXV, "layernorm_bwd: cols must be %%4 and <= 1024");
   if (rows <= 0) return 0;
@@ -472,8 +483,8 @@ extern "C" int b2p_layernorm_bwd(const float* dy, const float* x, const float* g
                      rows, (int)cols, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
                      drop_seed, drop_p, dx_dropped, b2p_dropout_threshold(in_drop_p),
                      in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed);
-  hipLaunchKernelGGL(ln_bwd_reduce, dim3(nblocks(2 * cols)), dim3(256), 0, st, workspace, nblk, (int)cols,
-                     dgamma, dbeta);
+  hipLaunchKernelGGL(ln_bwd_reduce, dim3(nblocks(3 * cols)), dim3(256), 0, st, workspace, nblk, (int)cols,
+                     dgamma, dbeta, dx_dropped ? dbias_in : nullptr);
   B2P_CHECK_LAUNCH();
   return 0;
 }

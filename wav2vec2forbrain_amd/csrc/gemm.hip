@@ -29,16 +29,6 @@ __device__ __forceinline__ int64_t batch_off(const b2p_operand& o, int z1, int z
   return i1 * o.bs1 + (int64_t)z2 * o.bs2;
 }
 
-__device__ __forceinline__ float4 ld4_guard(const float* p, int valid) {
-  // valid: number of leading elements that may be read (0..4)
-  if (valid >= 4) return *reinterpret_cast<const float4*>(p);
-  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (valid > 0) r.x = p[0];
-  if (valid > 1) r.y = p[1];
-  if (valid > 2) r.z = p[2];
-  return r;
-}
-
 // Precision traits -----------------------------------------------------------------
 template <int PREC> struct Prec;
 template <> struct Prec<0> {   // bf16 MFMA
@@ -78,7 +68,7 @@ struct Loader {
   int64_t mnoff;        // !INNER_K: fixed inner offset (mn) part
   int mnvalid;          // number of valid inner elements at this thread's chunk
 
-  __device__ __forceinline__ void init(const OpState& s, int tid, int mn0, int MNdim, int Kdim) {
+  __device__ __forceinline__ void init(const OpState& s, int tid, int mn0, int MNdim, int kstart) {
     if constexpr (INNER_K) {
       active = true;
 #pragma unroll
@@ -95,7 +85,7 @@ struct Loader {
           frame0[i] = 0;
         }
       }
-      const int kk = (tid & 7) * 4;
+      const int kk = kstart + (tid & 7) * 4;
       if constexpr (CONV) { tap = kk / s.Cg; ch = kk - tap * s.Cg; } else { tap = 0; ch = kk; }
     } else {
       // R/4 mn-chunks x 8 k-groups of 4
@@ -110,7 +100,7 @@ struct Loader {
         mnoff = (int64_t)(tap - s.pad) * s.ld + ch;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int k = 4 * g + j;   // first k-tile starts at 0
+          const int k = kstart + 4 * g + j;   // first k-tile of this block's K range
           tb[j] = k / s.T_out; tt[j] = k - tb[j] * s.T_out;
         }
       } else {
@@ -119,22 +109,34 @@ struct Loader {
     }
   }
 
+  // Branch-free loads: every lane issues one unconditional 16-B load (from a clamped, always
+  // in-bounds address when the element is outside the operand) and zeroes invalid elements with
+  // selects, so the global loads of a K-step stay in flight together (a per-load branch makes
+  // hipcc wait vmcnt(0) per load). In-bounds guarantee: ld % 4 == 0 => ld >= roundup4(dim).
+  __device__ __forceinline__ static float4 sel4(float4 x, bool ok, int nvalid) {
+    x.x = ok ? x.x : 0.f;
+    x.y = (ok && nvalid > 1) ? x.y : 0.f;
+    x.z = (ok && nvalid > 2) ? x.z : 0.f;
+    x.w = (ok && nvalid > 3) ? x.w : 0.f;
+    return x;
+  }
+
   __device__ __forceinline__ void load(const OpState& s, int tid, int k0, int Kdim) {
     if constexpr (INNER_K) {
       const int kk = k0 + (tid & 7) * 4;
       const int kvalid = Kdim - kk;
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        int valid = rowok[i] ? kvalid : 0;
+        bool ok = rowok[i] && kvalid > 0;
         const float* p;
         if constexpr (CONV) {
           const int f = frame0[i] + tap;
-          if (f < 0 || f >= s.T_in) valid = 0;
-          p = s.base + rowoff[i] + (int64_t)f * s.ld + ch;
+          ok = ok && f >= 0 && f < s.T_in;
+          p = ok ? s.base + rowoff[i] + (int64_t)f * s.ld + ch : s.base;
         } else {
-          p = s.base + rowoff[i] + kk;
+          p = ok ? s.base + rowoff[i] + kk : s.base;
         }
-        v[i] = ld4_guard(p, valid);
+        v[i] = sel4(*reinterpret_cast<const float4*>(p), ok, kvalid);
       }
       if constexpr (CONV) {
         ch += BK;
@@ -147,18 +149,18 @@ struct Loader {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int k = k0 + 4 * g + j;
-        int valid = (k < Kdim) ? mnvalid : 0;
+        bool ok = k < Kdim && mnvalid > 0;
         const float* p;
         if constexpr (CONV) {
           const int f = tt[j] * s.stride + tap - s.pad;
-          if (f < 0 || f >= s.T_in) valid = 0;
-          p = s.base + (int64_t)tb[j] * s.sample_stride + (int64_t)(tt[j] * s.stride) * s.ld + mnoff;
+          ok = ok && f >= 0 && f < s.T_in;
+          p = ok ? s.base + (int64_t)tb[j] * s.sample_stride + (int64_t)(tt[j] * s.stride) * s.ld + mnoff : s.base;
           tt[j] += BK;
           while (tt[j] >= s.T_out) { tt[j] -= s.T_out; ++tb[j]; }
         } else {
-          p = s.base + (int64_t)k * s.ld + mnoff;
+          p = ok ? s.base + (int64_t)k * s.ld + mnoff : s.base;
         }
-        v[j] = ld4_guard(p, valid);
+        v[j] = sel4(*reinterpret_cast<const float4*>(p), ok, mnvalid);
       }
     }
   }
@@ -252,17 +254,22 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave >> 1, wn = wave & 1;
-  const int z = blockIdx.z;
+  // blockIdx.z = batch index * ksplit + K-slice index
+  const int ks = d.ksplit > 1 ? d.ksplit : 1;
+  const int z = blockIdx.z / ks, ksl = blockIdx.z - (blockIdx.z / ks) * ks;
   const int z1 = z / d.nz2, z2 = z - z1 * d.nz2;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
-  const int M = (int)d.M, N = (int)d.N, K = (int)d.K;
+  const int M = (int)d.M, N = (int)d.N;
+  const int kchunk = ks > 1 ? (int)d.kchunk : (int)d.K;   // multiple of BK
+  const int kbeg = ksl * kchunk;
+  const int K = ((int)d.K < kbeg + kchunk) ? (int)d.K : kbeg + kchunk;   // exclusive end
 
   OpState sa = make_state(d.A, z1, z2);
   OpState sb = make_state(d.B, z1, z2);
   Loader<BM, AK, ACONV, PREC> la;
   Loader<BN, BKin, BCONV, PREC> lb;
-  la.init(sa, tid, m0, M, K);
-  lb.init(sb, tid, n0, N, K);
+  la.init(sa, tid, m0, M, kbeg);
+  lb.init(sb, tid, n0, N, kbeg);
 
   f32x4 acc[TM][TN];
 #pragma unroll
@@ -274,9 +281,9 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
 #define AS_(b) (smem + (b) * (BM + BN) * LS)
 #define BS_(b) (smem + (b) * (BM + BN) * LS + BM * LS)
 
-  const int nk = (K + BK - 1) / BK;
-  la.load(sa, tid, 0, K);
-  lb.load(sb, tid, 0, K);
+  const int nk = K > kbeg ? (K - kbeg + BK - 1) / BK : 0;
+  la.load(sa, tid, kbeg, K);
+  lb.load(sb, tid, kbeg, K);
   la.store(AS_(0), tid);
   lb.store(BS_(0), tid);
   __syncthreads();
@@ -285,8 +292,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      la.load(sa, tid, (kt + 1) * BK, K);
-      lb.load(sb, tid, (kt + 1) * BK, K);
+      la.load(sa, tid, kbeg + (kt + 1) * BK, K);
+      lb.load(sb, tid, kbeg + (kt + 1) * BK, K);
     }
     const T* A_ = AS_(cur);
     const T* B_ = BS_(cur);
@@ -334,7 +341,12 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
         const int n = n0 + wn * WN + j * 16 + (lane & 15);
-        epilogue_store(ea, z, z1, z2, m, n, acc[i][j][r]);
+        if (ks > 1) {
+          // split-K: raw partial into the slab of (batch z, slice ksl); reduced by splitk_reduce
+          if (m < M && n < N) d.workspace[((int64_t)z * ks + ksl) * (int64_t)M * N + (int64_t)m * N + n] = acc[i][j][r];
+        } else {
+          epilogue_store(ea, z, z1, z2, m, n, acc[i][j][r]);
+        }
       }
 #undef AS_
 #undef BS_
@@ -342,7 +354,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
 
 template <int BM, int BN, bool AK, bool BKin, bool ACONV, bool BCONV>
 int launch_prec(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st) {
-  dim3 grid((unsigned)((d.N + BN - 1) / BN), (unsigned)((d.M + BM - 1) / BM), (unsigned)(d.nz1 * d.nz2));
+  const int ks = d.ksplit > 1 ? d.ksplit : 1;
+  dim3 grid((unsigned)((d.N + BN - 1) / BN), (unsigned)((d.M + BM - 1) / BM), (unsigned)(d.nz1 * d.nz2 * ks));
   if (d.precision == 1)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKin, ACONV, BCONV, 1>), grid, dim3(NT), 0, st, d, ea);
   else
@@ -355,6 +368,24 @@ int launch_tiles(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st) {
   // narrow-N problems (pos-conv groups N=48, lm_head N=32) use a 128x64 tile
   if (d.N <= 64) return launch_prec<128, 64, AK, BKin, ACONV, BCONV>(d, ea, st);
   return launch_prec<128, 128, AK, BKin, ACONV, BCONV>(d, ea, st);
+}
+
+// C[z](m,n) = alpha * sum_s slab[z][s](m,n) + beta * C_old ; deterministic slice order
+__global__ void splitk_reduce(const float* __restrict__ ws, int ks, int64_t M, int64_t N, int nz2,
+                              b2p_epilogue e, int64_t total) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  const int64_t MN = M * N;
+  const int64_t z = i / MN, r = i - z * MN;
+  const int64_t m = r / N, n = r - m * N;
+  const float* p = ws + z * ks * MN + r;
+  float s = 0.f;
+  for (int q = 0; q < ks; ++q) s += p[(int64_t)q * MN];
+  const int64_t z1 = z / nz2, z2 = z - z1 * nz2;
+  float* c = e.C + z1 * e.cbs1 + z2 * e.cbs2 + m * e.ldc + n;
+  float v = e.alpha * s;
+  if (e.beta != 0.f) v += e.beta * *c;
+  *c = v;
 }
 
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
@@ -387,6 +418,14 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   B2P_CHECK_ARG(!(d.A.conv && d.B.conv), "gemm: at most one implicit-conv operand");
   if (d.ep.act_bwd != B2P_ACT_NONE) B2P_CHECK_ARG(d.ep.aux != nullptr, "gemm: act_bwd needs aux");
   B2P_CHECK_ARG(d.ep.drop_p >= 0.f && d.ep.drop_p < 1.f, "gemm: dropout p must be in [0,1)");
+  if (d.ksplit > 1) {
+    B2P_CHECK_ARG(d.workspace != nullptr, "gemm: split-K needs a workspace");
+    B2P_CHECK_ARG(d.kchunk > 0 && d.kchunk % 32 == 0 && (int64_t)d.kchunk * d.ksplit >= d.K,
+                  "gemm: kchunk must be a multiple of 32 covering K");
+    B2P_CHECK_ARG(d.workspace_floats >= (int64_t)d.ksplit * d.nz1 * d.nz2 * d.M * d.N, "gemm: split-K workspace too small");
+    B2P_CHECK_ARG(!d.ep.bias && !d.ep.pre_out && d.ep.act == 0 && d.ep.act_bwd == 0 && d.ep.drop_p == 0.f &&
+                  !d.ep.residual, "gemm: split-K supports alpha/beta epilogues only");
+  }
 
   EpiArgs ea;
   ea.e = d.ep;
@@ -415,6 +454,11 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
     return 1;
   }
   if (rc) return rc;
+  if (d.ksplit > 1) {
+    const int64_t total = (int64_t)d.nz1 * d.nz2 * d.M * d.N;
+    hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d.workspace,
+                       d.ksplit, d.M, d.N, d.nz2, d.ep, total);
+  }
   B2P_CHECK_LAUNCH();
   b2p_timing_end(d.timing_family, st, d.flops);
   return 0;

@@ -18,6 +18,16 @@ void b2p_set_error(const char* fmt, ...) {
 
 extern "C" const char* b2p_last_error(void) { return g_err; }
 extern "C" int b2p_version(void) { return 1; }
+extern "C" int b2p_abi_sizes(int64_t* out3) {
+  if (!out3) {
+    b2p_set_error("abi_sizes: NULL");
+    return 1;
+  }
+  out3[0] = (int64_t)sizeof(b2p_operand);
+  out3[1] = (int64_t)sizeof(b2p_epilogue);
+  out3[2] = (int64_t)sizeof(b2p_gemm_desc);
+  return 0;
+}
 
 // ------------------------------------------------------------------ timing
 namespace {

@@ -154,6 +154,21 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     d.precision = _prec()
     d.timing_family = timing or _GEMM_TIMING[0]
     d.flops = 2.0 * M * N * K * nz1 * nz2
+    ws = None
+    plain = (bias is None and pre_out is None and act == 0 and act_bwd == 0 and drop_p == 0.0 and residual is None)
+    if plain and K >= 2048:
+        bn = 64 if N <= 64 else 128
+        blocks = -(-M // 128) * -(-N // bn) * nz1 * nz2
+        if blocks < 240:
+            ks = min(-(-512 // blocks), K // 1024)
+            if ks >= 2:
+                kchunk = -(-K // ks)
+                kchunk = -(-kchunk // 32) * 32
+                ks = -(-K // kchunk)
+                ws = torch.empty(ks * nz1 * nz2 * M * N, device=C.device, dtype=torch.float32)
+                d.ksplit, d.kchunk = ks, kchunk
+                d.workspace = ws.data_ptr()
+                d.workspace_floats = ws.numel()
     _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
 
 
@@ -225,7 +240,7 @@ def _ln_fwd(x2d, g, b, eps, drop_p=0.0, seed=0):
 
 
 def _ln_bwd(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, seed=0, in_drop_p=-1.0,
-            in_seed=0):
+            in_seed=0, dbias_in=None):
     rows, cols = x.shape
     dx = torch.empty_like(x)
     dg = torch.empty(cols, device=x.device) if need_params else None
@@ -233,7 +248,8 @@ def _ln_bwd(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, s
     ws = torch.empty(int(_lib.load().b2p_layernorm_bwd_workspace(rows, cols)), device=x.device)
     dxd = torch.empty_like(x) if in_drop_p >= 0.0 else None
     _lib.call("b2p_layernorm_bwd", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows, cols,
-              _p(dx_accum), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed, _p(ws), _st())
+              _p(dx_accum), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed, _p(dbias_in),
+              _p(ws), _st())
     return dx, dg, db, dxd
 
 
@@ -639,13 +655,11 @@ class _EncoderLayer(torch.autograd.Function):
         dout = dout.contiguous().view(NT, D)
         x2 = x.view(NT, D)
         # LN2 backward -> dy2 ; dz2 = dropout-mask(dy2) (output dropout of the FFN)
-        dy2, dg2, dbe2, dz2 = _ln_bwd(dout, y2, g2, m2, r2, True, in_drop_p=p_hid, in_seed=seeds[3])
+        db2 = torch.empty(D, device=dev) if ng[15] else None
+        dy2, dg2, dbe2, dz2 = _ln_bwd(dout, y2, g2, m2, r2, True, in_drop_p=p_hid, in_seed=seeds[3], dbias_in=db2)
         dw2 = torch.empty_like(w2) if ng[14] else None
         if dw2 is not None:
             mm_tn(dz2, f, dw2)
-        db2 = torch.empty(D, device=dev) if ng[15] else None
-        if db2 is not None:
-            colsum(dz2, NT, D, db2)
         # dpre = (dz2 W2) * mask_act * gelu'(pre)
         dpre = torch.empty(NT, F, device=dev)
         gemm(NT, F, D, op(dz2, 0, D, True), op(w2, 0, F, False), dpre, F, drop_p=p_act, seed=seeds[2],
@@ -661,13 +675,11 @@ class _EncoderLayer(torch.autograd.Function):
         gemm(NT, D, F, op(dpre, 0, F, True), op(w1, 0, D, False), dx1, D, residual=dy2)
         del dpre
         # LN1 backward -> dy1 ; dz1 = dropout-mask(dy1) (attention output dropout)
-        dy1, dg1, dbe1, dz1 = _ln_bwd(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1])
+        dbo = torch.empty(D, device=dev) if ng[9] else None
+        dy1, dg1, dbe1, dz1 = _ln_bwd(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1], dbias_in=dbo)
         dwo = torch.empty_like(wo) if ng[8] else None
         if dwo is not None:
             mm_tn(dz1, O, dwo)
-        dbo = torch.empty(D, device=dev) if ng[9] else None
-        if dbo is not None:
-            colsum(dz1, NT, D, dbo)
         dO = torch.empty(NT, D, device=dev)
         mm_nn(dz1, wo, dO)
         # attention backward
