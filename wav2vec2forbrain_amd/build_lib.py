@@ -65,3 +65,22 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
 
 if __name__ == "__main__":
     print(build(verbose="-v" in sys.argv))
+
+
+def audit_scratch(src: str = "gemm.hip") -> dict:
+    """Compiles one source with -Rpass-analysis=kernel-resource-usage and returns
+    {kernel: scratch_bytes_per_lane}. A nonzero value means registers spilled or a private array
+    went to scratch (e.g. accumulators indexed dynamically) — a silent 4x slowdown seen once."""
+    import re
+    path = os.path.join(CSRC, src)
+    r = subprocess.run([HIPCC, *FLAGS, "-c", path, "-o", os.devnull, "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True)
+    out, cur = {}, None
+    for line in (r.stdout + r.stderr).splitlines():
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+        m = re.search(r"ScratchSize \[bytes/lane\]: (\d+)", line)
+        if m and cur:
+            out[cur] = int(m.group(1))
+    return out

@@ -332,22 +332,32 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
     __syncthreads();
   }
 
-  // epilogue: lane holds rows (lane>>4)*4 + r, column lane&15 of each 16x16 tile
+  // epilogue: lane holds rows (lane>>4)*4 + r, column lane&15 of each 16x16 tile. The split-K
+  // branch is hoisted out of the unrolled loops so acc[][] keeps constant indices (registers).
+  if (ks > 1) {
+    float* slab = d.workspace + ((int64_t)z * ks + ksl) * (int64_t)M * N;
 #pragma unroll
-  for (int i = 0; i < TM; ++i)
+    for (int i = 0; i < TM; ++i)
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        const int n = n0 + wn * WN + j * 16 + (lane & 15);
-        if (ks > 1) {
-          // split-K: raw partial into the slab of (batch z, slice ksl); reduced by splitk_reduce
-          if (m < M && n < N) d.workspace[((int64_t)z * ks + ksl) * (int64_t)M * N + (int64_t)m * N + n] = acc[i][j][r];
-        } else {
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          const int n = n0 + wn * WN + j * 16 + (lane & 15);
+          if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          const int n = n0 + wn * WN + j * 16 + (lane & 15);
           epilogue_store(ea, z, z1, z2, m, n, acc[i][j][r]);
         }
-      }
+  }
 #undef AS_
 #undef BS_
 }
