@@ -122,7 +122,7 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
   }
 }
 
-constexpr int LN_BWD_ROWS = 128;  // rows per block (32 per wave)
+constexpr int LN_BWD_ROWS = 16;   // rows per block (4 per wave): ~500 blocks at 8k rows
 __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, const float* __restrict__ x,
                                                 const float* __restrict__ gamma, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, float* __restrict__ dx,
@@ -214,16 +214,13 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
   }
 }
 
-__global__ void ln_bwd_reduce(const float* __restrict__ part, int nblk, int cols, float* __restrict__ dgamma,
-                              float* __restrict__ dbeta, float* __restrict__ dbias_in) {
+__global__ void ln_bwd_scatter(const float* __restrict__ red3, int cols, float* __restrict__ dgamma,
+                               float* __restrict__ dbeta, float* __restrict__ dbias_in) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= 3 * cols) return;
   const int q = c / cols, cc = c - q * cols;
   float* dst = q == 0 ? dgamma : (q == 1 ? dbeta : dbias_in);
-  if (!dst) return;
-  float s = 0.f;
-  for (int i = 0; i < nblk; ++i) s += part[((int64_t)i * 3 + q) * cols + cc];
-  dst[cc] = s;
+  if (dst) dst[cc] = red3[c];
 }
 
 // ------------------------------------------------------------------ attention softmax
@@ -466,7 +463,8 @@ extern "C" int b2p_layernorm_fwd(const float* x, const float* gamma, const float
 }
 
 extern "C" int64_t b2p_layernorm_bwd_workspace(int64_t rows, int64_t cols) {
-  return ((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS) * 3 * cols;
+  const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
+  return nblk * 3 * cols + 3 * cols + ((nblk + kColsumRows - 1) / kColsumRows) * 3 * cols;
 }
 
 extern "C" int b2p_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
@@ -483,8 +481,12 @@ extern "C" int b2p_layernorm_bwd(const float* dy, const float* x, const float* g
                      rows, (int)cols, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
                      drop_seed, drop_p, dx_dropped, b2p_dropout_threshold(in_drop_p),
                      in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed);
-  hipLaunchKernelGGL(ln_bwd_reduce, dim3(nblocks(3 * cols)), dim3(256), 0, st, workspace, nblk, (int)cols,
-                     dgamma, dbeta, dx_dropped ? dbias_in : nullptr);
+  // partials [nblk][3][cols] -> [3][cols] with the parallel two-phase column sum, then scatter
+  float* red3 = workspace + (int64_t)nblk * 3 * cols;
+  float* part2 = red3 + 3 * cols;
+  if (colsum_impl(workspace, nullptr, 1, nblk, 3 * cols, 3 * cols, 0, 0, red3, 0, part2, st)) return 1;
+  hipLaunchKernelGGL(ln_bwd_scatter, dim3(nblocks(3 * cols)), dim3(256), 0, st, red3, (int)cols, dgamma, dbeta,
+                     dx_dropped ? dbias_in : nullptr);
   B2P_CHECK_LAUNCH();
   return 0;
 }
