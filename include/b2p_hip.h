@@ -219,6 +219,43 @@ int b2p_adam_multi(const int64_t* table, int ntensors, int64_t max_numel, float 
                    float beta2, float eps, float weight_decay, float bias_c1, float bias_c2_sqrt,
                    b2p_stream_t stream);
 
+/* dropout with an extra output scale: y = x * keep(seed, i) * scale / (1-p) (macaron half-step) */
+int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t seed, float scale,
+                       b2p_stream_t stream);
+
+/* ------------------------------------------------------------------ Conformer
+ * transformers Wav2Vec2Conformer{SelfAttention,ConvolutionModule,RotaryPositionalEmbedding}
+ * as instantiated by reference src/model/w2v_conformer_custom_feat_extractor.py:62-112. */
+/* rotary on (B*T rows of H heads x D, row stride ld): out = x*cos + rotate_half(x)*sin with
+ * rotate_half(x) = cat(-x2, x1); inverse=1 applies the transpose (backward). cos/sin (T, D). */
+int b2p_rotary(const float* x, const float* cos_t, const float* sin_t, float* out, int64_t B,
+               int64_t T, int64_t H, int64_t D, int64_t ld, int inverse, b2p_stream_t stream);
+/* nn.GLU(dim=channels): out[m][c] = a[m][c] * sigmoid(a[m][C+c]); a is (M, 2C) */
+int b2p_glu_fwd(const float* a, float* out, int64_t M, int64_t C, b2p_stream_t stream);
+int b2p_glu_bwd(const float* a, const float* dout, float* da, int64_t M, int64_t C,
+                b2p_stream_t stream);
+/* depthwise Conv1d(C, C, K, padding=(K-1)/2, groups=C, bias=False), channels-last (B, T, C);
+ * w (C, K). Backward writes dx and/or dw (deterministic partial sums). */
+int b2p_dwconv_fwd(const float* x, const float* w, float* y, int64_t B, int64_t T, int64_t C,
+                   int K, b2p_stream_t stream);
+int64_t b2p_dwconv_bwd_workspace(int64_t B, int64_t T, int64_t C, int K);
+int b2p_dwconv_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw,
+                   int64_t B, int64_t T, int64_t C, int K, float* workspace, b2p_stream_t stream);
+/* BatchNorm1d over channels of (M, C) rows: training mode uses batch statistics (two-pass mean /
+ * biased variance), updates running stats (momentum, unbiased variance), applies gamma/beta and the
+ * fused activation act (B2P_ACT_SILU = swish). pre (optional) keeps the pre-activation. */
+int64_t b2p_batchnorm_workspace(int64_t M, int64_t C);
+int b2p_batchnorm_fwd(const float* x, const float* gamma, const float* beta, float* running_mean,
+                      float* running_var, float* y, float* pre, float* mean, float* rstd, int64_t M,
+                      int64_t C, float eps, float momentum, int act, float* workspace,
+                      b2p_stream_t stream);
+int b2p_batchnorm_eval(const float* x, const float* gamma, const float* beta,
+                       const float* running_mean, const float* running_var, float* y, int64_t M,
+                       int64_t C, float eps, int act, float* workspace, b2p_stream_t stream);
+int b2p_batchnorm_bwd(const float* dy, const float* pre, const float* x, const float* mean,
+                      const float* rstd, const float* gamma, float* dx, float* dgamma, float* dbeta,
+                      int64_t M, int64_t C, int act, float* workspace, b2p_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

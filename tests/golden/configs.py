@@ -16,6 +16,15 @@ CONFIGS = [
     dict(name="plumbing_base", seed=42, B=2, L=512, in_lens=[512, 384], tgt_range=(20, 50), hidden_size=768,
          layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2, bidirectional=True,
          fc_hidden=[], learnable_h0=False, full_grad_max=4096, infeasible=False),
+    # Conformer (rotary) tiny: every conformer code path, full small gradients
+    dict(name="tiny_conf", seed=44, B=2, L=96, in_lens=[96, 88], tgt_range=(2, 8), hidden_size=64, layers=2,
+         heads=4, ffn=128, pos_k=16, pos_groups=4, gru_hidden=32, gru_layers=2, bidirectional=True, fc_hidden=[48],
+         learnable_h0=False, full_grad_max=65536, infeasible=False, conformer=True, dw_kernel=7),
+    # BASELINE configs[2] architecture (wav2vec2-conformer-rope-large: 1024/24L/16H/4096, k31; README brain
+    # encoder H512x3, fc [256]) at bs=2, 288-bin windows
+    dict(name="conformer_large_b2", seed=45, B=2, L=288, in_lens=[288, 256], tgt_range=(10, 25), hidden_size=1024,
+         layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512, gru_layers=3, bidirectional=True,
+         fc_hidden=[256], learnable_h0=False, full_grad_max=4096, infeasible=False, conformer=True, dw_kernel=31),
 ]
 
 

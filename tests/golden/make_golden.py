@@ -66,14 +66,46 @@ def build_reference_model(cfg, tfw, bfe, w2v, base_args):
     return model
 
 
+def build_reference_conformer(cfg, bfe, base_args):
+    import transformers.models.wav2vec2_conformer.modeling_wav2vec2_conformer as tfc
+    from src.model import w2v_conformer_custom_feat_extractor as wc
+    name = "golden/" + cfg["name"]
+    base_args.PRETRAINED_LATENT_SIZES[name] = cfg["hidden_size"]
+    bfe.PRETRAINED_LATENT_SIZES[name] = cfg["hidden_size"]
+    hf = tfc.Wav2Vec2ConformerConfig(
+        hidden_size=cfg["hidden_size"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"],
+        intermediate_size=cfg["ffn"], hidden_act="swish", position_embeddings_type="rotary",
+        rotary_embedding_base=10000, conv_depthwise_kernel_size=cfg["dw_kernel"], hidden_dropout=0.0,
+        activation_dropout=0.0, attention_dropout=0.0, feat_proj_dropout=0.0, final_dropout=0.0, layerdrop=0.0,
+        conformer_conv_dropout=0.0, num_conv_pos_embeddings=cfg["pos_k"],
+        num_conv_pos_embedding_groups=cfg["pos_groups"], vocab_size=32)
+    hf._attn_implementation = "eager"
+    args = bfe.B2P2TBrainFeatureExtractorArgsModel(
+        encoder_gru_hidden_size=cfg["gru_hidden"], encoder_num_gru_layers=cfg["gru_layers"],
+        encoder_bidirectional=cfg["bidirectional"], encoder_fc_hidden_sizes=cfg["fc_hidden"],
+        encoder_learnable_inital_state=cfg["learnable_h0"])
+    brain = bfe.bfe_w_preprocessing_from_config(args, None, name)
+    # bypass __init__ (it always calls from_pretrained), then use the reference forward
+    model = wc.W2VConformerBrainEncoderModel.__new__(wc.W2VConformerBrainEncoderModel)
+    torch.nn.Module.__init__(model)
+    model.brain_encoder = brain
+    model.w2v_encoder = wc.Wav2Vec2ConformerWithoutFeatExtrForCTC(hf)
+    model.loss = torch.nn.CTCLoss(blank=0, reduction="mean", zero_infinity=True)
+    return model
+
+
 def run(cfg, modules):
     tfw, bfe, w2v, base_args = modules
     torch.manual_seed(0)
-    model = build_reference_model(cfg, tfw, bfe, w2v, base_args)
+    if cfg.get("conformer"):
+        model = build_reference_conformer(cfg, bfe, base_args)
+    else:
+        model = build_reference_model(cfg, tfw, bfe, w2v, base_args)
     sd = deterministic_state([(n, p.shape) for n, p in model.named_parameters()], seed=cfg["seed"])
     missing, unexpected = model.load_state_dict(sd, strict=False)
     assert not unexpected, unexpected
-    assert all(k.endswith("gaussian_smoother.weight") for k in missing), missing
+    assert all(k.endswith(("gaussian_smoother.weight", "inv_freq", "running_mean", "running_var", "num_batches_tracked"))
+               for k in missing), missing
     model.train()   # deterministic: every dropout and layerdrop is 0
     from src.datasets.batch_types import B2tSampleBatch
     x, day, in_lens, tgt, tgt_lens = make_batch(cfg)
@@ -85,7 +117,6 @@ def run(cfg, modules):
     out.loss.backward()
     res = {"loss": np.array(out.loss.item(), dtype=np.float64),
            "logits": out.logits.detach().numpy(),
-           "logit_lens": out.logit_lens.numpy(),
            "x": x.numpy(), "day_idxs": day.numpy(), "input_lens": in_lens.numpy(), "target": tgt.numpy(),
            "target_lens": tgt_lens.numpy()}
     names = []
@@ -102,6 +133,11 @@ def run(cfg, modules):
             res["gidx/" + n] = idx.numpy()
             res["gval/" + n] = flat[idx].numpy()
     res["param_names"] = np.array(names)
+    if out.logit_lens is not None:
+        res["logit_lens"] = out.logit_lens.numpy()
+    for n, bt in model.named_buffers():
+        if "running_" in n:
+            res["buf/" + n] = bt.numpy()
     path = os.path.join(OUT, f"{cfg['name']}.npz")
     np.savez_compressed(path, **res)
     print(f"{path}: loss={out.loss.item():.6f}  ({os.path.getsize(path)/1e6:.2f} MB)")
@@ -110,5 +146,7 @@ def run(cfg, modules):
 if __name__ == "__main__":
     mods = _import_reference()
     torch.set_num_threads(8)
+    only = sys.argv[1:]
     for c in CONFIGS:
-        run(c, mods)
+        if not only or c["name"] in only:
+            run(c, mods)

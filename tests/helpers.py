@@ -17,7 +17,14 @@ def load_fixture(name):
 
 
 def oracle_cfg(cfg):
-    from oracle.b2p2t_oracle import OracleConfig
+    from oracle.b2p2t_oracle import OracleConfig, ConformerOracleConfig
+    if cfg.get("conformer"):
+        return ConformerOracleConfig(
+            gru_hidden=cfg["gru_hidden"], gru_layers=cfg["gru_layers"], bidirectional=cfg["bidirectional"],
+            fc_hidden_sizes=list(cfg["fc_hidden"]), learnable_initial_state=cfg["learnable_h0"],
+            hidden_size=cfg["hidden_size"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"],
+            intermediate_size=cfg["ffn"], num_conv_pos_embeddings=cfg["pos_k"],
+            num_conv_pos_embedding_groups=cfg["pos_groups"], conv_depthwise_kernel_size=cfg["dw_kernel"])
     return OracleConfig(gru_hidden=cfg["gru_hidden"], gru_layers=cfg["gru_layers"], bidirectional=cfg["bidirectional"],
                         fc_hidden_sizes=list(cfg["fc_hidden"]), learnable_initial_state=cfg["learnable_h0"],
                         hidden_size=cfg["hidden_size"], num_hidden_layers=cfg["layers"],
@@ -28,10 +35,14 @@ def oracle_cfg(cfg):
 def w2v_cfg(cfg, train_dropouts=False):
     from wav2vec2forbrain_amd.model.w2v_config import W2VConfig
     p = 0.1 if train_dropouts else 0.0
+    extra = {}
+    if cfg.get("conformer"):
+        extra = dict(conformer=True, position_embeddings_type="rotary", hidden_act="swish",
+                     conv_depthwise_kernel_size=cfg["dw_kernel"], conformer_conv_dropout=p)
     return W2VConfig(hidden_size=cfg["hidden_size"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"],
                      intermediate_size=cfg["ffn"], hidden_dropout=p, activation_dropout=p, attention_dropout=p,
                      final_dropout=p, layerdrop=p, num_conv_pos_embeddings=cfg["pos_k"],
-                     num_conv_pos_embedding_groups=cfg["pos_groups"])
+                     num_conv_pos_embedding_groups=cfg["pos_groups"], **extra)
 
 
 def build_model(cfg, device="cuda", seed=None, train_dropouts=False):
@@ -49,8 +60,12 @@ def build_model(cfg, device="cuda", seed=None, train_dropouts=False):
         encoder_learnable_inital_state=cfg["learnable_h0"])
     torch.manual_seed(0)
     brain = bfe.B2P2TModel(args, bfe.B2TBrainFeatureExtractor(args, name, 256 * args.unfolder_kernel_len))
-    model = W2VBrainEncoderModel(W2VBrainEncoderModelArgs(), brain, name, skip_loading_weights=True,
-                                 w2v_config_override=w2v_cfg(cfg, train_dropouts))
+    if cfg.get("conformer"):
+        from wav2vec2forbrain_amd.model.w2v_conformer_custom_feat_extractor import W2VConformerBrainEncoderModel
+        model = W2VConformerBrainEncoderModel(brain, name, w2v_config_override=w2v_cfg(cfg, train_dropouts))
+    else:
+        model = W2VBrainEncoderModel(W2VBrainEncoderModelArgs(), brain, name, skip_loading_weights=True,
+                                     w2v_config_override=w2v_cfg(cfg, train_dropouts))
     init_deterministic_(model, cfg["seed"] if seed is None else seed)
     return model.to(device)
 

@@ -8,7 +8,7 @@ import torch
 from tests.helpers import CFG, load_fixture, oracle_cfg, oracle_state, batch_dict, build_model
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base"])
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2"])
 def test_state_dict_keys_match_reference(name):
     fx = load_fixture(name)
     model = build_model(CFG[name], device="cpu")
@@ -16,16 +16,21 @@ def test_state_dict_keys_match_reference(name):
     assert ours == list(fx["param_names"])
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base"])
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2"])
 def test_oracle_matches_reference_golden(name):
     cfg = CFG[name]
     fx = load_fixture(name)
     torch.set_num_threads(8)
-    from oracle.b2p2t_oracle import loss_and_grads, forward_loss
+    from oracle.b2p2t_oracle import loss_and_grads, conformer_loss_and_grads
     sd = oracle_state(cfg)
     b = batch_dict(cfg)
     assert np.array_equal(b["x"].numpy(), fx["x"])
-    loss, grads = loss_and_grads(sd, b, oracle_cfg(cfg))
+    if cfg.get("conformer"):
+        loss, grads, bn_state = conformer_loss_and_grads(sd, b, oracle_cfg(cfg))
+        for k, v in bn_state.items():
+            np.testing.assert_allclose(v.numpy(), fx["buf/" + k], rtol=1e-4, atol=1e-5, err_msg=k)
+    else:
+        loss, grads = loss_and_grads(sd, b, oracle_cfg(cfg))
     assert abs(float(loss) - float(fx["loss"])) <= 2e-5 * abs(float(fx["loss"])), (float(loss), float(fx["loss"]))
     gmax = max(float(fx["gnorm/" + n]) for n in fx["param_names"])
     for n in fx["param_names"]:

@@ -87,6 +87,18 @@ _SIGS = {
     "b2p_ctc_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "b2p_ctc_fwd_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "b2p_adam_multi": (c_i32, [c_p, c_i32, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_p]),
+    "b2p_dropout_scaled": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_f32, c_p]),
+    "b2p_rotary": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_glu_fwd": (c_i32, [c_p, c_p, c_i64, c_i64, c_p]),
+    "b2p_glu_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_p]),
+    "b2p_dwconv_fwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_dwconv_bwd_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i32]),
+    "b2p_dwconv_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p, c_p]),
+    "b2p_batchnorm_workspace": (c_i64, [c_i64, c_i64]),
+    "b2p_batchnorm_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_i32,
+                                  c_p, c_p]),
+    "b2p_batchnorm_eval": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_i32, c_p, c_p]),
+    "b2p_batchnorm_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p]),
 }
 
 # timing families (b2p_timing_*)

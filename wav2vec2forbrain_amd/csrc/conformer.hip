@@ -1,0 +1,361 @@
+// Conformer-specific kernels (transformers Wav2Vec2ConformerEncoderLayer / ConvolutionModule /
+// RotaryPositionalEmbedding, instantiated by reference
+// src/model/w2v_conformer_custom_feat_extractor.py:62-112): rotary embedding, GLU, depthwise
+// conv1d (k odd, 'same'), BatchNorm1d training statistics / apply / backward. HBM-bound, fp32,
+// channels-last (token-major) like every activation of this library.
+#include "common.h"
+#include "../../include/b2p_hip.h"
+
+int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_t N, int64_t ld, int64_t bstride,
+                int mode, float* out, int accumulate, float* part, hipStream_t st);
+
+namespace {
+inline unsigned nblk(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
+
+// x rows (B*T) of H heads x D; cos/sin (T, D). out = x*cos + rotate_half(x)*sin
+// rotate_half(x) = cat(-x[D/2:], x[:D/2]); inverse (backward) applies the transpose.
+__global__ void rotary_k(const float* __restrict__ x, const float* __restrict__ ct, const float* __restrict__ st,
+                         float* __restrict__ out, int64_t rows, int T, int H, int D, int64_t ld, int inverse) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t total = rows * H * D;
+  if (i >= total) return;
+  const int d = (int)(i % D);
+  const int h = (int)((i / D) % H);
+  const int64_t r = i / ((int64_t)D * H);
+  const int t = (int)(r % T);
+  const float* xr = x + r * ld + (int64_t)h * D;
+  const int half = D / 2;
+  const float c = ct[(int64_t)t * D + d];
+  float v;
+  if (!inverse) {
+    const float s = st[(int64_t)t * D + d];
+    const float rot = d < half ? -xr[d + half] : xr[d - half];
+    v = xr[d] * c + rot * s;
+  } else {
+    // dx[d] = dy[d] cos[d] + (d < half ? dy[d+half] sin[d+half] : -dy[d-half] sin[d-half])
+    const float other = d < half ? xr[d + half] * st[(int64_t)t * D + d + half]
+                                 : -xr[d - half] * st[(int64_t)t * D + d - half];
+    v = xr[d] * c + other;
+  }
+  out[r * ld + (int64_t)h * D + d] = v;
+}
+
+__global__ void glu_fwd_k(const float* __restrict__ a, float* __restrict__ out, int64_t M, int64_t C) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const int64_t m = i / C, c = i - m * C;
+  const float x = a[m * 2 * C + c], g = a[m * 2 * C + C + c];
+  out[i] = x * b2p_sigmoid(g);
+}
+
+__global__ void glu_bwd_k(const float* __restrict__ a, const float* __restrict__ dout, float* __restrict__ da,
+                          int64_t M, int64_t C) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const int64_t m = i / C, c = i - m * C;
+  const float x = a[m * 2 * C + c], g = a[m * 2 * C + C + c];
+  const float s = b2p_sigmoid(g);
+  const float d = dout[i];
+  da[m * 2 * C + c] = d * s;
+  da[m * 2 * C + C + c] = d * x * s * (1.f - s);
+}
+
+// depthwise conv, channels-last, zero 'same' padding p = (K-1)/2: y[b,t,c] = sum_k w[c,k] x[b,t+k-p,c]
+__global__ void dwconv_fwd_k(const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y,
+                             int64_t B, int64_t T, int64_t C, int K) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * T * C) return;
+  const int64_t c = i % C, t = (i / C) % T, b = i / (C * T);
+  const int p = (K - 1) / 2;
+  const float* xb = x + b * T * C + c;
+  const float* wc = w + c * K;
+  float acc = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const int64_t s = t + k - p;
+    if (s >= 0 && s < T) acc += wc[k] * xb[s * C];
+  }
+  y[i] = acc;
+}
+
+// dx[b,s,c] = sum_k w[c,k] dy[b, s-k+p, c]
+__global__ void dwconv_bwd_x_k(const float* __restrict__ dy, const float* __restrict__ w, float* __restrict__ dx,
+                               int64_t B, int64_t T, int64_t C, int K) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B * T * C) return;
+  const int64_t c = i % C, s = (i / C) % T, b = i / (C * T);
+  const int p = (K - 1) / 2;
+  const float* db = dy + b * T * C + c;
+  const float* wc = w + c * K;
+  float acc = 0.f;
+  for (int k = 0; k < K; ++k) {
+    const int64_t t = s - k + p;
+    if (t >= 0 && t < T) acc += wc[k] * db[t * C];
+  }
+  dx[i] = acc;
+}
+
+// dw partials: block = (64 channels, 64-frame tile of one sample); part[(b*ntile + tile)][k][c]
+constexpr int DW_TT = 64;
+__global__ void __launch_bounds__(256) dwconv_bwd_w_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                      float* __restrict__ part, int64_t B, int64_t T, int64_t C,
+                                                      int K, int ntile) {
+  const int cl = threadIdx.x & 63, kg = threadIdx.x >> 6;     // 4 groups of taps
+  const int64_t c = (int64_t)blockIdx.x * 64 + cl;
+  const int tile = blockIdx.y % ntile;
+  const int64_t b = blockIdx.y / ntile;
+  const int p = (K - 1) / 2;
+  const int64_t t0 = (int64_t)tile * DW_TT;
+  const int64_t t1 = t0 + DW_TT < T ? t0 + DW_TT : T;
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  if (c < C) {
+    const float* xb = x + b * T * C + c;
+    const float* db = dy + b * T * C + c;
+    for (int64_t t = t0; t < t1; ++t) {
+      const float g = db[t * C];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = kg * 8 + q;
+        const int64_t s = t + k - p;
+        if (k < K && s >= 0 && s < T) acc[q] += g * xb[s * C];
+      }
+    }
+    float* pp = part + (int64_t)blockIdx.y * K * C;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = kg * 8 + q;
+      if (k < K) pp[(int64_t)k * C + c] = acc[q];
+    }
+  }
+}
+
+__global__ void dw_transpose_k(const float* __restrict__ kc, float* __restrict__ ck, int64_t C, int K) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= C * K) return;
+  const int64_t c = i / K, k = i % K;
+  ck[i] = kc[k * C + c];
+}
+
+// ---- BatchNorm1d (training statistics over M rows, per channel)
+__global__ void bn_finalize_k(const float* __restrict__ sum, const float* __restrict__ sqdev, const float* __restrict__ mean,
+                              float* __restrict__ rstd, float* __restrict__ run_mean, float* __restrict__ run_var,
+                              int64_t C, int64_t count, float eps, float momentum) {
+  const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float mu = mean[c];
+  const float var = sqdev[c] / (float)count;
+  rstd[c] = rsqrtf(var + eps);
+  if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
+  if (run_var) {
+    const float unb = count > 1 ? sqdev[c] / (float)(count - 1) : var;
+    run_var[c] = (1.f - momentum) * run_var[c] + momentum * unb;
+  }
+  (void)sum;
+}
+
+__global__ void scale_k(float* __restrict__ v, int64_t n, float s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) v[i] *= s;
+}
+
+__device__ __forceinline__ float act_f(float v, int act) {
+  if (act == B2P_ACT_SILU) return b2p_silu(v);
+  if (act == B2P_ACT_GELU) return b2p_gelu(v);
+  return v;
+}
+__device__ __forceinline__ float act_g(float v, int act) {
+  if (act == B2P_ACT_SILU) return b2p_silu_grad(v);
+  if (act == B2P_ACT_GELU) return b2p_gelu_grad(v);
+  return 1.f;
+}
+
+// y = act(pre), pre = (x - mean) * rstd * gamma + beta
+__global__ void bn_apply_k(const float* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ rstd,
+                           const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ y,
+                           float* __restrict__ pre, int64_t M, int64_t C, int act) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const int64_t c = i % C;
+  const float v = (x[i] - mean[c]) * rstd[c] * gamma[c] + beta[c];
+  if (pre) pre[i] = v;
+  y[i] = act_f(v, act);
+}
+
+// g = dy * act'(pre)  (written to g)
+__global__ void bn_grad_pre_k(const float* __restrict__ dy, const float* __restrict__ pre, float* __restrict__ g,
+                              int64_t n, int act) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  g[i] = dy[i] * act_g(pre[i], act);
+}
+
+// dx = gamma*rstd/M * (M*g - sum_g - xhat * sum_gxhat), xhat = (x-mean)*rstd
+__global__ void bn_bwd_dx_k(const float* __restrict__ g, const float* __restrict__ x, const float* __restrict__ mean,
+                            const float* __restrict__ rstd, const float* __restrict__ gamma,
+                            const float* __restrict__ sum_g, const float* __restrict__ sum_gx, float* __restrict__ dx,
+                            int64_t M, int64_t C, int64_t count) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const int64_t c = i % C;
+  const float xh = (x[i] - mean[c]) * rstd[c];
+  const float inv = 1.f / (float)count;
+  dx[i] = gamma[c] * rstd[c] * (g[i] - sum_g[c] * inv - xh * sum_gx[c] * inv);
+}
+
+// xhat products for dgamma: t = g * (x - mean) * rstd
+__global__ void bn_gxhat_k(const float* __restrict__ g, const float* __restrict__ x, const float* __restrict__ mean,
+                           const float* __restrict__ rstd, float* __restrict__ t, int64_t M, int64_t C) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= M * C) return;
+  const int64_t c = i % C;
+  t[i] = g[i] * (x[i] - mean[c]) * rstd[c];
+}
+
+__global__ void dropout_scale_k(const float* __restrict__ x, float* __restrict__ y, int64_t n, uint32_t thr,
+                                float scale, uint64_t seed, int use_mask) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  y[i] = (!use_mask || b2p_keep(seed, (uint64_t)i, thr)) ? x[i] * scale : 0.f;
+}
+}  // namespace
+
+extern "C" int b2p_rotary(const float* x, const float* cos_t, const float* sin_t, float* out, int64_t B, int64_t T,
+                          int64_t H, int64_t D, int64_t ld, int inverse, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && cos_t && sin_t && out && x != out, "rotary: bad pointers");
+  B2P_CHECK_ARG(D % 2 == 0, "rotary: head dim must be even");
+  const int64_t n = B * T * H * D;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(rotary_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, cos_t, sin_t, out, B * T, (int)T,
+                     (int)H, (int)D, ld, inverse);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_glu_fwd(const float* a, float* out, int64_t M, int64_t C, b2p_stream_t stream) {
+  B2P_CHECK_ARG(a && out, "glu_fwd: NULL");
+  if (M * C <= 0) return 0;
+  hipLaunchKernelGGL(glu_fwd_k, dim3(nblk(M * C)), dim3(256), 0, (hipStream_t)stream, a, out, M, C);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_glu_bwd(const float* a, const float* dout, float* da, int64_t M, int64_t C, b2p_stream_t stream) {
+  B2P_CHECK_ARG(a && dout && da, "glu_bwd: NULL");
+  if (M * C <= 0) return 0;
+  hipLaunchKernelGGL(glu_bwd_k, dim3(nblk(M * C)), dim3(256), 0, (hipStream_t)stream, a, dout, da, M, C);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_dwconv_fwd(const float* x, const float* w, float* y, int64_t B, int64_t T, int64_t C, int K,
+                              b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && w && y, "dwconv_fwd: NULL");
+  B2P_CHECK_ARG(K % 2 == 1, "dwconv: kernel size must be odd ('same' padding)");
+  const int64_t n = B * T * C;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(dwconv_fwd_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, w, y, B, T, C, K);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t b2p_dwconv_bwd_workspace(int64_t B, int64_t T, int64_t C, int K) {
+  const int64_t ntile = (T + DW_TT - 1) / DW_TT;
+  const int64_t rows = B * ntile;
+  return rows * K * C + (int64_t)K * C + ((rows + 255) / 256) * K * C;
+}
+
+extern "C" int b2p_dwconv_bwd(const float* x, const float* w, const float* dy, float* dx, float* dw, int64_t B,
+                              int64_t T, int64_t C, int K, float* workspace, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && w && dy && workspace, "dwconv_bwd: NULL");
+  B2P_CHECK_ARG(K % 2 == 1 && K <= 32, "dwconv_bwd: odd kernel size <= 31 supported");
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n = B * T * C;
+  if (n <= 0) return 0;
+  if (dx) hipLaunchKernelGGL(dwconv_bwd_x_k, dim3(nblk(n)), dim3(256), 0, st, dy, w, dx, B, T, C, K);
+  if (dw) {
+    const int ntile = (int)((T + DW_TT - 1) / DW_TT);
+    float* part = workspace;
+    float* kc = part + B * ntile * (int64_t)K * C;
+    float* p2 = kc + (int64_t)K * C;
+    hipLaunchKernelGGL(dwconv_bwd_w_k, dim3((unsigned)((C + 63) / 64), (unsigned)(B * ntile)), dim3(256), 0, st, x,
+                       dy, part, B, T, C, K, ntile);
+    if (colsum_impl(part, nullptr, 1, B * ntile, (int64_t)K * C, (int64_t)K * C, 0, 0, kc, 0, p2, st)) return 1;
+    hipLaunchKernelGGL(dw_transpose_k, dim3(nblk(C * K)), dim3(256), 0, st, kc, dw, C, K);
+  }
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t b2p_batchnorm_workspace(int64_t M, int64_t C) {
+  return M * C + 4 * C + ((M + 255) / 256) * C;
+}
+
+// training-mode BN forward: mean/rstd (saved), running stats update, y = act(BN(x)), pre saved
+extern "C" int b2p_batchnorm_fwd(const float* x, const float* gamma, const float* beta, float* running_mean,
+                                 float* running_var, float* y, float* pre, float* mean, float* rstd, int64_t M,
+                                 int64_t C, float eps, float momentum, int act, float* workspace,
+                                 b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && gamma && beta && y && mean && rstd && workspace, "batchnorm_fwd: NULL");
+  hipStream_t st = (hipStream_t)stream;
+  if (M <= 0) return 0;
+  float* sqdev = workspace;
+  float* part = workspace + 4 * C;
+  // two-pass statistics: mean, then sum of squared deviations (mode 3)
+  if (colsum_impl(x, nullptr, 1, M, C, C, 0, 0, mean, 0, part, st)) return 1;
+  hipLaunchKernelGGL(scale_k, dim3(nblk(C)), dim3(256), 0, st, mean, C, 1.f / (float)M);
+  if (colsum_impl(x, mean, 1, M, C, C, 0, 3, sqdev, 0, part, st)) return 1;
+  hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sqdev, mean, rstd,
+                     running_mean, running_var, C, M, eps, momentum);
+  hipLaunchKernelGGL(bn_apply_k, dim3(nblk(M * C)), dim3(256), 0, st, x, mean, rstd, gamma, beta, y, pre, M, C, act);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+// eval-mode BN (running statistics) — forward only
+extern "C" int b2p_batchnorm_eval(const float* x, const float* gamma, const float* beta, const float* running_mean,
+                                  const float* running_var, float* y, int64_t M, int64_t C, float eps, int act,
+                                  float* workspace, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && gamma && beta && running_mean && running_var && y && workspace, "batchnorm_eval: NULL");
+  hipStream_t st = (hipStream_t)stream;
+  if (M <= 0) return 0;
+  float* rstd = workspace;
+  float* sq = workspace + C;
+  B2P_CHECK_HIP(hipMemcpyAsync(sq, running_var, C * sizeof(float), hipMemcpyDeviceToDevice, st));
+  hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sq, running_mean, rstd,
+                     (float*)nullptr, (float*)nullptr, C, (int64_t)1, eps, 0.f);
+  hipLaunchKernelGGL(bn_apply_k, dim3(nblk(M * C)), dim3(256), 0, st, x, running_mean, rstd, gamma, beta, y,
+                     (float*)nullptr, M, C, act);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+// BN backward through the fused activation: dy (grad of act output) -> dx, dgamma, dbeta
+extern "C" int b2p_batchnorm_bwd(const float* dy, const float* pre, const float* x, const float* mean,
+                                 const float* rstd, const float* gamma, float* dx, float* dgamma, float* dbeta,
+                                 int64_t M, int64_t C, int act, float* workspace, b2p_stream_t stream) {
+  B2P_CHECK_ARG(dy && pre && x && mean && rstd && gamma && dx && dgamma && dbeta && workspace, "batchnorm_bwd: NULL");
+  hipStream_t st = (hipStream_t)stream;
+  if (M <= 0) return 0;
+  float* g = workspace;                 // M*C
+  float* part = workspace + M * C + 4 * C;
+  hipLaunchKernelGGL(bn_grad_pre_k, dim3(nblk(M * C)), dim3(256), 0, st, dy, pre, g, M * C, act);
+  if (colsum_impl(g, nullptr, 1, M, C, C, 0, 0, dbeta, 0, part, st)) return 1;
+  hipLaunchKernelGGL(bn_gxhat_k, dim3(nblk(M * C)), dim3(256), 0, st, g, x, mean, rstd, dx, M, C);
+  if (colsum_impl(dx, nullptr, 1, M, C, C, 0, 0, dgamma, 0, part, st)) return 1;
+  hipLaunchKernelGGL(bn_bwd_dx_k, dim3(nblk(M * C)), dim3(256), 0, st, g, x, mean, rstd, gamma, dbeta, dgamma, dx, M,
+                     C, M);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t seed, float scale,
+                                  b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && y, "dropout_scaled: NULL");
+  B2P_CHECK_ARG(p >= 0.f && p < 1.f, "dropout_scaled: p in [0,1)");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(dropout_scale_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, y, n,
+                     b2p_dropout_threshold(p), p > 0.f ? scale / (1.f - p) : scale, seed, p > 0.f ? 1 : 0);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}

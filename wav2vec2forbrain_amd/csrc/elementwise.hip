@@ -20,11 +20,13 @@ __global__ void __launch_bounds__(256) colsum_p1(const float* __restrict__ X, co
   float s = 0.f;
   if (n < N) {
     const float* xp = X + b * bstride + n;
-    const float* yp = Y ? Y + b * bstride + n : nullptr;
+    const float* yp = (Y && mode == 2) ? Y + b * bstride + n : nullptr;
+    const float yc = (Y && mode == 3) ? Y[(int64_t)b * N + n] : 0.f;
 #pragma unroll 8
     for (int64_t m = m0 + rl; m < m1; m += 4) {
       const float x = xp[m * ld];
-      s += mode == 0 ? x : (mode == 1 ? x * x : x * yp[m * ld]);
+      const float dxc = x - yc;
+      s += mode == 0 ? x : (mode == 1 ? x * x : (mode == 2 ? x * yp[m * ld] : dxc * dxc));
     }
   }
   red[rl][c] = s;
@@ -44,6 +46,9 @@ __global__ void colsum_p2(const float* __restrict__ part, int nblk, int64_t N, f
   *o = accumulate ? *o + s : s;
 }
 
+}  // namespace
+
+// out[b][n] (+)= sum_m f(X[b][m][n]); mode 0: x, 1: x^2, 2: x*Y[b][m][n], 3: (x - Y[b][n])^2
 int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_t N, int64_t ld,
                 int64_t bstride, int mode, float* out, int accumulate, float* part, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
@@ -55,6 +60,8 @@ int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_
   B2P_CHECK_LAUNCH();
   return 0;
 }
+
+namespace {
 
 // ------------------------------------------------------------------ dropout
 __global__ void dropout_k(const float* __restrict__ x, float* __restrict__ y, int64_t n, uint32_t thr,

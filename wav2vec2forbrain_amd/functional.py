@@ -588,6 +588,52 @@ def pos_conv_ln(e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, training):
 
 
 # =====================================================================================
+# attention core shared by the w2v and Conformer layers: softmax(Q K^T * scale) -> dropout -> @ V
+# qkv (B*T, 3D) laid out [b][t][q|k|v][h][dh]
+# =====================================================================================
+def _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seed):
+    D = nh * dh
+    dev = qkv.device
+    Tp = (T + 3) // 4 * 4
+    S = torch.empty(B, nh, T, Tp, device=dev)
+    gemm(T, T, dh, op(qkv, 0, 3 * D, True, bs1=T * 3 * D, bs2=dh), op(qkv, D, 3 * D, True, bs1=T * 3 * D, bs2=dh),
+         S, Tp, cbs1=nh * T * Tp, cbs2=T * Tp, nz1=B, nz2=nh, alpha=dh ** -0.5)
+    P = torch.empty_like(S)
+    Pd = torch.empty_like(S) if p_attn > 0 else P
+    _lib.call("b2p_softmax_fwd", _p(S), _p(P), _p(Pd), B * nh * T, T, Tp, float(p_attn), seed, _st())
+    del S
+    O = torch.empty(B * T, D, device=dev)
+    gemm(T, dh, T, op(Pd, 0, Tp, True, bs1=nh * T * Tp, bs2=T * Tp),
+         op(qkv, 2 * D, 3 * D, False, bs1=T * 3 * D, bs2=dh), O, D, cbs1=T * D, cbs2=dh, nz1=B, nz2=nh)
+    return P, (Pd if p_attn > 0 else None), O
+
+
+def _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seed):
+    """returns dqkv (B*T, 3D) = [dQ | dK | dV]"""
+    D = nh * dh
+    dev = qkv.device
+    Tp = P.shape[-1]
+    Pd = P if Pd is None else Pd
+    scale = dh ** -0.5
+    dPd = torch.empty(B, nh, T, Tp, device=dev)
+    gemm(T, T, dh, op(dO, 0, D, True, bs1=T * D, bs2=dh), op(qkv, 2 * D, 3 * D, True, bs1=T * 3 * D, bs2=dh),
+         dPd, Tp, cbs1=nh * T * Tp, cbs2=T * Tp, nz1=B, nz2=nh)
+    dqkv = torch.empty(B * T, 3 * D, device=dev)
+    gemm(T, dh, T, op(Pd, 0, Tp, False, bs1=nh * T * Tp, bs2=T * Tp), op(dO, 0, D, False, bs1=T * D, bs2=dh),
+         dqkv, 3 * D, c_off=2 * D, cbs1=T * 3 * D, cbs2=dh, nz1=B, nz2=nh)
+    dS = torch.empty_like(dPd)
+    _lib.call("b2p_softmax_bwd", _p(P), _p(dPd), _p(dS), B * nh * T, T, Tp, float(p_attn), seed, _st())
+    del dPd
+    gemm(T, dh, T, op(dS, 0, Tp, True, bs1=nh * T * Tp, bs2=T * Tp),
+         op(qkv, D, 3 * D, False, bs1=T * 3 * D, bs2=dh), dqkv, 3 * D, c_off=0, cbs1=T * 3 * D, cbs2=dh,
+         nz1=B, nz2=nh, alpha=scale)
+    gemm(T, dh, T, op(dS, 0, Tp, False, bs1=nh * T * Tp, bs2=T * Tp),
+         op(qkv, 0, 3 * D, False, bs1=T * 3 * D, bs2=dh), dqkv, 3 * D, c_off=D, cbs1=T * 3 * D, cbs2=dh,
+         nz1=B, nz2=nh, alpha=scale)
+    return dqkv
+
+
+# =====================================================================================
 # post-LN transformer encoder layer (Wav2Vec2EncoderLayer)
 # =====================================================================================
 class _EncoderLayer(torch.autograd.Function):
@@ -600,24 +646,11 @@ class _EncoderLayer(torch.autograd.Function):
         NT = B * T
         F = w1.shape[0]
         dev = x.device
-        Tp = (T + 3) // 4 * 4
-        scale = dh ** -0.5
         x2 = x.view(NT, D)
         qkv = torch.empty(NT, 3 * D, device=dev)
         for i, (w, b) in enumerate(((wq, bq), (wk, bk), (wv, bv))):
             gemm(NT, D, D, op(x2, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=b)
-        # scores S[b,h] = Q K^T * scale
-        S = torch.empty(B, nh, T, Tp, device=dev)
-        gemm(T, T, dh, op(qkv, 0, 3 * D, True, bs1=T * 3 * D, bs2=dh), op(qkv, D, 3 * D, True, bs1=T * 3 * D, bs2=dh),
-             S, Tp, cbs1=nh * T * Tp, cbs2=T * Tp, nz1=B, nz2=nh, alpha=scale)
-        P = torch.empty_like(S)
-        Pd = torch.empty_like(S) if p_attn > 0 else P
-        _lib.call("b2p_softmax_fwd", _p(S), _p(P), _p(Pd), B * nh * T, T, Tp, float(p_attn), seeds[0], _st())
-        del S
-        # O[b,t,h,:] = Pd[b,h] @ V[b,:,h,:]
-        O = torch.empty(NT, D, device=dev)
-        gemm(T, dh, T, op(Pd, 0, Tp, True, bs1=nh * T * Tp, bs2=T * Tp),
-             op(qkv, 2 * D, 3 * D, False, bs1=T * 3 * D, bs2=dh), O, D, cbs1=T * D, cbs2=dh, nz1=B, nz2=nh)
+        P, Pd, O = _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seeds[0])
         # y1 = x + dropout(O Wo^T + bo)
         y1 = torch.empty(NT, D, device=dev)
         gemm(NT, D, D, op(O, 0, D, True), op(wo, 0, D, True), y1, D, bias=bo, drop_p=p_hid, seed=seeds[1],
@@ -632,7 +665,7 @@ class _EncoderLayer(torch.autograd.Function):
         gemm(NT, D, F, op(f, 0, F, True), op(w2, 0, F, True), y2, D, bias=b2, drop_p=p_hid, seed=seeds[3],
              residual=x1)
         out, m2, r2 = _ln_fwd(y2, g2, be2, eps)
-        ctx.save_for_backward(x, qkv, P, Pd if p_attn > 0 else None, O, y1, x1, m1, r1, pre, f, y2, m2, r2,
+        ctx.save_for_backward(x, qkv, P, Pd, O, y1, x1, m1, r1, pre, f, y2, m2, r2,
                               wq, wk, wv, wo, g1, w1, w2, g2)
         ctx.cfg = cfg
         ctx.has_b = [b is not None for b in (bq, bk, bv, bo, b1, b2)]
@@ -642,8 +675,6 @@ class _EncoderLayer(torch.autograd.Function):
     def backward(ctx, dout):
         (x, qkv, P, Pd, O, y1, x1, m1, r1, pre, f, y2, m2, r2, wq, wk, wv, wo, g1, w1, w2, g2) = ctx.saved_tensors
         nh, eps, p_attn, p_hid, p_act, seeds = ctx.cfg
-        if Pd is None:
-            Pd = P
         B, T, D = x.shape
         dh = D // nh
         NT = B * T
@@ -682,25 +713,7 @@ class _EncoderLayer(torch.autograd.Function):
             mm_tn(dz1, O, dwo)
         dO = torch.empty(NT, D, device=dev)
         mm_nn(dz1, wo, dO)
-        # attention backward
-        dPd = torch.empty(B, nh, T, Tp, device=dev)
-        gemm(T, T, dh, op(dO, 0, D, True, bs1=T * D, bs2=dh), op(qkv, 2 * D, 3 * D, True, bs1=T * 3 * D, bs2=dh),
-             dPd, Tp, cbs1=nh * T * Tp, cbs2=T * Tp, nz1=B, nz2=nh)
-        dqkv = torch.empty(NT, 3 * D, device=dev)
-        # dV = Pd^T dO
-        gemm(T, dh, T, op(Pd, 0, Tp, False, bs1=nh * T * Tp, bs2=T * Tp), op(dO, 0, D, False, bs1=T * D, bs2=dh),
-             dqkv, 3 * D, c_off=2 * D, cbs1=T * 3 * D, cbs2=dh, nz1=B, nz2=nh)
-        dS = torch.empty_like(dPd)
-        _lib.call("b2p_softmax_bwd", _p(P), _p(dPd), _p(dS), B * nh * T, T, Tp, float(p_attn), seeds[0], _st())
-        del dPd
-        # dQ = dS K * scale ; dK = dS^T Q * scale
-        gemm(T, dh, T, op(dS, 0, Tp, True, bs1=nh * T * Tp, bs2=T * Tp),
-             op(qkv, D, 3 * D, False, bs1=T * 3 * D, bs2=dh), dqkv, 3 * D, c_off=0, cbs1=T * 3 * D, cbs2=dh,
-             nz1=B, nz2=nh, alpha=scale)
-        gemm(T, dh, T, op(dS, 0, Tp, False, bs1=nh * T * Tp, bs2=T * Tp),
-             op(qkv, 0, 3 * D, False, bs1=T * 3 * D, bs2=dh), dqkv, 3 * D, c_off=D, cbs1=T * 3 * D, cbs2=dh,
-             nz1=B, nz2=nh, alpha=scale)
-        del dS
+        dqkv = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seeds[0])
         grads_w = []
         for i, w in enumerate((wq, wk, wv)):
             gw = gb = None
@@ -762,3 +775,296 @@ def ctc_loss(logits, targets, in_lens, tgt_lens, blank=0):
     in_lens = in_lens.to(torch.int32).contiguous()
     tgt_lens = tgt_lens.to(torch.int64).contiguous()
     return _CTC.apply(logits.contiguous(), targets, in_lens, tgt_lens, blank)
+
+
+# =====================================================================================
+# Conformer (transformers Wav2Vec2ConformerEncoderLayer, rotary variant) — reference
+# src/model/w2v_conformer_custom_feat_extractor.py:62-112
+# =====================================================================================
+class _LayerNorm(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, g, b, eps):
+        _chk(x, "layer_norm.x")
+        C = x.shape[-1]
+        x2 = x.view(-1, C)
+        y, mean, rstd = _ln_fwd(x2, g, b, eps)
+        ctx.save_for_backward(x2, g, mean, rstd)
+        return y.view(x.shape)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, g, mean, rstd = ctx.saved_tensors
+        dx, dg, db, _ = _ln_bwd(dy.contiguous().view(x2.shape), x2, g, mean, rstd)
+        return dx.view(dy.shape), dg, db, None
+
+
+def layer_norm(x, g, b, eps):
+    return _LayerNorm.apply(x.contiguous(), g, b, float(eps))
+
+
+def _dropout_scaled(x, p, seed, scale):
+    y = torch.empty_like(x)
+    _lib.call("b2p_dropout_scaled", _p(x), _p(y), x.numel(), float(p), seed, float(scale), _st())
+    return y
+
+
+class _FFNBlock(torch.autograd.Function):
+    """y = x + scale * dropout_h(W2 dropout_a(act(W1 LN(x) + b1)) + b2)   (macaron half-step, scale 0.5)"""
+
+    @staticmethod
+    def forward(ctx, x, g, b, w1, b1, w2, b2, cfg):
+        act, eps, p_act, p_hid, s_act, s_hid, scale = cfg
+        _chk(x, "ffn.x")
+        B, T, D = x.shape
+        NT, F = B * T, w1.shape[0]
+        dev = x.device
+        x2 = x.view(NT, D)
+        h, mean, rstd = _ln_fwd(x2, g, b, eps)
+        pre = torch.empty(NT, F, device=dev)
+        f = torch.empty(NT, F, device=dev)
+        gemm(NT, F, D, op(h, 0, D, True), op(w1, 0, D, True), f, F, bias=b1, pre_out=pre, act=act, drop_p=p_act,
+             seed=s_act)
+        bs = b2 * scale if b2 is not None else None
+        y = torch.empty(NT, D, device=dev)
+        gemm(NT, D, F, op(f, 0, F, True), op(w2, 0, F, True), y, D, alpha=scale, bias=bs, drop_p=p_hid, seed=s_hid,
+             residual=x2)
+        ctx.save_for_backward(x2, h, mean, rstd, pre, f, g, w1, w2)
+        ctx.cfg = cfg
+        ctx.shape = (B, T, D)
+        ctx.has_b = (b1 is not None, b2 is not None)
+        return y.view(B, T, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, mean, rstd, pre, f, g, w1, w2 = ctx.saved_tensors
+        act, eps, p_act, p_hid, s_act, s_hid, scale = ctx.cfg
+        NT, D = x2.shape
+        F = w1.shape[0]
+        dev = x2.device
+        ng = ctx.needs_input_grad
+        dy = dy.contiguous().view(NT, D)
+        dz = _dropout_scaled(dy, p_hid, s_hid, scale)
+        dw2 = db2 = dw1 = db1 = None
+        if ng[5]:
+            dw2 = torch.empty_like(w2)
+            mm_tn(dz, f, dw2)
+        if ctx.has_b[1] and ng[6]:
+            db2 = torch.empty(D, device=dev)
+            colsum(dz, NT, D, db2)
+        dpre = torch.empty(NT, F, device=dev)
+        gemm(NT, F, D, op(dz, 0, D, True), op(w2, 0, F, False), dpre, F, drop_p=p_act, seed=s_act, act_bwd=act,
+             aux=pre)
+        if ng[3]:
+            dw1 = torch.empty_like(w1)
+            mm_tn(dpre, h, dw1)
+        if ctx.has_b[0] and ng[4]:
+            db1 = torch.empty(F, device=dev)
+            colsum(dpre, NT, F, db1)
+        dh = torch.empty(NT, D, device=dev)
+        mm_nn(dpre, w1, dh)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        return dx.view(ctx.shape), dg, db, dw1, db1, dw2, db2, None
+
+
+_ROT = {}
+
+
+def rotary_tables(T, D, base, device):
+    """TF conf Wav2Vec2ConformerRotaryPositionalEmbedding: inv_freq = base^(-arange(0,D,2)/D),
+    emb = cat(t*inv_freq, t*inv_freq) -> (cos, sin) of shape (T, D). Cached per (T, D, base)."""
+    key = (T, D, base, str(device))
+    if key not in _ROT:
+        inv_freq = 1.0 / (base ** (torch.arange(0, D, 2, dtype=torch.int64).float() / D))
+        t = torch.arange(T).type_as(inv_freq)
+        freqs = torch.einsum("i,j->ij", t, inv_freq)
+        emb = torch.cat((freqs, freqs), dim=-1)
+        _ROT[key] = (emb.cos().contiguous().to(device), emb.sin().contiguous().to(device))
+    return _ROT[key]
+
+
+class _ConformerAttnBlock(torch.autograd.Function):
+    """y = x + dropout(linear_out(Attn(q=k=rotary(LN x), v=LN x)))  (TF conf Wav2Vec2ConformerSelfAttention)"""
+
+    @staticmethod
+    def forward(ctx, x, g, b, wq, bq, wk, bk, wv, bv, wo, bo, cos_t, sin_t, cfg):
+        nh, eps, p_attn, p_out, seeds = cfg
+        _chk(x, "conformer_attn.x")
+        B, T, D = x.shape
+        NT, hd = B * T, D // nh
+        dev = x.device
+        x2 = x.view(NT, D)
+        h, mean, rstd = _ln_fwd(x2, g, b, eps)
+        if cos_t is not None:
+            hr = torch.empty_like(h)
+            _lib.call("b2p_rotary", _p(h), _p(cos_t), _p(sin_t), _p(hr), B, T, nh, hd, D, 0, _st())
+        else:
+            hr = h
+        qkv = torch.empty(NT, 3 * D, device=dev)
+        for i, (w, bb, src) in enumerate(((wq, bq, hr), (wk, bk, hr), (wv, bv, h))):
+            gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=bb)
+        P, Pd, O = _attn_core_fwd(qkv, B, T, nh, hd, p_attn, seeds[0])
+        y = torch.empty(NT, D, device=dev)
+        gemm(NT, D, D, op(O, 0, D, True), op(wo, 0, D, True), y, D, bias=bo, drop_p=p_out, seed=seeds[1], residual=x2)
+        ctx.save_for_backward(x2, h, hr if cos_t is not None else None, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo,
+                              cos_t, sin_t)
+        ctx.cfg = cfg
+        ctx.shape = (B, T, D)
+        ctx.has_b = [t is not None for t in (bq, bk, bv, bo)]
+        return y.view(B, T, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo, cos_t, sin_t = ctx.saved_tensors
+        nh, eps, p_attn, p_out, seeds = ctx.cfg
+        B, T, D = ctx.shape
+        NT, hd = B * T, D // nh
+        dev = x2.device
+        ng = ctx.needs_input_grad
+        hr_ = h if hr is None else hr
+        dy = dy.contiguous().view(NT, D)
+        dz = _dropout_scaled(dy, p_out, seeds[1], 1.0)
+        dwo = dbo = None
+        if ng[9]:
+            dwo = torch.empty_like(wo)
+            mm_tn(dz, O, dwo)
+        if ctx.has_b[3] and ng[10]:
+            dbo = torch.empty(D, device=dev)
+            colsum(dz, NT, D, dbo)
+        dO = torch.empty(NT, D, device=dev)
+        mm_nn(dz, wo, dO)
+        dqkv = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, hd, p_attn, seeds[0])
+        grads = []
+        for i, (w, src) in enumerate(((wq, hr_), (wk, hr_), (wv, h))):
+            gw = gb = None
+            if ng[3 + 2 * i]:
+                gw = torch.empty_like(w)
+                gemm(D, D, NT, op(dqkv, i * D, 3 * D, False), op(src, 0, D, False), gw, D)
+            if ctx.has_b[i] and ng[4 + 2 * i]:
+                gb = torch.empty(D, device=dev)
+                colsum(_view_off(dqkv, i * D), NT, D, gb, ld=3 * D)
+            grads += [gw, gb]
+        # dh = rotary^T(dQ Wq + dK Wk) + dV Wv
+        dh = torch.empty(NT, D, device=dev)
+        if cos_t is not None:
+            dhr = torch.empty(NT, D, device=dev)
+            gemm(NT, D, D, op(dqkv, 0, 3 * D, True), op(wq, 0, D, False), dhr, D)
+            gemm(NT, D, D, op(dqkv, D, 3 * D, True), op(wk, 0, D, False), dhr, D, beta=1.0)
+            _lib.call("b2p_rotary", _p(dhr), _p(cos_t), _p(sin_t), _p(dh), B, T, nh, hd, D, 1, _st())
+            gemm(NT, D, D, op(dqkv, 2 * D, 3 * D, True), op(wv, 0, D, False), dh, D, beta=1.0)
+        else:
+            for i, w in enumerate((wq, wk, wv)):
+                gemm(NT, D, D, op(dqkv, i * D, 3 * D, True), op(w, 0, D, False), dh, D, beta=0.0 if i == 0 else 1.0)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        return (dx.view(B, T, D), dg, db, *grads, dwo, dbo, None, None, None)
+
+
+class _ConvModule(torch.autograd.Function):
+    """y = x + dropout(pw2(act(BN(dwconv(GLU(pw1(LN x)))))))   (TF conf Wav2Vec2ConformerConvolutionModule)"""
+
+    @staticmethod
+    def forward(ctx, x, g, b, w_pw1, w_dw, bn_g, bn_b, w_pw2, bn_rm, bn_rv, cfg):
+        act, eps, bn_eps, momentum, p, seed, training = cfg
+        _chk(x, "conv_module.x")
+        B, T, D = x.shape
+        NT = B * T
+        K = w_dw.shape[-1]
+        dev = x.device
+        x2 = x.view(NT, D)
+        h, mean, rstd = _ln_fwd(x2, g, b, eps)
+        a = torch.empty(NT, 2 * D, device=dev)
+        gemm(NT, 2 * D, D, op(h, 0, D, True), op(w_pw1, 0, D, True), a, 2 * D)
+        u = torch.empty(NT, D, device=dev)
+        _lib.call("b2p_glu_fwd", _p(a), _p(u), NT, D, _st())
+        c = torch.empty(NT, D, device=dev)
+        _lib.call("b2p_dwconv_fwd", _p(u), _p(w_dw), _p(c), B, T, D, K, _st())
+        s = torch.empty(NT, D, device=dev)
+        ws = torch.empty(int(_lib.load().b2p_batchnorm_workspace(NT, D)), device=dev)
+        if training:
+            pre = torch.empty(NT, D, device=dev)
+            bm = torch.empty(D, device=dev)
+            br = torch.empty(D, device=dev)
+            _lib.call("b2p_batchnorm_fwd", _p(c), _p(bn_g), _p(bn_b), _p(bn_rm), _p(bn_rv), _p(s), _p(pre), _p(bm),
+                      _p(br), NT, D, float(bn_eps), float(momentum), act, _p(ws), _st())
+        else:
+            pre = bm = br = None
+            _lib.call("b2p_batchnorm_eval", _p(c), _p(bn_g), _p(bn_b), _p(bn_rm), _p(bn_rv), _p(s), NT, D,
+                      float(bn_eps), act, _p(ws), _st())
+        y = torch.empty(NT, D, device=dev)
+        gemm(NT, D, D, op(s, 0, D, True), op(w_pw2, 0, D, True), y, D, drop_p=p, seed=seed, residual=x2)
+        ctx.save_for_backward(x2, h, mean, rstd, a, u, c, pre, bm, br, s, g, w_pw1, w_dw, bn_g, w_pw2)
+        ctx.cfg = cfg
+        ctx.shape = (B, T, D, K)
+        return y.view(B, T, D)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x2, h, mean, rstd, a, u, c, pre, bm, br, s, g, w_pw1, w_dw, bn_g, w_pw2 = ctx.saved_tensors
+        act, eps, bn_eps, momentum, p, seed, training = ctx.cfg
+        if not training:
+            raise RuntimeError("conv module backward in eval mode (running BN statistics) is not supported")
+        B, T, D, K = ctx.shape
+        NT = B * T
+        dev = x2.device
+        ng = ctx.needs_input_grad
+        dy = dy.contiguous().view(NT, D)
+        do = _dropout_scaled(dy, p, seed, 1.0)
+        dpw2 = None
+        if ng[7]:
+            dpw2 = torch.empty_like(w_pw2)
+            mm_tn(do, s, dpw2.view(D, D))
+        ds = torch.empty(NT, D, device=dev)
+        mm_nn(do, w_pw2.view(D, D), ds)
+        dc = torch.empty(NT, D, device=dev)
+        dbn_g = torch.empty(D, device=dev)
+        dbn_b = torch.empty(D, device=dev)
+        ws = torch.empty(int(_lib.load().b2p_batchnorm_workspace(NT, D)), device=dev)
+        _lib.call("b2p_batchnorm_bwd", _p(ds), _p(pre), _p(c), _p(bm), _p(br), _p(bn_g), _p(dc), _p(dbn_g), _p(dbn_b),
+                  NT, D, act, _p(ws), _st())
+        du = torch.empty(NT, D, device=dev)
+        ddw = torch.empty_like(w_dw) if ng[4] else None
+        wsd = torch.empty(int(_lib.load().b2p_dwconv_bwd_workspace(B, T, D, K)), device=dev)
+        _lib.call("b2p_dwconv_bwd", _p(u), _p(w_dw), _p(dc), _p(du), _p(ddw), B, T, D, K, _p(wsd), _st())
+        da = torch.empty(NT, 2 * D, device=dev)
+        _lib.call("b2p_glu_bwd", _p(a), _p(du), _p(da), NT, D, _st())
+        dpw1 = None
+        if ng[3]:
+            dpw1 = torch.empty_like(w_pw1)
+            mm_tn(da, h, dpw1.view(2 * D, D))
+        dh = torch.empty(NT, D, device=dev)
+        mm_nn(da, w_pw1.view(2 * D, D), dh)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        return dx.view(B, T, D), dg, db, dpw1, ddw, dbn_g, dbn_b, dpw2, None, None, None
+
+
+def conformer_ffn(x, ln, w1, b1, w2, b2, act, p_act, p_hid, training, scale=0.5):
+    if not training:
+        p_act = p_hid = 0.0
+    cfg = (act, float(ln.eps), float(p_act), float(p_hid), SEEDS.next() if p_act > 0 else 0,
+           SEEDS.next() if p_hid > 0 else 0, float(scale))
+    return _FFNBlock.apply(x.contiguous(), ln.weight, ln.bias, w1, b1, w2, b2, cfg)
+
+
+def conformer_attention(x, ln, q, k, v, o, nh, rotary, p_attn, p_out, training):
+    if not training:
+        p_attn = p_out = 0.0
+    B, T, D = x.shape
+    cos_t = sin_t = None
+    if rotary is not None:
+        cos_t, sin_t = rotary_tables(T, D // nh, rotary, x.device)
+    seeds = (SEEDS.next() if p_attn > 0 else 0, SEEDS.next() if p_out > 0 else 0)
+    cfg = (nh, float(ln.eps), float(p_attn), float(p_out), seeds)
+    return _ConformerAttnBlock.apply(x.contiguous(), ln.weight, ln.bias, q.weight, q.bias, k.weight, k.bias, v.weight,
+                                     v.bias, o.weight, o.bias, cos_t, sin_t, cfg)
+
+
+def conformer_conv_module(x, cm, act, p, training):
+    bn = cm.batch_norm
+    if not training:
+        p = 0.0
+    cfg = (act, float(cm.layer_norm.eps), float(bn.eps), float(bn.momentum if bn.momentum is not None else 0.1),
+           float(p), SEEDS.next() if p > 0 else 0, bool(training))
+    if training and bn.num_batches_tracked is not None:
+        bn.num_batches_tracked.add_(1)
+    return _ConvModule.apply(x.contiguous(), cm.layer_norm.weight, cm.layer_norm.bias, cm.pointwise_conv1.weight,
+                             cm.depthwise_conv.weight, bn.weight, bn.bias, cm.pointwise_conv2.weight, bn.running_mean,
+                             bn.running_var, cfg)
