@@ -30,7 +30,18 @@ BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md,
 STEP_TFLOP_BASE_BS32 = 5.216
 
 
-def make_config(bs, L):
+# train-step FLOPs per config at bs=32, L=1024
+STEP_TFLOP = {"base": 5.216, "conformer": 30.06}
+
+
+def make_config(bs, L, kind="base"):
+    if kind == "conformer":
+        # BASELINE configs[2]: wav2vec2-conformer-rope-large (1024/24L/16H/4096, k31), README brain
+        # encoder H512x3, fc [256]
+        return dict(name="bench_conformer", seed=42, B=bs, L=L, in_lens=[L] * bs, tgt_range=(60, 120),
+                    hidden_size=1024, layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512,
+                    gru_layers=3, bidirectional=True, fc_hidden=[256], learnable_h0=False, full_grad_max=0,
+                    infeasible=False, conformer=True, dw_kernel=31)
     return dict(name="bench_base", seed=42, B=bs, L=L, in_lens=[L] * bs, tgt_range=(60, 120), hidden_size=768,
                 layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2,
                 bidirectional=True, fc_hidden=[], learnable_h0=False, full_grad_max=0, infeasible=False)
@@ -97,6 +108,8 @@ def main():
     ap.add_argument("--bs", type=int, default=32)
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--config", choices=["base", "conformer"], default="base",
+                    help="base = BASELINE configs[1] (headline); conformer = configs[2]")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -114,7 +127,7 @@ def main():
     from wav2vec2forbrain_amd.train.ddp import GradBucketReducer, unused_param_names
 
     Fn.set_precision("bf16")
-    cfg = make_config(args.bs, args.seq)
+    cfg = make_config(args.bs, args.seq, args.config)
     model = build(cfg, device)
     model.train()
     skip = unused_param_names(model)
@@ -159,7 +172,7 @@ def main():
     steps_per_s = args.steps / dt * 1.0          # global steps/s (every rank does one step per step)
     gemm_ms, gemm_n, gemm_flops = ms
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
-    step_tflop = STEP_TFLOP_BASE_BS32 * args.bs / 32 * args.seq / 1024
+    step_tflop = STEP_TFLOP[args.config] * args.bs / 32 * args.seq / 1024
     res = {
         "metric": "train steps/sec + CTC loss, b2p2t_gru+w2v bs=32 seq=1024",
         "value": round(steps_per_s, 4),
@@ -173,8 +186,10 @@ def main():
         "vs_baseline": None,
         "dtype": "bf16",
         "data": "synthetic (x~N(0,1) 256-ch windows, random-init weights of the wav2vec2-base architecture)",
-        "config": {"workload": "b2p2t_gru+w2v wav2vec2-base (12L/768), GRU H256x2 bidir, train mode, "
-                               "unfreeze=brain_encoder, Adam", "global_batch": args.bs * world,
+        "config": {"workload": ("b2p2t_gru+w2v wav2vec2-base (12L/768), GRU H256x2 bidir, train mode, "
+                                "unfreeze=brain_encoder, Adam") if args.config == "base" else
+                               ("b2p2t_gru+w2v_conformer rope-large (24L/1024, k31), GRU H512x3 bidir, fc [256], "
+                                "train mode, unfreeze=brain_encoder, Adam"), "global_batch": args.bs * world,
                    "per_gpu_batch": args.bs, "seq_len": args.seq, "parallelism": f"dp{world}"},
         "ctc_loss": round(losses[-1], 5),
         "samples_per_s": round(steps_per_s * args.bs * world, 2),
@@ -184,7 +199,9 @@ def main():
                      "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": None,
                      "launches": gemm_n, "avg_launch_us": round(gemm_ms * 1e3 / max(gemm_n, 1), 2)},
     }
-    if world == 1 and not args.no_cpu_baseline:
+    if args.config != "base":
+        res["metric"] = "train steps/sec + CTC loss, b2p2t_gru+w2v_conformer bs=32 seq=1024"
+    if world == 1 and not args.no_cpu_baseline and args.config == "base":
         res["cpu_baseline"] = cpu_baseline(L=args.seq)
     print(json.dumps(res), flush=True)
     if world > 1:

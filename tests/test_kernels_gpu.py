@@ -271,10 +271,16 @@ def test_conformer_elementwise_kernels():
     B, T, nh, dh, K = 2, 37, 4, 16, 7
     D = nh * dh
     x = torch.randn(B, T, D)
+    keep = []                       # device copies must outlive the raw-pointer calls
+
+    def dev(t):
+        d = t.cuda()
+        keep.append(d)
+        return d.data_ptr()
     # rotary
     cos_t, sin_t = Fn.rotary_tables(T, dh, 10000, "cuda")
     out = torch.empty(B * T, D, device="cuda")
-    Fn._lib.call("b2p_rotary", x.cuda().data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), out.data_ptr(), B, T, nh, dh,
+    Fn._lib.call("b2p_rotary", dev(x), cos_t.data_ptr(), sin_t.data_ptr(), out.data_ptr(), B, T, nh, dh,
                  D, 0, Fn._st())
     xr = x.clone().requires_grad_(True)
     ref = rotary_apply(xr, nh, 10000)
@@ -282,20 +288,20 @@ def test_conformer_elementwise_kernels():
     g = torch.randn_like(ref)
     (gx,) = torch.autograd.grad(ref, xr, g)
     back = torch.empty(B * T, D, device="cuda")
-    Fn._lib.call("b2p_rotary", g.cuda().data_ptr(), cos_t.data_ptr(), sin_t.data_ptr(), back.data_ptr(), B, T, nh, dh,
+    Fn._lib.call("b2p_rotary", dev(g), cos_t.data_ptr(), sin_t.data_ptr(), back.data_ptr(), B, T, nh, dh,
                  D, 1, Fn._st())
     assert _rel(back.view(B, T, D).cpu(), gx) < 1e-5
     # GLU
     a = torch.randn(B * T, 2 * D)
     u = torch.empty(B * T, D, device="cuda")
-    Fn._lib.call("b2p_glu_fwd", a.cuda().data_ptr(), u.data_ptr(), B * T, D, Fn._st())
+    Fn._lib.call("b2p_glu_fwd", dev(a), u.data_ptr(), B * T, D, Fn._st())
     ar = a.clone().requires_grad_(True)
     ur = F.glu(ar, dim=1)
     assert _rel(u.cpu(), ur) < 1e-6
     gu = torch.randn_like(ur)
     (ga,) = torch.autograd.grad(ur, ar, gu)
     da = torch.empty(B * T, 2 * D, device="cuda")
-    Fn._lib.call("b2p_glu_bwd", a.cuda().data_ptr(), gu.cuda().data_ptr(), da.data_ptr(), B * T, D, Fn._st())
+    Fn._lib.call("b2p_glu_bwd", dev(a), dev(gu), da.data_ptr(), B * T, D, Fn._st())
     assert _rel(da.cpu(), ga) < 1e-5
     # depthwise conv
     w = torch.randn(D, 1, K)
@@ -303,14 +309,14 @@ def test_conformer_elementwise_kernels():
     wc = w.clone().requires_grad_(True)
     yc = F.conv1d(xc.transpose(1, 2), wc, padding=(K - 1) // 2, groups=D).transpose(1, 2)
     y = torch.empty(B, T, D, device="cuda")
-    Fn._lib.call("b2p_dwconv_fwd", x.cuda().data_ptr(), w.cuda().data_ptr(), y.data_ptr(), B, T, D, K, Fn._st())
+    Fn._lib.call("b2p_dwconv_fwd", dev(x), dev(w), y.data_ptr(), B, T, D, K, Fn._st())
     assert _rel(y.cpu(), yc) < 1e-5
     gy = torch.randn_like(yc)
     gxc, gwc = torch.autograd.grad(yc, (xc, wc), gy)
     dx = torch.empty(B, T, D, device="cuda")
     dw = torch.empty(D, 1, K, device="cuda")
     ws = torch.empty(int(Fn._lib.load().b2p_dwconv_bwd_workspace(B, T, D, K)), device="cuda")
-    Fn._lib.call("b2p_dwconv_bwd", x.cuda().data_ptr(), w.cuda().data_ptr(), gy.cuda().data_ptr(), dx.data_ptr(),
+    Fn._lib.call("b2p_dwconv_bwd", dev(x), dev(w), dev(gy), dx.data_ptr(),
                  dw.data_ptr(), B, T, D, K, ws.data_ptr(), Fn._st())
     assert _rel(dx.cpu(), gxc) < 1e-5 and _rel(dw.cpu(), gwc) < 1e-5
     # BatchNorm (train) + SiLU
@@ -328,7 +334,7 @@ def test_conformer_elementwise_kernels():
     rstd = torch.empty(D, device="cuda")
     rmg, rvg = rm.cuda(), rv.cuda()
     ws = torch.empty(int(Fn._lib.load().b2p_batchnorm_workspace(M, D)), device="cuda")
-    Fn._lib.call("b2p_batchnorm_fwd", xb.cuda().data_ptr(), gam.cuda().data_ptr(), bet.cuda().data_ptr(),
+    Fn._lib.call("b2p_batchnorm_fwd", dev(xb), dev(gam), dev(bet),
                  rmg.data_ptr(), rvg.data_ptr(), yb.data_ptr(), pre.data_ptr(), mean.data_ptr(), rstd.data_ptr(), M, D,
                  1e-5, 0.1, Fn.ACT["silu"], ws.data_ptr(), Fn._st())
     assert _rel(yb.cpu(), yr) < 1e-5
@@ -338,7 +344,7 @@ def test_conformer_elementwise_kernels():
     dxb = torch.empty(M, D, device="cuda")
     dg = torch.empty(D, device="cuda")
     db = torch.empty(D, device="cuda")
-    Fn._lib.call("b2p_batchnorm_bwd", gyb.cuda().data_ptr(), pre.data_ptr(), xb.cuda().data_ptr(), mean.data_ptr(),
-                 rstd.data_ptr(), gam.cuda().data_ptr(), dxb.data_ptr(), dg.data_ptr(), db.data_ptr(), M, D,
+    Fn._lib.call("b2p_batchnorm_bwd", dev(gyb), pre.data_ptr(), dev(xb), mean.data_ptr(),
+                 rstd.data_ptr(), dev(gam), dxb.data_ptr(), dg.data_ptr(), db.data_ptr(), M, D,
                  Fn.ACT["silu"], ws.data_ptr(), Fn._st())
     assert _rel(dxb.cpu(), gx_) < 1e-4 and _rel(dg.cpu(), gg_) < 1e-4 and _rel(db.cpu(), gb_) < 1e-4
