@@ -298,7 +298,7 @@ def test_conformer_elementwise_kernels():
     ar = a.clone().requires_grad_(True)
     ur = F.glu(ar, dim=1)
     assert _rel(u.cpu(), ur) < 1e-6
-    gu = torch.randn_like(ur)
+    gu = torch.randn(ur.shape)
     (ga,) = torch.autograd.grad(ur, ar, gu)
     da = torch.empty(B * T, 2 * D, device="cuda")
     Fn._lib.call("b2p_glu_bwd", dev(a), dev(gu), da.data_ptr(), B * T, D, Fn._st())
@@ -311,7 +311,7 @@ def test_conformer_elementwise_kernels():
     y = torch.empty(B, T, D, device="cuda")
     Fn._lib.call("b2p_dwconv_fwd", dev(x), dev(w), y.data_ptr(), B, T, D, K, Fn._st())
     assert _rel(y.cpu(), yc) < 1e-5
-    gy = torch.randn_like(yc)
+    gy = torch.randn(yc.shape)            # contiguous (B, T, D)
     gxc, gwc = torch.autograd.grad(yc, (xc, wc), gy)
     dx = torch.empty(B, T, D, device="cuda")
     dw = torch.empty(D, 1, K, device="cuda")
@@ -339,7 +339,7 @@ def test_conformer_elementwise_kernels():
                  1e-5, 0.1, Fn.ACT["silu"], ws.data_ptr(), Fn._st())
     assert _rel(yb.cpu(), yr) < 1e-5
     assert _rel(rmg.cpu(), rm_ref) < 1e-5 and _rel(rvg.cpu(), rv_ref) < 1e-5
-    gyb = torch.randn_like(yr)
+    gyb = torch.randn(yr.shape)
     gx_, gg_, gb_ = torch.autograd.grad(yr, (xr, gr, br), gyb)
     dxb = torch.empty(M, D, device="cuda")
     dg = torch.empty(D, device="cuda")

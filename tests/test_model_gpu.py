@@ -47,9 +47,11 @@ def test_step_matches_reference_golden(name, mode):
             b = dict(model.named_buffers())[k[4:]]
             tol = 1e-3 if mode == "fp32" else 3e-2
             np.testing.assert_allclose(b.cpu().numpy(), fx[k], rtol=tol, atol=tol * np.abs(fx[k]).max())
-    lt = 2e-4 if mode == "fp32" else 3e-2
-    np.testing.assert_allclose(out.logits.detach().cpu().numpy(), fx["logits"], rtol=0,
-                               atol=lt * np.abs(fx["logits"]).max())
+    lg = out.logits.detach().cpu().numpy()
+    if mode == "fp32":
+        np.testing.assert_allclose(lg, fx["logits"], rtol=0, atol=2e-4 * np.abs(fx["logits"]).max())
+    else:   # bf16 through up to 24 layers: relative L2 error of the logits
+        assert np.linalg.norm(lg - fx["logits"]) <= 2e-2 * np.linalg.norm(fx["logits"])
     gmax = max(float(fx["gnorm/" + n]) for n in fx["param_names"])
     gtol = 2e-3 if mode == "fp32" else 5e-2
     params = dict(model.named_parameters())
