@@ -40,8 +40,9 @@ int b2p_timing_read(int family, float* total_ms, int* count, double* total_flops
 
 /* ------------------------------------------------------------------ GEMM
  * C[z](m,n) = epilogue( alpha * sum_k A[z](m,k) * B[z](k,n) ), bf16 MFMA (fp32 accumulate)
- * or exact-fp32 MFMA (precision=1). Operands are fp32 in HBM and converted while being
- * staged into LDS. Replaces every nn.Linear / matmul / conv-as-GEMM of the path:
+ * or exact-fp32 MFMA (precision=1). Operands are fp32 in HBM (converted while being staged
+ * into LDS) or bf16 in HBM (copied straight into LDS by global_load_lds, transposed on the LDS
+ * read with ds_read_b64_tr_b16 when the operand's contiguous dimension is m/n). Replaces every nn.Linear / matmul / conv-as-GEMM of the path:
  *   nn.Linear (TF w2v q/k/v/out_proj, FFN, lm_head: modeling_wav2vec2.py Wav2Vec2Attention,
  *   Wav2Vec2FeedForward; src/model/w2v_custom_feat_extractor.py:152;
  *   src/util/nn_helper.py:31-49 create_fully_connected),
@@ -52,7 +53,7 @@ int b2p_timing_read(int family, float* total_ms, int* count, double* total_flops
  *   conv view), attention QK^T / PV (eager_attention_forward).
  */
 typedef struct {
-  const float* ptr;
+  const void* ptr;       /* fp32 (dtype 0) or bf16 (dtype 1) elements                   */
   int64_t ld;            /* elements between consecutive outer indices                 */
   int64_t bs1, bs2;      /* batch strides for z1 = z / nz2 and z2 = z % nz2            */
   const int64_t* gather1;/* optional: offset uses gather1[z1] * bs1 instead of z1*bs1  */
@@ -61,7 +62,10 @@ typedef struct {
   /* implicit conv1d view: logical element (r, j) with r = b*conv_T_out + t and
    * j = tap*conv_Cg + ch maps to src[b*conv_sample_stride + (t*conv_stride + tap - conv_pad)*ld + ch],
    * zero when the frame index falls outside [0, conv_T_in). */
-  int32_t conv_T_out, conv_T_in, conv_stride, conv_pad, conv_Cg, _pad0;
+  int32_t conv_T_out, conv_T_in, conv_stride, conv_pad, conv_Cg;
+  int32_t dtype;         /* 0 = fp32 (converted while staged into LDS), 1 = bf16: both operands
+                          * bf16 selects the LDS-DMA kernel (global_load_lds, ptr/ld/bs/Cg
+                          * multiples of 8 elements, K % 8 == 0 for a k-contiguous operand)  */
   int64_t conv_sample_stride;
 } b2p_operand;
 
@@ -84,6 +88,8 @@ typedef struct {
   uint64_t drop_seed;
   const float* residual;      /* optional: added last                                          */
   int64_t ldr, rbs1, rbs2;
+  uint16_t* C16;              /* optional bf16 copy of the final value (strides of C); C may be
+                               * NULL when only the bf16 copy is wanted (then beta must be 0)    */
 } b2p_epilogue;
 
 typedef struct {
@@ -133,6 +139,20 @@ int b2p_layernorm_bwd(const float* dy, const float* x, const float* gamma, const
                       int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
                       float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
                       float* workspace, b2p_stream_t stream);
+/* As above, plus bf16 copies for the next GEMM's operand (NULL = none): y16 = bf16(y);
+ * d16 = bf16(dx_dropped) when dx_dropped != NULL, else bf16(dx). */
+int b2p_layernorm_fwd16(const float* x, const float* gamma, const float* beta, float* y, uint16_t* y16,
+                        float* mean, float* rstd, int64_t rows, int64_t cols, float eps,
+                        float drop_p, uint64_t drop_seed, b2p_stream_t stream);
+int b2p_layernorm_bwd16(const float* dy, const float* x, const float* gamma, const float* mean,
+                        const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                        int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
+                        float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
+                        uint16_t* d16, float* workspace, b2p_stream_t stream);
+
+/* fp32 -> bf16 (round to nearest even), the GEMM operand copy of a weight or activation
+ * (master copies stay fp32; replaces the implicit .to(bfloat16) of autocast) */
+int b2p_cast_bf16(const float* x, uint16_t* y, int64_t n, b2p_stream_t stream);
 
 /* Row softmax for attention scores (eager_attention_forward: softmax(QK^T*scale) + dropout).
  * S rows of length n (row stride ld). Writes P (pre-dropout) and Pd (dropped, scaled). */

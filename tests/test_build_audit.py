@@ -3,7 +3,7 @@ dynamically-indexed private arrays)."""
 import pytest
 
 
-@pytest.mark.parametrize("src", ["gemm.hip", "gru.hip", "elementwise.hip", "ctc.hip"])
+@pytest.mark.parametrize("src", ["gemm.hip", "gemm16.hip", "gru.hip", "elementwise.hip", "ctc.hip"])
 def test_no_scratch(src):
     from wav2vec2forbrain_amd.build_lib import audit_scratch
     res = audit_scratch(src)

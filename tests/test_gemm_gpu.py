@@ -175,3 +175,95 @@ def test_grouped_conv_view(mode):
         A = Fn.conv_op(x, 0, D, T, T, 1, K // 2, Ig, T * D, True, bs1=Ig)
         Fn.gemm(B * T, Og, K * Ig, A, Fn.op(wp, 0, K * Ig, True, bs1=Og * K * Ig), out, D, cbs1=Og, nz1=G)
         _close(out, ref, mode)
+
+
+# ------------------------------------------------------------------ bf16 operands (gemm16.hip)
+def _b16(t):
+    return t.to(torch.bfloat16).contiguous()
+
+
+def _close16(out, ref, tol=5e-5):
+    scale = ref.abs().max().item() + 1e-6
+    err = (out.float() - ref).abs().max().item()
+    assert err <= tol * scale, f"max err {err} vs scale {scale}"
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (130, 72, 40), (1, 8, 8), (300, 264, 96), (257, 136, 2056),
+                                   (96, 64, 8192)])
+def test_bf16_operands_layouts(M, N, K):
+    """LDS-DMA kernel: NT / NN / TN on bf16 operands vs fp64 products of the same bf16 values
+    (exact products, fp32 accumulation); tails in M, N and K, split-K for the long-K case."""
+    Fn = _fn()
+    torch.manual_seed(10)
+    Mp, Np = (M + 7) // 8 * 8, (N + 7) // 8 * 8
+    a = _b16(torch.randn(M, K, device="cuda"))
+    w = _b16(torch.randn(N, K, device="cuda"))
+    b = _b16(torch.randn(K, Np, device="cuda"))
+    at = _b16(torch.randn(K, Mp, device="cuda"))
+    with Fn.precision("bf16"):
+        out = torch.full((M, Np), float("nan"), device="cuda")
+        Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), out, Np)
+        _close16(out[:, :N], (a.double() @ w.double().t()).float())
+        out2 = torch.full((M, Np), float("nan"), device="cuda")
+        Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(b, 0, Np, False), out2, Np)
+        _close16(out2[:, :N], (a.double() @ b[:, :N].double()).float())
+        out3 = torch.full((M, Np), float("nan"), device="cuda")
+        Fn.gemm(M, N, K, Fn.op(at, 0, Mp, False), Fn.op(b, 0, Np, False), out3, Np)
+        _close16(out3[:, :N], (at[:, :M].double().t() @ b[:, :N].double()).float())
+
+
+def test_bf16_epilogue_c16_and_batching():
+    """Epilogue on the bf16 kernel (bias, GELU, pre_out, residual), bf16 copy output with and
+    without the fp32 output, batched strides and the gathered (day) B operand + bias."""
+    Fn = _fn()
+    torch.manual_seed(11)
+    M, N, K = 200, 96, 72
+    x = _b16(torch.randn(M, K, device="cuda"))
+    w = _b16(torch.randn(N, K, device="cuda") / 8)
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda")
+    ref_pre = (x.double() @ w.double().t()).float() + bias
+    with Fn.precision("bf16"):
+        out = torch.empty(M, N, device="cuda")
+        pre = torch.empty(M, N, device="cuda")
+        c16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        Fn.gemm(M, N, K, Fn.op(x, 0, K, True), Fn.op(w, 0, K, True), out, N, bias=bias, act=Fn.ACT["gelu"],
+                pre_out=pre, residual=res, C16=c16)
+        _close16(pre, ref_pre)
+        ref = F.gelu(ref_pre) + res
+        _close16(out, ref, tol=1e-4)
+        assert torch.equal(c16, out.to(torch.bfloat16))
+        only16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        Fn.gemm(M, N, K, Fn.op(x, 0, K, True), Fn.op(w, 0, K, True), None, N, bias=bias, C16=only16)
+        torch.testing.assert_close(only16.float(), ref_pre, rtol=1e-2, atol=1e-2 * ref_pre.abs().max().item())
+    # gathered per-sample B (inner n) + gathered bias: the day layer
+    B, L, C, nd = 4, 40, 32, 6
+    xs = _b16(torch.randn(B, L, C, device="cuda"))
+    W = _b16(torch.randn(nd, C, C, device="cuda"))
+    bb = torch.randn(nd, 1, C, device="cuda")
+    day = torch.tensor([5, 0, 5, 2], device="cuda")
+    o = torch.empty(B, L, C, device="cuda")
+    with Fn.precision("bf16"):
+        Fn.gemm(L, C, C, Fn.op(xs, 0, C, True, bs1=L * C), Fn.op(W, 0, C, False, bs1=C * C, gather=day), o, C,
+                cbs1=L * C, nz1=B, bias=bb, biasbs1=C, bias_gather=day)
+    ref = torch.einsum("btd,bdk->btk", xs.double(), W[day].double()).float() + bb[day]
+    _close16(o, ref)
+
+
+def test_bf16_implicit_unfold_view():
+    """Implicit unfold (conv view on A) over a bf16 source: the GRU layer-0 projection."""
+    Fn = _fn()
+    from oracle.b2p2t_oracle import unfold
+    torch.manual_seed(12)
+    B, L, C, k, s, N = 3, 72, 16, 8, 4, 40
+    T = (L - k) // s + 1
+    x = _b16(torch.randn(B, L, C, device="cuda"))
+    w = torch.randn(N, C * k, device="cuda")
+    u = unfold(x.float().cpu(), k, s).cuda()
+    wp = torch.empty(N, k * C, device="cuda")
+    Fn._lib.call("b2p_conv_weight_permute", w.data_ptr(), wp.data_ptr(), N, C, k, 0, Fn._st())
+    wp16 = _b16(wp)
+    with Fn.precision("bf16"):
+        out = torch.empty(B * T, N, device="cuda")
+        Fn.gemm(B * T, N, k * C, Fn.conv_op(x, 0, C, T, L, s, 0, C, L * C, True), Fn.op(wp16, 0, k * C, True), out, N)
+    _close16(out, (u.view(B * T, -1).double() @ w.to(torch.bfloat16).double().t()).float())

@@ -348,3 +348,60 @@ def test_conformer_elementwise_kernels():
                  rstd.data_ptr(), dev(gam), dxb.data_ptr(), dg.data_ptr(), db.data_ptr(), M, D,
                  Fn.ACT["silu"], ws.data_ptr(), Fn._st())
     assert _rel(dxb.cpu(), gx_) < 1e-4 and _rel(dg.cpu(), gg_) < 1e-4 and _rel(db.cpu(), gb_) < 1e-4
+
+
+def test_cast_and_layernorm_bf16_copies():
+    """b2p_cast_bf16 == torch RNE rounding; LayerNorm fwd/bwd bf16 copies equal the rounded fp32
+    outputs they shadow."""
+    Fn = _fn()
+    torch.manual_seed(21)
+    x = torch.randn(1003, device="cuda") * 7
+    torch.testing.assert_close(Fn.cast16(x), x.to(torch.bfloat16), rtol=0, atol=0)
+    rows, cols = 77, 768
+    xx = torch.randn(rows, cols, device="cuda")
+    g = 1 + 0.1 * torch.randn(cols, device="cuda")
+    b = 0.1 * torch.randn(cols, device="cuda")
+    y, y16, m, r = Fn._ln_fwd16(xx, g, b, 1e-5)
+    y0, m0, r0 = Fn._ln_fwd(xx, g, b, 1e-5)
+    assert torch.equal(y, y0) and torch.equal(y16, y.to(torch.bfloat16))
+    dy = torch.randn(rows, cols, device="cuda")
+    dx, dg, db, dxd, d16 = Fn._ln_bwd16(dy, xx, g, m, r, True, in_drop_p=0.1, in_seed=5)
+    dx0, dg0, db0, dxd0 = Fn._ln_bwd(dy, xx, g, m, r, True, in_drop_p=0.1, in_seed=5)
+    assert torch.equal(dx, dx0) and torch.equal(dxd, dxd0) and torch.equal(d16, dxd.to(torch.bfloat16))
+    dx, dg, db, dxd, d16 = Fn._ln_bwd16(dy, xx, g, m, r, True)
+    assert dxd is None and torch.equal(d16, dx.to(torch.bfloat16))
+
+
+def test_encoder_layer_bf16_operands_match_fp32_path():
+    """_EncoderLayer16 (bf16 operands in HBM, fused QKV) vs _EncoderLayer (fp32 operands) in
+    train mode with identical dropout seeds: same masks, bf16-level agreement of output and
+    every gradient; and the cached bf16 weights refresh after an in-place optimiser update."""
+    Fn = _fn()
+    torch.manual_seed(22)
+    B, T, D, nh, Ff = 2, 37, 64, 4, 128
+    shapes = [(D, D), (D,), (D, D), (D,), (D, D), (D,), (D, D), (D,), (D,), (D,), (Ff, D), (Ff,), (D, Ff), (D,), (D,), (D,)]
+    ps = [(torch.randn(*s) / math.sqrt(s[-1])).cuda() for s in shapes]
+    ps[8] = torch.ones(D, device="cuda"); ps[14] = torch.ones(D, device="cuda")
+    x = torch.randn(B, T, D, device="cuda")
+    cfg = (nh, 1e-5, 0.1, 0.1, 0.1, (31, 32, 33, 34))
+    dy = torch.randn(B, T, D, device="cuda")
+    res = []
+    for cls, mode in ((Fn._EncoderLayer, "fp32"), (Fn._EncoderLayer16, "bf16")):
+        with Fn.precision(mode):
+            pg = [p.clone().requires_grad_(True) for p in ps]
+            xg = x.clone().requires_grad_(True)
+            out = cls.apply(xg, cfg, *pg)
+            res.append([out] + list(torch.autograd.grad(out, [xg] + pg, dy)))
+    for i, (a, b) in enumerate(zip(res[0], res[1])):
+        if i == 5:     # k_proj bias gradient: mathematically 0 (softmax shift invariance), rounding noise
+            assert b.abs().max().item() < 3e-2 * res[0][1].abs().max().item()
+            continue
+        assert _rel(b.cpu(), a.cpu()) < 3e-2, (i, _rel(b.cpu(), a.cpu()))
+    # cache refresh: change a weight in place through a raw pointer + epoch bump
+    with Fn.precision("bf16"):
+        w = ps[10].clone()
+        w16a = Fn.weight16(w).clone()
+        Fn._lib.call("b2p_dropout", w.data_ptr(), w.data_ptr(), w.numel(), 0.5, 9, Fn._st())   # in-place write
+        assert torch.equal(Fn.weight16(w), w16a)          # torch cannot see it ...
+        Fn.bump_param_epoch([w])
+        assert torch.equal(Fn.weight16(w), w.to(torch.bfloat16))   # ... the epoch bump can

@@ -28,18 +28,20 @@ def main():
     NT, D, F, T, B, nh = 7968, 768, 3072, 249, 32, 12
     res = []
 
+    cv = (lambda t: t.to(torch.bfloat16)) if B16 else (lambda t: t)
+
     def lin(M, N, K, kind):
-        a = torch.randn(M, K, device=dev)
-        w = torch.randn(N, K, device=dev)
+        a = cv(torch.randn(M, K, device=dev))
+        w = cv(torch.randn(N, K, device=dev))
         out = torch.empty(M, N, device=dev)
         if kind == "nt":
             f = lambda: Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), out, N)
         elif kind == "nn":
-            bm = torch.randn(K, N, device=dev)
+            bm = cv(torch.randn(K, N, device=dev))
             f = lambda: Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(bm, 0, N, False), out, N)
         else:
-            at = torch.randn(K, M, device=dev)
-            bm = torch.randn(K, N, device=dev)
+            at = cv(torch.randn(K, M, device=dev))
+            bm = cv(torch.randn(K, N, device=dev))
             f = lambda: Fn.gemm(M, N, K, Fn.op(at, 0, M, False), Fn.op(bm, 0, N, False), out, N)
         ms = timeit(f)
         res.append(dict(shape=f"{kind} {M}x{N}x{K}", ms=round(ms, 4), tflops=round(2 * M * N * K / ms / 1e9, 1)))
@@ -52,12 +54,18 @@ def main():
     lin(4096, 4096, 4096, "nt")
     # GRU layer-0 implicit unfold projection
     L, C = 1024, 256
-    x = torch.randn(B, L, C, device=dev)
-    wp = torch.randn(1536, 8192, device=dev)
+    x = cv(torch.randn(B, L, C, device=dev))
+    wp = cv(torch.randn(1536, 8192, device=dev))
     gi = torch.empty(B * T, 1536, device=dev)
     A = Fn.conv_op(x, 0, C, T, L, 4, 0, C, L * C, True)
     ms = timeit(lambda: Fn.gemm(B * T, 1536, 8192, A, Fn.op(wp, 0, 8192, True), gi, 1536))
     res.append(dict(shape="unfold-proj 7968x1536x8192", ms=round(ms, 4), tflops=round(2 * B * T * 1536 * 8192 / ms / 1e9, 1)))
+    if B16:
+        for r in res:
+            r["operands"] = "bf16"
+        for r in res:
+            print(json.dumps(r))
+        return
     # pos-conv grouped
     e = torch.randn(B, T, D, device=dev)
     wq = torch.randn(D, 128 * 48, device=dev)
@@ -82,7 +90,11 @@ def main():
         print(json.dumps(r))
 
 
+B16 = False
+
 if __name__ == "__main__":
     mode = sys.argv[1] if len(sys.argv) > 1 else "bf16"
+    if mode == "b16":
+        B16, mode = True, "bf16"
     with Fn.precision(mode):
         main()

@@ -31,7 +31,7 @@ class Operand(ctypes.Structure):
         ("ptr", c_p), ("ld", c_i64), ("bs1", c_i64), ("bs2", c_i64), ("gather1", c_p),
         ("inner_is_k", c_i32), ("conv", c_i32),
         ("conv_T_out", c_i32), ("conv_T_in", c_i32), ("conv_stride", c_i32), ("conv_pad", c_i32),
-        ("conv_Cg", c_i32), ("_pad0", c_i32), ("conv_sample_stride", c_i64),
+        ("conv_Cg", c_i32), ("dtype", c_i32), ("conv_sample_stride", c_i64),
     ]
 
 
@@ -41,7 +41,7 @@ class Epilogue(ctypes.Structure):
         ("alpha", c_f32), ("beta", c_f32), ("bias", c_p), ("biasbs1", c_i64), ("bias_gather", c_p), ("pre_out", c_p),
         ("act", c_i32), ("act_bwd", c_i32), ("aux", c_p), ("ldaux", c_i64), ("abs1", c_i64),
         ("abs2", c_i64), ("drop_p", c_f32), ("_pad0", c_i32), ("drop_seed", c_u64),
-        ("residual", c_p), ("ldr", c_i64), ("rbs1", c_i64), ("rbs2", c_i64),
+        ("residual", c_p), ("ldr", c_i64), ("rbs1", c_i64), ("rbs2", c_i64), ("C16", c_p),
     ]
 
 
@@ -70,6 +70,10 @@ _SIGS = {
     "b2p_layernorm_bwd_workspace": (c_i64, [c_i64, c_i64]),
     "b2p_layernorm_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_f32, c_u64,
                                   c_p, c_f32, c_u64, c_p, c_p, c_p]),
+    "b2p_layernorm_fwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_u64, c_p]),
+    "b2p_layernorm_bwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_f32, c_u64,
+                                    c_p, c_f32, c_u64, c_p, c_p, c_p, c_p]),
+    "b2p_cast_bf16": (c_i32, [c_p, c_p, c_i64, c_p]),
     "b2p_softmax_fwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_u64, c_p]),
     "b2p_softmax_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_u64, c_p]),
     "b2p_act_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i32, c_p]),

@@ -9,6 +9,18 @@ typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) __bf16 bf16x4;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 
+// fp32 -> bf16 bits, round-to-nearest-even (plain cast: v_cvt_pk_bf16_f32, keeps NaN a NaN)
+__device__ __forceinline__ uint16_t b2p_bf16_bits(float v) {
+  return __builtin_bit_cast(uint16_t, (__bf16)v);
+}
+__device__ __forceinline__ uint2 b2p_pack_bf16x4(float4 v) {
+  return make_uint2((uint32_t)b2p_bf16_bits(v.x) | ((uint32_t)b2p_bf16_bits(v.y) << 16),
+                    (uint32_t)b2p_bf16_bits(v.z) | ((uint32_t)b2p_bf16_bits(v.w) << 16));
+}
+__device__ __forceinline__ float b2p_bf16_to_f32(uint16_t b) {
+  return __builtin_bit_cast(float, (uint32_t)b << 16);
+}
+
 // ---------------------------------------------------------------------------
 // error reporting: every C-ABI entry returns 0 on success, nonzero on failure
 // and leaves a message retrievable through b2p_last_error().

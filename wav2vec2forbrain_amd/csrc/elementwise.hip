@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
                                                 const float* __restrict__ beta, float* __restrict__ y,
                                                 float* __restrict__ mean, float* __restrict__ rstd,
                                                 int64_t rows, int cols, float eps, uint32_t thr, float dscale,
-                                                uint64_t seed, float drop_p) {
+                                                uint64_t seed, float drop_p, uint16_t* __restrict__ y16) {
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -125,6 +125,7 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
         o.w = b2p_keep(seed, base + 3, thr) ? o.w * dscale : 0.f;
       }
       yr[c] = o;
+      if (y16) reinterpret_cast<uint2*>(y16 + row * cols)[c] = b2p_pack_bf16x4(o);
     }
   }
 }
@@ -136,7 +137,7 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
                                                 const float* __restrict__ dx_accum, float* __restrict__ part,
                                                 int64_t rows, int cols, uint32_t thr, float dscale, uint64_t seed,
                                                 float drop_p, float* __restrict__ dxd, uint32_t thr2, float dscale2,
-                                                uint64_t seed2) {
+                                                uint64_t seed2, uint16_t* __restrict__ d16) {
   __shared__ float red[4][3][LN_MAXV * 256];   // cols <= 1024
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = cols >> 2;
@@ -190,6 +191,7 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
         o.w = rs * (gg[i].w - s1 - xh[i].w * s2);
         if (acc) { const float4 a = acc[c]; o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w; }
         dxr[c] = o;
+        if (d16 && !dxd) reinterpret_cast<uint2*>(d16 + row * cols)[c] = b2p_pack_bf16x4(o);
         if (dxd) {   // gradient of the dropout that produced this LN's input (residual branch)
           const uint64_t base = (uint64_t)row * cols + 4 * c;
           float4 q;
@@ -198,6 +200,7 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
           q.z = b2p_keep(seed2, base + 2, thr2) ? o.z * dscale2 : 0.f;
           q.w = b2p_keep(seed2, base + 3, thr2) ? o.w * dscale2 : 0.f;
           reinterpret_cast<float4*>(dxd + row * cols)[c] = q;
+          if (d16) reinterpret_cast<uint2*>(d16 + row * cols)[c] = b2p_pack_bf16x4(q);
           dd[i].x += q.x; dd[i].y += q.y; dd[i].z += q.z; dd[i].w += q.w;
         }
       }
@@ -456,17 +459,24 @@ extern "C" int b2p_dropout(const float* x, float* y, int64_t n, float p, uint64_
   return 0;
 }
 
-extern "C" int b2p_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean,
-                                 float* rstd, int64_t rows, int64_t cols, float eps, float drop_p,
-                                 uint64_t drop_seed, b2p_stream_t stream) {
+extern "C" int b2p_layernorm_fwd16(const float* x, const float* gamma, const float* beta, float* y, uint16_t* y16,
+                                   float* mean, float* rstd, int64_t rows, int64_t cols, float eps, float drop_p,
+                                   uint64_t drop_seed, b2p_stream_t stream) {
   B2P_CHECK_ARG(x && gamma && beta && y && mean && rstd, "layernorm_fwd: NULL pointer");
   B2P_CHECK_ARG(cols % 4 == 0 && cols <= 64 * 4 * LN_MAXV, "layernorm_fwd: cols must be %%4 and <= 1024");
+  B2P_CHECK_ARG(((uintptr_t)y16 & 7u) == 0, "layernorm_fwd: y16 must be 8-byte aligned");
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(ln_fwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, y,
                      mean, rstd, rows, (int)cols, eps, b2p_dropout_threshold(drop_p),
-                     drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, drop_seed, drop_p);
+                     drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, drop_seed, drop_p, y16);
   B2P_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int b2p_layernorm_fwd(const float* x, const float* gamma, const float* beta, float* y, float* mean,
+                                 float* rstd, int64_t rows, int64_t cols, float eps, float drop_p,
+                                 uint64_t drop_seed, b2p_stream_t stream) {
+  return b2p_layernorm_fwd16(x, gamma, beta, y, nullptr, mean, rstd, rows, cols, eps, drop_p, drop_seed, stream);
 }
 
 extern "C" int64_t b2p_layernorm_bwd_workspace(int64_t rows, int64_t cols) {
@@ -474,26 +484,56 @@ extern "C" int64_t b2p_layernorm_bwd_workspace(int64_t rows, int64_t cols) {
   return nblk * 3 * cols + 3 * cols + ((nblk + kColsumRows - 1) / kColsumRows) * 3 * cols;
 }
 
-extern "C" int b2p_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
-                                 const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
-                                 int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
-                                 float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
-                                 float* workspace, b2p_stream_t stream) {
+extern "C" int b2p_layernorm_bwd16(const float* dy, const float* x, const float* gamma, const float* mean,
+                                   const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                                   int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
+                                   float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
+                                   uint16_t* d16, float* workspace, b2p_stream_t stream) {
   B2P_CHECK_ARG(dy && x && gamma && mean && rstd && dx && workspace, "layernorm_bwd: NULL pointer");
   B2P_CHECK_ARG(cols % 4 == 0 && cols <= 64 * 4 * LN_MAXV, "layernorm_bwd: cols must be %%4 and <= 1024");
+  B2P_CHECK_ARG(((uintptr_t)d16 & 7u) == 0, "layernorm_bwd: d16 must be 8-byte aligned");
   if (rows <= 0) return 0;
   const int nblk = (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(ln_bwd_k, dim3(nblk), dim3(256), 0, st, dy, x, gamma, mean, rstd, dx, dx_accum, workspace,
                      rows, (int)cols, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
                      drop_seed, drop_p, dx_dropped, b2p_dropout_threshold(in_drop_p),
-                     in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed);
+                     in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed, d16);
   // partials [nblk][3][cols] -> [3][cols] with the parallel two-phase column sum, then scatter
   float* red3 = workspace + (int64_t)nblk * 3 * cols;
   float* part2 = red3 + 3 * cols;
   if (colsum_impl(workspace, nullptr, 1, nblk, 3 * cols, 3 * cols, 0, 0, red3, 0, part2, st)) return 1;
   hipLaunchKernelGGL(ln_bwd_scatter, dim3(nblocks(3 * cols)), dim3(256), 0, st, red3, (int)cols, dgamma, dbeta,
                      dx_dropped ? dbias_in : nullptr);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_layernorm_bwd(const float* dy, const float* x, const float* gamma, const float* mean,
+                                 const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                                 int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
+                                 float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
+                                 float* workspace, b2p_stream_t stream) {
+  return b2p_layernorm_bwd16(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, rows, cols, dx_accum, drop_p, drop_seed,
+                             dx_dropped, in_drop_p, in_drop_seed, dbias_in, nullptr, workspace, stream);
+}
+
+// ------------------------------------------------------------------ fp32 -> bf16 cast
+__global__ void cast_bf16_k(const float* __restrict__ x, uint16_t* __restrict__ y, int64_t n4, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n4) {
+    reinterpret_cast<uint2*>(y)[i] = b2p_pack_bf16x4(reinterpret_cast<const float4*>(x)[i]);
+  } else if (i == n4) {
+    for (int64_t j = 4 * n4; j < n; ++j) y[j] = b2p_bf16_bits(x[j]);
+  }
+}
+
+extern "C" int b2p_cast_bf16(const float* x, uint16_t* y, int64_t n, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && y, "cast_bf16: NULL pointer");
+  B2P_CHECK_ARG(((uintptr_t)x & 15u) == 0 && ((uintptr_t)y & 7u) == 0, "cast_bf16: misaligned pointers");
+  if (n <= 0) return 0;
+  const int64_t n4 = n / 4;
+  hipLaunchKernelGGL(cast_bf16_k, dim3(nblocks(n4 + 1)), dim3(256), 0, (hipStream_t)stream, x, y, n4, n);
   B2P_CHECK_LAUNCH();
   return 0;
 }

@@ -4,15 +4,16 @@
 // Operands live in HBM as fp32 (activations, master weights, gradients) and are converted
 // while staging into LDS: bf16 for v_mfma_f32_16x16x32_bf16 (fp32 accumulate), or kept fp32
 // for v_mfma_f32_16x16x4_f32 (exact-fp32 parity mode). 256 threads = 4 waves (2 x 2), each
-// wave owns a (BM/2) x (BN/2) sub-tile of 16x16 MFMA tiles; BK = 32; two LDS buffers with
+// wave owns a (BM/2) x (BN/2) sub-tile of 16x16 MFMA tiles; K tile KB = 32 or 64; two LDS buffers with
 // register staging (global loads for tile k+1 are in flight while tile k is computed).
 #include "common.h"
 #include "../../include/b2p_hip.h"
 #include "timing.h"
+#include "gemm_epi.h"
+#include <stdlib.h>
 
 namespace {
 
-constexpr int BK = 32;
 constexpr int NT = 256;
 
 // ------------------------------------------------------------------ operand views
@@ -30,18 +31,18 @@ __device__ __forceinline__ int64_t batch_off(const b2p_operand& o, int z1, int z
 }
 
 // Precision traits -----------------------------------------------------------------
-template <int PREC> struct Prec;
-template <> struct Prec<0> {   // bf16 MFMA
+template <int PREC, int KB> struct Prec;
+template <int KB> struct Prec<0, KB> {   // bf16 MFMA
   typedef __bf16 T;
-  static constexpr int LDS_STRIDE = BK + 8;   // 80 B rows: 16-B aligned ds_read_b128
+  static constexpr int LDS_STRIDE = KB + 8;   // rows 16-B aligned for ds_read_b128; odd multiple of 16 B
 };
-template <> struct Prec<1> {   // fp32 MFMA
+template <int KB> struct Prec<1, KB> {   // fp32 MFMA
   typedef float T;
-  static constexpr int LDS_STRIDE = BK + 1;
+  static constexpr int LDS_STRIDE = KB + 1;
 };
 
-template <int PREC>
-__device__ __forceinline__ void st4(typename Prec<PREC>::T* dst, float a, float b, float c, float d) {
+template <int PREC, int KB>
+__device__ __forceinline__ void st4(typename Prec<PREC, KB>::T* dst, float a, float b, float c, float d) {
   if constexpr (PREC == 0) {
     bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
     *reinterpret_cast<bf16x4*>(dst) = v;
@@ -51,29 +52,36 @@ __device__ __forceinline__ void st4(typename Prec<PREC>::T* dst, float a, float 
 }
 
 // ------------------------------------------------------------------ tile loader
-// Loads an R x BK (rows = M or N index, cols = k) tile of an operand into registers and
-// writes it K-contiguous into LDS: lds[row][k].
-template <int R, bool INNER_K, bool CONV, int PREC>
+// Loads an R x KB (rows = M or N index, cols = k) tile of an operand into registers and writes it
+// K-contiguous into LDS: lds[row][k].
+//  INNER_K: the operand's contiguous dim is k: CPR = KB/4 float4 chunks per row, RPP = NT/CPR rows
+//           per pass, NV = R/RPP float4 per thread.
+//  !INNER_K: contiguous dim is m/n: 4(k) x 4(mn) register blocks transposed on the way to LDS;
+//           NC = R/4 mn-chunks x KG = KB/4 k-groups = NBLK blocks per thread (0.5 -> half active).
+template <int R, int KB, bool INNER_K, bool CONV, int PREC>
 struct Loader {
-  static constexpr int NV = INNER_K ? R / 32 : 4;  // float4 registers per thread
+  static constexpr int CPR = KB / 4;
+  static constexpr int RPP = NT / CPR;
+  static constexpr int NC = R / 4, KG = KB / 4;
+  static constexpr int NBLK = (NC * KG) >= NT ? (NC * KG) / NT : 1;
+  static constexpr int NV = INNER_K ? R / RPP : 4 * NBLK;
   float4 v[NV];
   bool active;
-  // INNER_K: per-row precomputed frame / row offsets, one k-tracker
-  int64_t rowoff[INNER_K ? R / 32 : 1];
-  int frame0[INNER_K ? R / 32 : 1];
-  bool rowok[INNER_K ? R / 32 : 1];
-  int tap, ch;          // conv tracker for inner index (INNER_K: k; !INNER_K: mn fixed)
-  // !INNER_K: per-k-row trackers
-  int tb[4], tt[4];
-  int64_t mnoff;        // !INNER_K: fixed inner offset (mn) part
-  int mnvalid;          // number of valid inner elements at this thread's chunk
+  int64_t rowoff[INNER_K ? NV : 1];
+  int frame0[INNER_K ? NV : 1];
+  bool rowok[INNER_K ? NV : 1];
+  int tap, ch;                         // INNER_K conv: k tracker; !INNER_K conv: fixed (mn) tap/ch
+  int tb[INNER_K ? 1 : NBLK][4], tt[INNER_K ? 1 : NBLK][4];
+  int64_t mnoff[INNER_K ? 1 : NBLK];
+  int mnvalid[INNER_K ? 1 : NBLK];
+  int gk[INNER_K ? 1 : NBLK];          // k-group of each block
 
   __device__ __forceinline__ void init(const OpState& s, int tid, int mn0, int MNdim, int kstart) {
     if constexpr (INNER_K) {
       active = true;
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        const int row = mn0 + (tid >> 3) + 32 * i;
+        const int row = mn0 + tid / CPR + RPP * i;
         rowok[i] = row < MNdim;
         if constexpr (CONV) {
           const int rr = rowok[i] ? row : 0;
@@ -85,34 +93,35 @@ struct Loader {
           frame0[i] = 0;
         }
       }
-      const int kk = kstart + (tid & 7) * 4;
+      const int kk = kstart + (tid % CPR) * 4;
       if constexpr (CONV) { tap = kk / s.Cg; ch = kk - tap * s.Cg; } else { tap = 0; ch = kk; }
     } else {
-      // R/4 mn-chunks x 8 k-groups of 4
-      const int nchunk = R / 4;
-      const int c = tid % nchunk, g = tid / nchunk;
-      active = g < 8;
-      const int mn = mn0 + 4 * c;
-      mnvalid = MNdim - mn;
-      if constexpr (CONV) {
-        const int mm = mnvalid > 0 ? mn : 0;
-        tap = mm / s.Cg; ch = mm - tap * s.Cg;
-        mnoff = (int64_t)(tap - s.pad) * s.ld + ch;
+      active = (NC * KG >= NT) || tid < NC * KG;
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = kstart + 4 * g + j;   // first k-tile of this block's K range
-          tb[j] = k / s.T_out; tt[j] = k - tb[j] * s.T_out;
+      for (int q = 0; q < NBLK; ++q) {
+        const int bidx = tid + NT * q;
+        const int c = bidx % NC, g = bidx / NC;
+        gk[q] = g;
+        const int mn = mn0 + 4 * c;
+        mnvalid[q] = MNdim - mn;
+        if constexpr (CONV) {
+          const int mm = mnvalid[q] > 0 ? mn : 0;
+          const int tp = mm / s.Cg, cc = mm - tp * s.Cg;
+          mnoff[q] = (int64_t)(tp - s.pad) * s.ld + cc;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int k = kstart + 4 * g + j;
+            tb[q][j] = k / s.T_out; tt[q][j] = k - tb[q][j] * s.T_out;
+          }
+          tbtap[q] = tp;   // frame = tt*stride + tap - pad (validity), address via mnoff
+        } else {
+          mnoff[q] = mn;
         }
-      } else {
-        mnoff = mn;
       }
     }
   }
+  int tbtap[INNER_K ? 1 : NBLK];
 
-  // Branch-free loads: every lane issues one unconditional 16-B load (from a clamped, always
-  // in-bounds address when the element is outside the operand) and zeroes invalid elements with
-  // selects, so the global loads of a K-step stay in flight together (a per-load branch makes
-  // hipcc wait vmcnt(0) per load). In-bounds guarantee: ld % 4 == 0 => ld >= roundup4(dim).
   __device__ __forceinline__ static float4 sel4(float4 x, bool ok, int nvalid) {
     x.x = ok ? x.x : 0.f;
     x.y = (ok && nvalid > 1) ? x.y : 0.f;
@@ -121,9 +130,13 @@ struct Loader {
     return x;
   }
 
+  // Branch-free loads: every lane issues one unconditional 16-B load (from a clamped, always
+  // in-bounds address when the element is outside the operand) and zeroes invalid elements with
+  // selects, so the global loads of a K-step stay in flight together (a per-load branch makes
+  // hipcc wait vmcnt(0) per load). In-bounds guarantee: ld % 4 == 0 => ld >= roundup4(dim).
   __device__ __forceinline__ void load(const OpState& s, int tid, int k0, int Kdim) {
     if constexpr (INNER_K) {
-      const int kk = k0 + (tid & 7) * 4;
+      const int kk = k0 + (tid % CPR) * 4;
       const int kvalid = Kdim - kk;
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
@@ -139,56 +152,62 @@ struct Loader {
         v[i] = sel4(*reinterpret_cast<const float4*>(p), ok, kvalid);
       }
       if constexpr (CONV) {
-        ch += BK;
+        ch += KB;
         while (ch >= s.Cg) { ch -= s.Cg; ++tap; }
       }
     } else {
       if (!active) return;
-      const int nchunk = R / 4;
-      const int g = tid / nchunk;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int k = k0 + 4 * g + j;
-        bool ok = k < Kdim && mnvalid > 0;
-        const float* p;
-        if constexpr (CONV) {
-          const int f = tt[j] * s.stride + tap - s.pad;
-          ok = ok && f >= 0 && f < s.T_in;
-          p = ok ? s.base + (int64_t)tb[j] * s.sample_stride + (int64_t)(tt[j] * s.stride) * s.ld + mnoff : s.base;
-          tt[j] += BK;
-          while (tt[j] >= s.T_out) { tt[j] -= s.T_out; ++tb[j]; }
-        } else {
-          p = ok ? s.base + (int64_t)k * s.ld + mnoff : s.base;
+      for (int q = 0; q < NBLK; ++q) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = k0 + 4 * gk[q] + j;
+          bool ok = k < Kdim && mnvalid[q] > 0;
+          const float* p;
+          if constexpr (CONV) {
+            const int f = tt[q][j] * s.stride + tbtap[q] - s.pad;
+            ok = ok && f >= 0 && f < s.T_in;
+            p = ok ? s.base + (int64_t)tb[q][j] * s.sample_stride + (int64_t)(tt[q][j] * s.stride) * s.ld + mnoff[q]
+                   : s.base;
+            tt[q][j] += KB;
+            while (tt[q][j] >= s.T_out) { tt[q][j] -= s.T_out; ++tb[q][j]; }
+          } else {
+            p = ok ? s.base + (int64_t)k * s.ld + mnoff[q] : s.base;
+          }
+          v[4 * q + j] = sel4(*reinterpret_cast<const float4*>(p), ok, mnvalid[q]);
         }
-        v[j] = sel4(*reinterpret_cast<const float4*>(p), ok, mnvalid);
       }
     }
   }
 
-  __device__ __forceinline__ void store(typename Prec<PREC>::T* lds, int tid) {
-    constexpr int LS = Prec<PREC>::LDS_STRIDE;
+  __device__ __forceinline__ void store(typename Prec<PREC, KB>::T* lds, int tid) {
+    constexpr int LS = Prec<PREC, KB>::LDS_STRIDE;
     if constexpr (INNER_K) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
-        const int row = (tid >> 3) + 32 * i;
-        st4<PREC>(lds + row * LS + (tid & 7) * 4, v[i].x, v[i].y, v[i].z, v[i].w);
+        const int row = tid / CPR + RPP * i;
+        st4<PREC, KB>(lds + row * LS + (tid % CPR) * 4, v[i].x, v[i].y, v[i].z, v[i].w);
       }
     } else {
       if (!active) return;
-      const int nchunk = R / 4;
-      const int c = tid % nchunk, g = tid / nchunk;
-      typename Prec<PREC>::T* d = lds + (4 * c) * LS + 4 * g;
-      st4<PREC>(d + 0 * LS, v[0].x, v[1].x, v[2].x, v[3].x);
-      st4<PREC>(d + 1 * LS, v[0].y, v[1].y, v[2].y, v[3].y);
-      st4<PREC>(d + 2 * LS, v[0].z, v[1].z, v[2].z, v[3].z);
-      st4<PREC>(d + 3 * LS, v[0].w, v[1].w, v[2].w, v[3].w);
+#pragma unroll
+      for (int q = 0; q < NBLK; ++q) {
+        const int bidx = tid + NT * q;
+        const int c = bidx % NC, g = bidx / NC;
+        typename Prec<PREC, KB>::T* d = lds + (4 * c) * LS + 4 * g;
+        const float4* w = v + 4 * q;
+        st4<PREC, KB>(d + 0 * LS, w[0].x, w[1].x, w[2].x, w[3].x);
+        st4<PREC, KB>(d + 1 * LS, w[0].y, w[1].y, w[2].y, w[3].y);
+        st4<PREC, KB>(d + 2 * LS, w[0].z, w[1].z, w[2].z, w[3].z);
+        st4<PREC, KB>(d + 3 * LS, w[0].w, w[1].w, w[2].w, w[3].w);
+      }
     }
   }
 };
 
 __device__ __forceinline__ OpState make_state(const b2p_operand& o, int z1, int z2) {
   OpState s;
-  s.base = o.ptr + batch_off(o, z1, z2);
+  s.base = static_cast<const float*>(o.ptr) + batch_off(o, z1, z2);
   s.ld = o.ld;
   s.T_out = o.conv_T_out > 0 ? o.conv_T_out : 1;
   s.T_in = o.conv_T_in;
@@ -199,54 +218,11 @@ __device__ __forceinline__ OpState make_state(const b2p_operand& o, int z1, int 
   return s;
 }
 
-// ------------------------------------------------------------------ epilogue
-__device__ __forceinline__ float apply_act(float v, int act) {
-  if (act == B2P_ACT_GELU) return b2p_gelu(v);
-  if (act == B2P_ACT_SOFTSIGN) return v / (1.0f + fabsf(v));
-  if (act == B2P_ACT_SILU) return b2p_silu(v);
-  return v;
-}
-__device__ __forceinline__ float act_grad(float x, int act) {
-  if (act == B2P_ACT_GELU) return b2p_gelu_grad(x);
-  if (act == B2P_ACT_SOFTSIGN) { const float d = 1.0f + fabsf(x); return 1.0f / (d * d); }
-  if (act == B2P_ACT_SILU) return b2p_silu_grad(x);
-  return 1.0f;
-}
-
-struct EpiArgs {
-  b2p_epilogue e;
-  int64_t M, N;
-  uint32_t drop_thr;
-  float drop_scale;
-};
-
-__device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, int z2, int m, int n,
-                                               float acc) {
-  if (m >= a.M || n >= a.N) return;
-  const b2p_epilogue& e = a.e;
-  const int64_t coff = (int64_t)z1 * e.cbs1 + (int64_t)z2 * e.cbs2 + (int64_t)m * e.ldc + n;
-  float v = e.alpha * acc;
-  if (e.beta != 0.0f) v += e.beta * e.C[coff];
-  if (e.bias) v += e.bias[(e.bias_gather ? e.bias_gather[z1] : (int64_t)z1) * e.biasbs1 + n];
-  if (e.pre_out) e.pre_out[coff] = v;
-  v = apply_act(v, e.act);
-  if (e.drop_p > 0.0f) {
-    const uint64_t idx = ((uint64_t)z * (uint64_t)a.M + (uint64_t)m) * (uint64_t)a.N + (uint64_t)n;
-    v = b2p_keep(e.drop_seed, idx, a.drop_thr) ? v * a.drop_scale : 0.0f;
-  }
-  if (e.act_bwd != B2P_ACT_NONE) {
-    const float x = e.aux[(int64_t)z1 * e.abs1 + (int64_t)z2 * e.abs2 + (int64_t)m * e.ldaux + n];
-    v *= act_grad(x, e.act_bwd);
-  }
-  if (e.residual) v += e.residual[(int64_t)z1 * e.rbs1 + (int64_t)z2 * e.rbs2 + (int64_t)m * e.ldr + n];
-  e.C[coff] = v;
-}
-
 // ------------------------------------------------------------------ kernel
-template <int BM, int BN, bool AK, bool BKin, bool ACONV, bool BCONV, int PREC>
+template <int BM, int BN, int KB, bool AK, bool BKin, bool ACONV, bool BCONV, int PREC>
 __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const EpiArgs ea) {
-  typedef typename Prec<PREC>::T T;
-  constexpr int LS = Prec<PREC>::LDS_STRIDE;
+  typedef typename Prec<PREC, KB>::T T;
+  constexpr int LS = Prec<PREC, KB>::LDS_STRIDE;
   constexpr int WM = BM / 2, WN = BN / 2;     // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;   // 16x16 MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) T smem[2 * (BM + BN) * LS];
@@ -260,14 +236,14 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
   const int z1 = z / d.nz2, z2 = z - z1 * d.nz2;
   const int m0 = blockIdx.y * BM, n0 = blockIdx.x * BN;
   const int M = (int)d.M, N = (int)d.N;
-  const int kchunk = ks > 1 ? (int)d.kchunk : (int)d.K;   // multiple of BK
+  const int kchunk = ks > 1 ? (int)d.kchunk : (int)d.K;   // multiple of KB
   const int kbeg = ksl * kchunk;
   const int K = ((int)d.K < kbeg + kchunk) ? (int)d.K : kbeg + kchunk;   // exclusive end
 
   OpState sa = make_state(d.A, z1, z2);
   OpState sb = make_state(d.B, z1, z2);
-  Loader<BM, AK, ACONV, PREC> la;
-  Loader<BN, BKin, BCONV, PREC> lb;
+  Loader<BM, KB, AK, ACONV, PREC> la;
+  Loader<BN, KB, BKin, BCONV, PREC> lb;
   la.init(sa, tid, m0, M, kbeg);
   lb.init(sb, tid, n0, N, kbeg);
 
@@ -281,7 +257,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
 #define AS_(b) (smem + (b) * (BM + BN) * LS)
 #define BS_(b) (smem + (b) * (BM + BN) * LS + BM * LS)
 
-  const int nk = K > kbeg ? (K - kbeg + BK - 1) / BK : 0;
+  const int nk = K > kbeg ? (K - kbeg + KB - 1) / KB : 0;
   la.load(sa, tid, kbeg, K);
   lb.load(sb, tid, kbeg, K);
   la.store(AS_(0), tid);
@@ -292,27 +268,30 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
     const int cur = kt & 1;
     const bool more = kt + 1 < nk;
     if (more) {
-      la.load(sa, tid, kbeg + (kt + 1) * BK, K);
-      lb.load(sb, tid, kbeg + (kt + 1) * BK, K);
+      la.load(sa, tid, kbeg + (kt + 1) * KB, K);
+      lb.load(sb, tid, kbeg + (kt + 1) * KB, K);
     }
     const T* A_ = AS_(cur);
     const T* B_ = BS_(cur);
     if constexpr (PREC == 0) {
-      bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(A_ + (wm * WM + i * 16 + (lane & 15)) * LS + 8 * (lane >> 4));
+      for (int kk = 0; kk < KB / 32; ++kk) {
+        bf16x8 af[TM], bfr[TN];
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        bfr[j] = *reinterpret_cast<const bf16x8*>(B_ + (wn * WN + j * 16 + (lane & 15)) * LS + 8 * (lane >> 4));
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const bf16x8*>(A_ + (wm * WM + i * 16 + (lane & 15)) * LS + 32 * kk + 8 * (lane >> 4));
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          bfr[j] = *reinterpret_cast<const bf16x8*>(B_ + (wn * WN + j * 16 + (lane & 15)) * LS + 32 * kk + 8 * (lane >> 4));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
-      for (int ks = 0; ks < BK / 4; ++ks) {
+      for (int ks = 0; ks < KB / 4; ++ks) {
         float af[TM], bfr[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i) af[i] = A_[(wm * WM + i * 16 + (lane & 15)) * LS + 4 * ks + (lane >> 4)];
@@ -336,22 +315,22 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
   // branch is hoisted out of the unrolled loops so acc[][] keeps constant indices (registers).
   if (ks > 1) {
     float* slab = d.workspace + ((int64_t)z * ks + ksl) * (int64_t)M * N;
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int i = 0; i < TM; ++i)
-#pragma unroll
+#pragma clang loop unroll(full)
       for (int j = 0; j < TN; ++j)
-#pragma unroll
+#pragma clang loop unroll(full)
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
           const int n = n0 + wn * WN + j * 16 + (lane & 15);
           if (m < M && n < N) slab[(int64_t)m * N + n] = acc[i][j][r];
         }
   } else {
-#pragma unroll
+#pragma clang loop unroll(full)
     for (int i = 0; i < TM; ++i)
-#pragma unroll
+#pragma clang loop unroll(full)
       for (int j = 0; j < TN; ++j)
-#pragma unroll
+#pragma clang loop unroll(full)
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
           const int n = n0 + wn * WN + j * 16 + (lane & 15);
@@ -362,14 +341,27 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
 #undef BS_
 }
 
+// K-tile selection: B2P_GEMM_KB=32|64 (default 64 for bf16; fp32 parity mode keeps 32 so its
+// LDS footprint stays at 2 x (BM+BN) x 33 floats).
+int kb_choice() {
+  static int kb = [] {
+    const char* e = getenv("B2P_GEMM_KB");
+    const int v = e ? atoi(e) : 64;
+    return v == 32 ? 32 : 64;
+  }();
+  return kb;
+}
+
 template <int BM, int BN, bool AK, bool BKin, bool ACONV, bool BCONV>
 int launch_prec(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st) {
   const int ks = d.ksplit > 1 ? d.ksplit : 1;
   dim3 grid((unsigned)((d.N + BN - 1) / BN), (unsigned)((d.M + BM - 1) / BM), (unsigned)(d.nz1 * d.nz2 * ks));
   if (d.precision == 1)
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKin, ACONV, BCONV, 1>), grid, dim3(NT), 0, st, d, ea);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKin, ACONV, BCONV, 1>), grid, dim3(NT), 0, st, d, ea);
+  else if (kb_choice() == 64 && (ks == 1 || d.kchunk % 64 == 0))
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 64, AK, BKin, ACONV, BCONV, 0>), grid, dim3(NT), 0, st, d, ea);
   else
-    hipLaunchKernelGGL((gemm_kernel<BM, BN, AK, BKin, ACONV, BCONV, 0>), grid, dim3(NT), 0, st, d, ea);
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKin, ACONV, BCONV, 0>), grid, dim3(NT), 0, st, d, ea);
   return 0;
 }
 
@@ -380,34 +372,19 @@ int launch_tiles(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st) {
   return launch_prec<128, 128, AK, BKin, ACONV, BCONV>(d, ea, st);
 }
 
-// C[z](m,n) = alpha * sum_s slab[z][s](m,n) + beta * C_old ; deterministic slice order
-__global__ void splitk_reduce(const float* __restrict__ ws, int ks, int64_t M, int64_t N, int nz2,
-                              b2p_epilogue e, int64_t total) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= total) return;
-  const int64_t MN = M * N;
-  const int64_t z = i / MN, r = i - z * MN;
-  const int64_t m = r / N, n = r - m * N;
-  const float* p = ws + z * ks * MN + r;
-  float s = 0.f;
-  for (int q = 0; q < ks; ++q) s += p[(int64_t)q * MN];
-  const int64_t z1 = z / nz2, z2 = z - z1 * nz2;
-  float* c = e.C + z1 * e.cbs1 + z2 * e.cbs2 + m * e.ldc + n;
-  float v = e.alpha * s;
-  if (e.beta != 0.f) v += e.beta * *c;
-  *c = v;
-}
-
 bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 
 int check_operand(const b2p_operand& o, const char* name) {
   B2P_CHECK_ARG(o.ptr != nullptr, "gemm: operand %s is NULL", name);
   B2P_CHECK_ARG(aligned16(o.ptr), "gemm: operand %s not 16-byte aligned", name);
-  B2P_CHECK_ARG(o.ld % 4 == 0 && o.bs1 % 4 == 0 && o.bs2 % 4 == 0,
-                "gemm: operand %s strides must be multiples of 4 (ld=%lld)", name, (long long)o.ld);
+  B2P_CHECK_ARG(o.dtype == 0 || o.dtype == 1, "gemm: operand %s dtype must be 0 (fp32) or 1 (bf16)", name);
+  const int64_t v = o.dtype == 1 ? 8 : 4;   // elements per 16-byte vector
+  B2P_CHECK_ARG(o.ld % v == 0 && o.bs1 % v == 0 && o.bs2 % v == 0,
+                "gemm: operand %s strides must be multiples of %lld (ld=%lld)", name, (long long)v, (long long)o.ld);
   if (o.conv) {
-    B2P_CHECK_ARG(o.conv_Cg > 0 && o.conv_Cg % 4 == 0, "gemm: operand %s conv_Cg must be a multiple of 4", name);
-    B2P_CHECK_ARG(o.conv_sample_stride % 4 == 0, "gemm: operand %s conv sample stride %% 4", name);
+    B2P_CHECK_ARG(o.conv_Cg > 0 && o.conv_Cg % v == 0, "gemm: operand %s conv_Cg must be a multiple of %lld", name,
+                  (long long)v);
+    B2P_CHECK_ARG(o.conv_sample_stride % v == 0, "gemm: operand %s conv sample stride %% %lld", name, (long long)v);
     B2P_CHECK_ARG(o.conv_T_out > 0 && o.conv_T_in > 0 && o.conv_stride > 0, "gemm: operand %s bad conv geometry", name);
   }
   return 0;
@@ -423,32 +400,40 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   B2P_CHECK_ARG(d.nz1 >= 1 && d.nz2 >= 1, "gemm: batch dims must be >= 1");
   B2P_CHECK_ARG(d.precision == 0 || d.precision == 1, "gemm: precision must be 0 or 1");
   if (d.M == 0 || d.N == 0) return 0;
-  B2P_CHECK_ARG(d.ep.C != nullptr, "gemm: C is NULL");
+  B2P_CHECK_ARG(d.ep.C != nullptr || d.ep.C16 != nullptr, "gemm: C and C16 are NULL");
+  B2P_CHECK_ARG(d.ep.C != nullptr || d.ep.beta == 0.f, "gemm: beta != 0 needs C");
   if (check_operand(d.A, "A") || check_operand(d.B, "B")) return 1;
+  B2P_CHECK_ARG(d.A.dtype == d.B.dtype, "gemm: operands must share a dtype");
+  const bool bf16_ops = d.A.dtype == 1;
+  if (bf16_ops) {
+    B2P_CHECK_ARG(d.precision == 0, "gemm: bf16 operands need precision 0");
+    B2P_CHECK_ARG(!(d.A.inner_is_k || d.B.inner_is_k) || d.K % 8 == 0,
+                  "gemm: bf16 k-contiguous operand needs K %% 8 == 0 (K=%lld)", (long long)d.K);
+    B2P_CHECK_ARG(!d.B.conv, "gemm: bf16 path supports a conv view on A only");
+    B2P_CHECK_ARG(!d.A.conv || d.A.inner_is_k, "gemm: bf16 conv view needs A inner=k");
+  }
   B2P_CHECK_ARG(!(d.A.conv && d.B.conv), "gemm: at most one implicit-conv operand");
   if (d.ep.act_bwd != B2P_ACT_NONE) B2P_CHECK_ARG(d.ep.aux != nullptr, "gemm: act_bwd needs aux");
   B2P_CHECK_ARG(d.ep.drop_p >= 0.f && d.ep.drop_p < 1.f, "gemm: dropout p must be in [0,1)");
   if (d.ksplit > 1) {
     B2P_CHECK_ARG(d.workspace != nullptr, "gemm: split-K needs a workspace");
-    B2P_CHECK_ARG(d.kchunk > 0 && d.kchunk % 32 == 0 && (int64_t)d.kchunk * d.ksplit >= d.K,
-                  "gemm: kchunk must be a multiple of 32 covering K");
+    B2P_CHECK_ARG(d.kchunk > 0 && d.kchunk % (bf16_ops ? 64 : 32) == 0 && (int64_t)d.kchunk * d.ksplit >= d.K,
+                  "gemm: kchunk must be a multiple of %d covering K", bf16_ops ? 64 : 32);
     B2P_CHECK_ARG(d.workspace_floats >= (int64_t)d.ksplit * d.nz1 * d.nz2 * d.M * d.N, "gemm: split-K workspace too small");
     B2P_CHECK_ARG(!d.ep.bias && !d.ep.pre_out && d.ep.act == 0 && d.ep.act_bwd == 0 && d.ep.drop_p == 0.f &&
                   !d.ep.residual, "gemm: split-K supports alpha/beta epilogues only");
   }
 
-  EpiArgs ea;
-  ea.e = d.ep;
-  ea.M = d.M;
-  ea.N = d.N;
-  ea.drop_thr = b2p_dropout_threshold(d.ep.drop_p);
-  ea.drop_scale = d.ep.drop_p > 0.f ? 1.0f / (1.0f - d.ep.drop_p) : 1.0f;
+  const EpiArgs ea = make_epi_args(d);
 
   hipStream_t st = (hipStream_t)stream;
   b2p_timing_begin(d.timing_family, st);
   const bool AK = d.A.inner_is_k != 0, BKn = d.B.inner_is_k != 0;
   int rc;
-  if (AK && BKn) {
+  if (bf16_ops) {
+    B2P_CHECK_ARG(AK || !BKn, "gemm: A inner=m with B inner=k layout not supported");
+    rc = b2p_gemm16_launch(d, st);
+  } else if (AK && BKn) {
     if (d.A.conv) rc = launch_tiles<true, true, true, false>(d, ea, st);
     else if (d.B.conv) { b2p_set_error("gemm: conv view on B requires B inner=n"); return 1; }
     else rc = launch_tiles<true, true, false, false>(d, ea, st);

@@ -1,0 +1,354 @@
+// bf16-operand GEMM for gfx950: operands live in HBM as bf16 and are copied straight into LDS
+// with global_load_lds_dwordx4 (no VGPR staging, no conversion), then fed to
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+//
+// Tile 128 x 128 x KT (KT = 64 or 32), 256 threads = 4 waves (2 x 2), each wave a 64 x 64 sub-tile
+// (4 x 4 MFMA tiles); S LDS stages with S-1 tiles in flight behind counted vmcnt waits and raw
+// s_barrier (a __syncthreads() would drain every outstanding DMA); the epilogue is staged through
+// LDS so C / bias / aux / residual move as 16-byte vectors.
+//
+// LDS images (byte offsets inside one 16 KB operand stage; every glds wave-instruction writes
+// 1024 contiguous bytes, lane L at +16*L, so swizzles are applied to the GLOBAL source address):
+//  * k-contiguous operand ([row][KT k]): chunk c (8 k-values) of row r is stored in slot
+//    c ^ swz_k(r). A ds_read_b128 fragment read (16 rows x one chunk per 16-lane group) then
+//    covers all 64 banks once: conflict-free (measured SQ_LDS_BANK_CONFLICT = 0).
+//  * m/n-contiguous operand ([64 k][128 mn], 256-B rows): chunk c of row r in slot
+//    c ^ (((r & 3) << 2) | ((r >> 2) & 3)); read with ds_read_b64_tr_b16 (4 k-rows x 16 columns per
+//    16-lane group, delivered column-major = the MFMA operand layout).
+//
+// Elements outside the operand (k >= K, rows >= M/N, conv frames outside [0, T_in)) are loaded
+// from a 16-byte zero page instead, so the loads stay branch-free.
+#include "common.h"
+#include "../../include/b2p_hip.h"
+#include "gemm_epi.h"
+#include <stdio.h>
+#include <stdlib.h>
+
+namespace {
+
+constexpr int NT16 = 256;
+constexpr int TILE = 128;
+
+__device__ __attribute__((aligned(16))) uint32_t g_zero_page[8];   // zero-initialised
+
+typedef __attribute__((address_space(3))) void lds_t;
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ void glds16(const void* src, lds_t* dst) {
+  __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// swizzle of a k-contiguous image with 2*KT-byte rows (slot = chunk ^ swz_k(row)); both make a
+// 16x32 ds_read_b128 fragment read conflict-free (each 16-lane group covers all 64 banks once)
+template <int KT>
+__device__ __forceinline__ int swz_k(int r) {
+  if constexpr (KT == 64) return (r >> 1) & 7;
+  else return ((r >> 3) & 1) << 1;
+}
+// swizzle of an mn-contiguous image with 256-B rows (128 bf16), for ds_read_b64_tr_b16
+__device__ __forceinline__ int swz_t(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+// per-lane source state of one 128 x KT operand tile: NI glds wave-instructions per wave per tile
+template <int KT, bool INNER_K, bool CONV>
+struct Src {
+  static constexpr int NJ = TILE * KT * 2 / 1024;   // instructions per tile (all waves)
+  static constexpr int NI = NJ / 4;                 // per wave
+  static constexpr int RPI = 1024 / (2 * KT);       // INNER_K: rows per instruction
+  static constexpr int LPR = KT / 8;                // INNER_K: lanes per row
+  const uint16_t* p[NI];
+  int kofs[NI];
+  bool ok[NI];
+  int64_t rowoff[NI];
+  int frame0[NI], tap[NI], ch[NI];
+  const uint16_t* base;
+  int64_t ld;
+  int T_in, Cg;
+
+  __device__ __forceinline__ void init(const b2p_operand& o, int z1, int z2, int wave, int lane, int mn0, int MN,
+                                       int kbeg) {
+    const int64_t i1 = o.gather1 ? o.gather1[z1] : (int64_t)z1;
+    base = static_cast<const uint16_t*>(o.ptr) + i1 * o.bs1 + (int64_t)z2 * o.bs2;
+    ld = o.ld;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int j = wave * NI + i;
+      if constexpr (INNER_K) {
+        const int r = RPI * j + lane / LPR;
+        const int c = (lane % LPR) ^ swz_k<KT>(r);
+        const int row = mn0 + r;
+        ok[i] = row < MN;
+        kofs[i] = 8 * c;
+        if constexpr (CONV) {
+          const int T_out = o.conv_T_out;
+          const int rr = ok[i] ? row : 0;
+          const int b = rr / T_out, t = rr - b * T_out;
+          rowoff[i] = (int64_t)b * o.conv_sample_stride;
+          frame0[i] = t * o.conv_stride - o.conv_pad;
+          const int k = kbeg + 8 * c;
+          tap[i] = k / o.conv_Cg;
+          ch[i] = k - tap[i] * o.conv_Cg;
+          p[i] = base;
+        } else {
+          p[i] = base + (int64_t)(ok[i] ? row : 0) * ld + kbeg + 8 * c;
+        }
+      } else {
+        const int r = 4 * j + (lane >> 4);
+        const int c = (lane & 15) ^ swz_t(r);
+        const int mn = mn0 + 8 * c;
+        ok[i] = mn < MN;
+        kofs[i] = r;
+        p[i] = base + (int64_t)(kbeg + r) * ld + (ok[i] ? mn : 0);
+      }
+    }
+    if constexpr (CONV) {
+      T_in = o.conv_T_in;
+      Cg = o.conv_Cg;
+    }
+  }
+
+  // this wave's NI glds for the tile starting at k0 into the operand image `img`
+  __device__ __forceinline__ void issue(char* img, int wave, int k0, int K) {
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const void* src;
+      if constexpr (INNER_K && CONV) {
+        const int f = frame0[i] + tap[i];
+        const bool v = ok[i] && (k0 + kofs[i] < K) && f >= 0 && f < T_in;
+        src = v ? (const void*)(base + rowoff[i] + (int64_t)f * ld + ch[i]) : (const void*)g_zero_page;
+        ch[i] += KT;
+        while (ch[i] >= Cg) { ch[i] -= Cg; ++tap[i]; }
+      } else {
+        const bool v = ok[i] && (k0 + kofs[i] < K);
+        src = v ? (const void*)p[i] : (const void*)g_zero_page;
+        p[i] += INNER_K ? (int64_t)KT : (int64_t)KT * ld;
+      }
+      glds16(src, (lds_t*)(img + (wave * NI + i) * 1024));
+    }
+  }
+};
+
+// fragment reads ------------------------------------------------------------------------------
+// k-contiguous image: rows row0 .. row0+15 (lane & 15) x k = 32*kk + 8*(lane>>4) .. +7
+template <int KT>
+__device__ __forceinline__ bf16x8 frag_k(const char* img, int row0, int kk, int lane) {
+  const int r = row0 + (lane & 15);
+  const int c = (4 * kk + (lane >> 4)) ^ swz_k<KT>(r);
+  return *reinterpret_cast<const bf16x8*>(img + r * (2 * KT) + c * 16);
+}
+// mn-contiguous image: columns col0 .. col0+15 (lane & 15) x k = 32*kk + 8*(lane>>4) .. +7
+__device__ __forceinline__ bf16x8 frag_t(const char* img, int col0, int kk, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int chunk = (col0 >> 3) + (p >> 1);
+  s16x4 h[2];
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    const int row = 32 * kk + 8 * g + 4 * hh + q;
+    const char* a = img + row * 256 + ((chunk ^ swz_t(row)) << 4) + 8 * (p & 1);
+    h[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a));
+  }
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {h[0][0], h[0][1], h[0][2], h[0][3], h[1][0], h[1][1], h[1][2], h[1][3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
+constexpr int blocks_per_cu(int kt, int s) { return s * 2 * TILE * kt * 2 > 80 * 1024 ? 1 : 2; }
+
+// KT: k-tile (32 or 64); S: LDS stages (S-1 tiles in flight while one is computed)
+template <int KT, int S, bool AK, bool BK, bool ACONV>
+__global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(const b2p_gemm_desc d, const EpiArgs ea, int tiles_m,
+                                                         int tiles_n) {
+  constexpr int OP_BYTES = TILE * KT * 2;
+  constexpr int STAGE_BYTES = 2 * OP_BYTES;
+  constexpr int CS_LD = TILE + 4;                       // epilogue staging row (floats)
+  constexpr int LDS_MAIN = S * STAGE_BYTES;
+  constexpr int LDS_EPI = 64 * CS_LD * 4;
+  constexpr int LDS_BYTES = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+  constexpr int PT = 2 * Src<KT, AK, ACONV>::NI;        // glds per wave per tile (A + B)
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+
+  // XCD-aware remap (bijective): blocks with equal blockIdx.x % 8 share an XCD and its L2, so
+  // give each such group a contiguous range of tiles (neighbouring tiles share A rows).
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = tiles_m * tiles_n;
+  const int zz = wgid / tiles;
+  const int t = wgid - zz * tiles;
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+
+  const int ks = d.ksplit > 1 ? d.ksplit : 1;
+  const int z = zz / ks, ksl = zz - z * ks;
+  const int z1 = z / d.nz2, z2 = z - z1 * d.nz2;
+  const int m0 = tm * TILE, n0 = tn * TILE;
+  const int M = (int)d.M, N = (int)d.N;
+  const int kchunk = ks > 1 ? (int)d.kchunk : (int)d.K;
+  const int kbeg = ksl * kchunk;
+  const int K = ((int)d.K < kbeg + kchunk) ? (int)d.K : kbeg + kchunk;
+  const int nk = K > kbeg ? (K - kbeg + KT - 1) / KT : 0;
+
+  Src<KT, AK, ACONV> sa;
+  Src<KT, BK, false> sb;
+  sa.init(d.A, z1, z2, wave, lane, m0, M, kbeg);
+  sb.init(d.B, z1, z2, wave, lane, n0, N, kbeg);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: S-1 tiles in flight
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s) {
+    if (s < nk) {
+      sa.issue(smem + s * STAGE_BYTES, wave, kbeg + s * KT, K);
+      sb.issue(smem + s * STAGE_BYTES + OP_BYTES, wave, kbeg + s * KT, K);
+    }
+  }
+  int cur = 0;              // stage of tile kt
+  int nxt = S - 1;          // stage receiving tile kt + S - 1
+  for (int kt = 0; kt < nk; ++kt) {
+    // this wave's share of tile kt has landed (later tiles may stay in flight) ...
+    if (kt + S - 2 < nk) wait_vm<(S - 2) * PT>();
+    else wait_vm<0>();
+    // ... and everyone's has; every wave is also done reading stage kt-1 (= nxt)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (kt + S - 1 < nk) {
+      char* img = smem + nxt * STAGE_BYTES;
+      sa.issue(img, wave, kbeg + (kt + S - 1) * KT, K);
+      sb.issue(img + OP_BYTES, wave, kbeg + (kt + S - 1) * KT, K);
+    }
+    const char* As = smem + cur * STAGE_BYTES;
+    const char* Bs = As + OP_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < KT / 32; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        af[i] = AK ? frag_k<KT>(As, wm * 64 + i * 16, kk, lane) : frag_t(As, wm * 64 + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        bfr[j] = BK ? frag_k<KT>(Bs, wn * 64 + j * 16, kk, lane) : frag_t(Bs, wn * 64 + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    cur = cur + 1 == S ? 0 : cur + 1;
+    nxt = nxt + 1 == S ? 0 : nxt + 1;
+  }
+
+  // epilogue, staged through LDS in two 64-row halves so that every thread then handles 4
+  // consecutive columns (16-B loads/stores of C, bias, aux, residual; 8-B bf16 copy)
+  float* Cs = reinterpret_cast<float*>(smem);
+  float* slab = ks > 1 ? d.workspace + ((int64_t)z * ks + ksl) * (int64_t)M * N : nullptr;
+  const int cg = tid & 31, rbase = tid >> 5;
+#pragma clang loop unroll(full)
+  for (int half = 0; half < 2; ++half) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (wm == half) {
+#pragma clang loop unroll(full)
+      for (int i = 0; i < 4; ++i)
+#pragma clang loop unroll(full)
+        for (int j = 0; j < 4; ++j)
+#pragma clang loop unroll(full)
+          for (int r = 0; r < 4; ++r)
+            Cs[(i * 16 + (lane >> 4) * 4 + r) * CS_LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+    }
+    __syncthreads();
+#pragma clang loop unroll(full)
+    for (int i = 0; i < 8; ++i) {
+      const int rl = rbase + 8 * i;
+      const float4 v = *reinterpret_cast<const float4*>(Cs + rl * CS_LD + 4 * cg);
+      const int m = m0 + half * 64 + rl, n = n0 + 4 * cg;
+      if (ks > 1) {
+        if (m < M) {
+          float* dst = slab + (int64_t)m * N + n;
+          if (ea.vec4 && n + 4 <= N) *reinterpret_cast<float4*>(dst) = v;
+          else {
+            if (n < N) dst[0] = v.x;
+            if (n + 1 < N) dst[1] = v.y;
+            if (n + 2 < N) dst[2] = v.z;
+            if (n + 3 < N) dst[3] = v.w;
+          }
+        }
+      } else {
+        epilogue_store4(ea, z, z1, z2, m, n, v);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+// K-tile / stage selection (B2P_GEMM16=KT,S for experiments; default 64,2)
+static void cfg16(int* kt, int* st) {
+  static int v[2] = {0, 0};
+  if (!v[0]) {
+    int a = 64, b = 2;
+    if (const char* e = getenv("B2P_GEMM16")) sscanf(e, "%d,%d", &a, &b);
+    if (!((a == 64 && (b == 2 || b == 3)) || (a == 32 && (b == 2 || b == 3 || b == 4)))) { a = 64; b = 2; }
+    v[0] = a; v[1] = b;
+  }
+  *kt = v[0];
+  *st = v[1];
+}
+
+template <int KT, int S>
+static void launch16(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st, dim3 grid, int tm, int tn) {
+  const dim3 block(NT16);
+  const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
+  if (AK && BK) {
+    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<KT, S, true, true, true>), grid, block, 0, st, d, ea, tm, tn);
+    else hipLaunchKernelGGL((gemm16_kernel<KT, S, true, true, false>), grid, block, 0, st, d, ea, tm, tn);
+  } else if (AK && !BK) {
+    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<KT, S, true, false, true>), grid, block, 0, st, d, ea, tm, tn);
+    else hipLaunchKernelGGL((gemm16_kernel<KT, S, true, false, false>), grid, block, 0, st, d, ea, tm, tn);
+  } else {
+    hipLaunchKernelGGL((gemm16_kernel<KT, S, false, false, false>), grid, block, 0, st, d, ea, tm, tn);
+  }
+}
+
+int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
+  const EpiArgs ea = make_epi_args(d);
+  const int ks = d.ksplit > 1 ? d.ksplit : 1;
+  const int tm = (int)((d.M + TILE - 1) / TILE), tn = (int)((d.N + TILE - 1) / TILE);
+  const int64_t nwg = (int64_t)tm * tn * d.nz1 * d.nz2 * ks;
+  if (nwg >= (1ll << 31)) {
+    b2p_set_error("gemm16: grid too large");
+    return 1;
+  }
+  int kt, stg;
+  cfg16(&kt, &stg);
+  if (!getenv("B2P_GEMM16")) {
+    // measured (tools/bench_gemm.py b16): 64-deep k-tiles win on long unsplit plain K (fewer
+    // barriers per FLOP), 32-deep on short K, split-K slices and the implicit-conv operand
+    const int64_t kblk = ks > 1 ? d.kchunk : d.K;
+    kt = (kblk >= 2048 && ks == 1 && !d.A.conv) ? 64 : 32;
+    stg = 2;
+  }
+  if (ks > 1 && d.kchunk % kt != 0) kt = 32;
+  const dim3 grid((unsigned)nwg);
+  if (kt == 64) {
+    if (stg == 3) launch16<64, 3>(d, ea, st, grid, tm, tn);
+    else launch16<64, 2>(d, ea, st, grid, tm, tn);
+  } else {
+    if (stg == 4) launch16<32, 4>(d, ea, st, grid, tm, tn);
+    else if (stg == 3) launch16<32, 3>(d, ea, st, grid, tm, tn);
+    else launch16<32, 2>(d, ea, st, grid, tm, tn);
+  }
+  return 0;
+}

@@ -95,7 +95,10 @@ def _chk(t: torch.Tensor, name: str) -> None:
 
 
 def _p(t, off: int = 0):
-    return None if t is None else t.data_ptr() + 4 * off
+    if t is None:
+        return None
+    es = t.element_size() if isinstance(t, torch.Tensor) else 4
+    return t.data_ptr() + es * off
 
 
 def _st():
@@ -112,6 +115,7 @@ def op(t, off=0, ld=0, k_inner=True, bs1=0, bs2=0, gather=None):
     o.gather1 = None if gather is None else gather.data_ptr()
     o.inner_is_k = 1 if k_inner else 0
     o.conv = 0
+    o.dtype = 1 if isinstance(t, torch.Tensor) and t.dtype == torch.bfloat16 else 0
     return o
 
 
@@ -129,7 +133,9 @@ def conv_op(t, off, ld, T_out, T_in, stride, pad, Cg, sample_stride, k_inner=Tru
 
 def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1, nz2=1, alpha=1.0,
          beta=0.0, bias=None, biasbs1=0, bias_gather=None, pre_out=None, act=0, act_bwd=0, aux=None, ldaux=0, abs1=0, abs2=0,
-         drop_p=0.0, seed=0, residual=None, r_off=0, ldr=0, rbs1=0, rbs2=0, timing=0):
+         drop_p=0.0, seed=0, residual=None, r_off=0, ldr=0, rbs1=0, rbs2=0, timing=0, C16=None):
+    """C may be None when only the bf16 copy C16 (same strides) is wanted. Both operands bf16
+    (Operand.dtype 1) selects the LDS-DMA kernel (gemm16.hip)."""
     d = GemmDesc()
     d.M, d.N, d.K = M, N, K
     d.nz1, d.nz2 = nz1, nz2
@@ -137,6 +143,7 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     d.B = B
     e = Epilogue()
     e.C = _p(C, c_off)
+    e.C16 = _p(C16, c_off)
     e.ldc, e.cbs1, e.cbs2 = ldc, cbs1, cbs2
     e.alpha, e.beta = alpha, beta
     e.bias = _p(bias)
@@ -157,15 +164,18 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     ws = None
     plain = (bias is None and pre_out is None and act == 0 and act_bwd == 0 and drop_p == 0.0 and residual is None)
     if plain and K >= 2048:
-        bn = 64 if N <= 64 else 128
+        b16 = A.dtype == 1
+        bn = 64 if (N <= 64 and not b16) else 128
         blocks = -(-M // 128) * -(-N // bn) * nz1 * nz2
         if blocks < 240:
             ks = min(-(-512 // blocks), K // 1024)
             if ks >= 2:
+                q = 64 if b16 else 32
                 kchunk = -(-K // ks)
-                kchunk = -(-kchunk // 32) * 32
+                kchunk = -(-kchunk // q) * q
                 ks = -(-K // kchunk)
-                ws = torch.empty(ks * nz1 * nz2 * M * N, device=C.device, dtype=torch.float32)
+                dev = (C if C is not None else C16).device
+                ws = torch.empty(ks * nz1 * nz2 * M * N, device=dev, dtype=torch.float32)
                 d.ksplit, d.kchunk = ks, kchunk
                 d.workspace = ws.data_ptr()
                 d.workspace_floats = ws.numel()
@@ -251,6 +261,116 @@ def _ln_bwd(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, s
               _p(dx_accum), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed, _p(dbias_in),
               _p(ws), _st())
     return dx, dg, db, dxd
+
+
+
+# ------------------------------------------------------------------ bf16 GEMM operands
+# In bf16 mode every large GEMM reads bf16 copies of its operands straight into LDS (gemm16.hip).
+# Master weights, activations needed by elementwise kernels, and all gradients stay fp32; the
+# bf16 copies are written by the producing kernel (GEMM epilogue C16, LayerNorm y16/d16) or by
+# one cast. Rounding is the same RNE fp32->bf16 the fp32-operand kernel applies while staging,
+# so both paths compute the same products.
+BF16 = torch.bfloat16
+_PARAM_EPOCH: dict = {}
+_W16: dict = {}
+
+
+def bf16_mode() -> bool:
+    return _prec() == 0
+
+
+def bump_param_epoch(params) -> None:
+    """Called by optimisers that update parameters in place through raw pointers (HipAdam):
+    torch's version counter does not see those writes, so cached bf16 weight copies would go
+    stale without this."""
+    for p in params:
+        _PARAM_EPOCH[id(p)] = _PARAM_EPOCH.get(id(p), 0) + 1
+
+
+def _stamp(ws):
+    return tuple((id(w), w.data_ptr(), tuple(w.shape), w._version, _PARAM_EPOCH.get(id(w), 0)) for w in ws)
+
+
+def cast16(x, out=None):
+    out = torch.empty(x.shape, device=x.device, dtype=BF16) if out is None else out
+    _lib.call("b2p_cast_bf16", _p(x), _p(out), x.numel(), _st())
+    return out
+
+
+def weight16(*ws):
+    """bf16 copy of fp32 weight(s), rows concatenated ([wq; wk; wv] -> one QKV operand); cached
+    until any source tensor changes (version counter or optimiser epoch)."""
+    key = tuple(id(w) for w in ws)
+    st = _stamp(ws)
+    hit = _W16.get(key)
+    if hit is not None and hit[0] == st:
+        return hit[1]
+    rows = sum(w.shape[0] for w in ws)
+    out = torch.empty((rows,) + tuple(ws[0].shape[1:]), device=ws[0].device, dtype=BF16)
+    off = 0
+    for w in ws:
+        _chk(w, "weight16")
+        _lib.call("b2p_cast_bf16", _p(w), _p(out, off), w.numel(), _st())
+        off += w.numel()
+    _W16[key] = (st, out)
+    return out
+
+
+def bias_cat(*bs):
+    """fp32 concatenation of biases (None -> zeros), cached like weight16."""
+    ref = next(b for b in bs if b is not None)
+    real = tuple(b for b in bs if b is not None)
+    key = ("bias",) + tuple(id(b) if b is not None else None for b in bs)
+    st = _stamp(real)
+    hit = _W16.get(key)
+    if hit is not None and hit[0] == st:
+        return hit[1]
+    out = torch.zeros(sum(ref.numel() for _ in bs), device=ref.device)
+    n = ref.numel()
+    for i, b in enumerate(bs):
+        if b is not None:
+            out[i * n:(i + 1) * n].copy_(b)
+    _W16[key] = (st, out)
+    return out
+
+
+def attach16(x, x16) -> None:
+    """Marks x16 as the bf16 copy of x (consumed by the next op's GEMM instead of a cast)."""
+    x._b16 = (x._version, x16)
+
+
+def to16(x):
+    t = getattr(x, "_b16", None)
+    if t is not None and t[0] == x._version:
+        return t[1]
+    return cast16(x.contiguous())
+
+
+def _ln_fwd16(x2d, g, b, eps, drop_p=0.0, seed=0):
+    rows, cols = x2d.shape
+    y = torch.empty_like(x2d)
+    y16 = torch.empty(rows, cols, device=x2d.device, dtype=BF16)
+    mean = torch.empty(rows, device=x2d.device)
+    rstd = torch.empty(rows, device=x2d.device)
+    _lib.call("b2p_layernorm_fwd16", _p(x2d), _p(g), _p(b), _p(y), _p(y16), _p(mean), _p(rstd), rows, cols,
+              float(eps), float(drop_p), seed, _st())
+    return y, y16, mean, rstd
+
+
+def _ln_bwd16(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, seed=0, in_drop_p=-1.0,
+              in_seed=0, dbias_in=None):
+    """as _ln_bwd, plus d16 = bf16(dx_dropped if in_drop_p >= 0 else dx)"""
+    rows, cols = x.shape
+    dx = torch.empty_like(x)
+    dg = torch.empty(cols, device=x.device) if need_params else None
+    db = torch.empty(cols, device=x.device) if need_params else None
+    ws = torch.empty(int(_lib.load().b2p_layernorm_bwd_workspace(rows, cols)), device=x.device)
+    dxd = torch.empty_like(x) if in_drop_p >= 0.0 else None
+    d16 = torch.empty(rows, cols, device=x.device, dtype=BF16)
+    _lib.call("b2p_layernorm_bwd16", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows,
+              cols, _p(dx_accum), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed,
+              _p(dbias_in), _p(d16), _p(ws), _st())
+    return dx, dg, db, dxd, d16
 
 
 # =====================================================================================
@@ -591,7 +711,7 @@ def pos_conv_ln(e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, training):
 # attention core shared by the w2v and Conformer layers: softmax(Q K^T * scale) -> dropout -> @ V
 # qkv (B*T, 3D) laid out [b][t][q|k|v][h][dh]
 # =====================================================================================
-def _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seed):
+def _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seed, want16=False):
     D = nh * dh
     dev = qkv.device
     Tp = (T + 3) // 4 * 4
@@ -603,13 +723,16 @@ def _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seed):
     _lib.call("b2p_softmax_fwd", _p(S), _p(P), _p(Pd), B * nh * T, T, Tp, float(p_attn), seed, _st())
     del S
     O = torch.empty(B * T, D, device=dev)
+    O16 = torch.empty(B * T, D, device=dev, dtype=BF16) if want16 else None
     gemm(T, dh, T, op(Pd, 0, Tp, True, bs1=nh * T * Tp, bs2=T * Tp),
-         op(qkv, 2 * D, 3 * D, False, bs1=T * 3 * D, bs2=dh), O, D, cbs1=T * D, cbs2=dh, nz1=B, nz2=nh)
+         op(qkv, 2 * D, 3 * D, False, bs1=T * 3 * D, bs2=dh), O, D, cbs1=T * D, cbs2=dh, nz1=B, nz2=nh, C16=O16)
+    if want16:
+        return P, (Pd if p_attn > 0 else None), O, O16
     return P, (Pd if p_attn > 0 else None), O
 
 
-def _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seed):
-    """returns dqkv (B*T, 3D) = [dQ | dK | dV]"""
+def _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seed, want16=False):
+    """returns dqkv (B*T, 3D) = [dQ | dK | dV] (and its bf16 copy when want16)"""
     D = nh * dh
     dev = qkv.device
     Tp = P.shape[-1]
@@ -619,17 +742,20 @@ def _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seed):
     gemm(T, T, dh, op(dO, 0, D, True, bs1=T * D, bs2=dh), op(qkv, 2 * D, 3 * D, True, bs1=T * 3 * D, bs2=dh),
          dPd, Tp, cbs1=nh * T * Tp, cbs2=T * Tp, nz1=B, nz2=nh)
     dqkv = torch.empty(B * T, 3 * D, device=dev)
+    d16 = torch.empty(B * T, 3 * D, device=dev, dtype=BF16) if want16 else None
     gemm(T, dh, T, op(Pd, 0, Tp, False, bs1=nh * T * Tp, bs2=T * Tp), op(dO, 0, D, False, bs1=T * D, bs2=dh),
-         dqkv, 3 * D, c_off=2 * D, cbs1=T * 3 * D, cbs2=dh, nz1=B, nz2=nh)
+         dqkv, 3 * D, c_off=2 * D, cbs1=T * 3 * D, cbs2=dh, nz1=B, nz2=nh, C16=d16)
     dS = torch.empty_like(dPd)
     _lib.call("b2p_softmax_bwd", _p(P), _p(dPd), _p(dS), B * nh * T, T, Tp, float(p_attn), seed, _st())
     del dPd
     gemm(T, dh, T, op(dS, 0, Tp, True, bs1=nh * T * Tp, bs2=T * Tp),
          op(qkv, D, 3 * D, False, bs1=T * 3 * D, bs2=dh), dqkv, 3 * D, c_off=0, cbs1=T * 3 * D, cbs2=dh,
-         nz1=B, nz2=nh, alpha=scale)
+         nz1=B, nz2=nh, alpha=scale, C16=d16)
     gemm(T, dh, T, op(dS, 0, Tp, False, bs1=nh * T * Tp, bs2=T * Tp),
          op(qkv, 0, 3 * D, False, bs1=T * 3 * D, bs2=dh), dqkv, 3 * D, c_off=D, cbs1=T * 3 * D, cbs2=dh,
-         nz1=B, nz2=nh, alpha=scale)
+         nz1=B, nz2=nh, alpha=scale, C16=d16)
+    if want16:
+        return dqkv, d16
     return dqkv
 
 
@@ -734,11 +860,134 @@ class _EncoderLayer(torch.autograd.Function):
         return (dx, None, *grads_w, dwo, dbo, dg1, dbe1, dw1, db1, dw2, db2, dg2, dbe2)
 
 
+class _EncoderLayer16(torch.autograd.Function):
+    """bf16-operand variant of _EncoderLayer (same math, same dropout masks): Q/K/V fused into one
+    GEMM over the concatenated bf16 weight, every projection reading bf16 copies written by the
+    producing kernel; fp32 residual stream, LayerNorm statistics and gradients."""
+
+    @staticmethod
+    def forward(ctx, x, cfg, wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
+        nh, eps, p_attn, p_hid, p_act, seeds = cfg
+        _chk(x, "encoder_layer.x")
+        B, T, D = x.shape
+        dh = D // nh
+        NT = B * T
+        F = w1.shape[0]
+        dev = x.device
+        x2 = x.view(NT, D)
+        x16 = to16(x).view(NT, D)
+        wqkv16 = weight16(wq, wk, wv)
+        bqkv = bias_cat(bq, bk, bv) if any(b is not None for b in (bq, bk, bv)) else None
+        qkv = torch.empty(NT, 3 * D, device=dev)
+        gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), qkv, 3 * D, bias=bqkv)
+        P, Pd, _O, O16 = _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seeds[0], want16=True)
+        del _O
+        # y1 = x + dropout(O Wo^T + bo)
+        wo16 = weight16(wo)
+        y1 = torch.empty(NT, D, device=dev)
+        gemm(NT, D, D, op(O16, 0, D, True), op(wo16, 0, D, True), y1, D, bias=bo, drop_p=p_hid, seed=seeds[1],
+             residual=x2)
+        x1, x1_16, m1, r1 = _ln_fwd16(y1, g1, be1, eps)
+        # FFN: f = dropout(gelu(x1 W1^T + b1)) (bf16 only: it is a GEMM operand and nothing else)
+        w1_16, w2_16 = weight16(w1), weight16(w2)
+        pre = torch.empty(NT, F, device=dev)
+        f16 = torch.empty(NT, F, device=dev, dtype=BF16)
+        gemm(NT, F, D, op(x1_16, 0, D, True), op(w1_16, 0, D, True), None, F, bias=b1, pre_out=pre,
+             act=ACT["gelu"], drop_p=p_act, seed=seeds[2], C16=f16)
+        y2 = torch.empty(NT, D, device=dev)
+        gemm(NT, D, F, op(f16, 0, F, True), op(w2_16, 0, F, True), y2, D, bias=b2, drop_p=p_hid, seed=seeds[3],
+             residual=x1)
+        del x1
+        out, out16, m2, r2 = _ln_fwd16(y2, g2, be2, eps)
+        ctx.save_for_backward(x16, qkv, P, Pd, O16, y1, x1_16, m1, r1, pre, f16, y2, m2, r2,
+                              wq, wk, wv, wo, g1, w1, w2, g2)
+        ctx.cfg = cfg
+        ctx.shape = (B, T, D)
+        ctx.has_b = [b is not None for b in (bq, bk, bv, bo, b1, b2)]
+        res = out.view(B, T, D)
+        attach16(res, out16.view(B, T, D))
+        return res
+
+    @staticmethod
+    def backward(ctx, dout):
+        (x16, qkv, P, Pd, O16, y1, x1_16, m1, r1, pre, f16, y2, m2, r2, wq, wk, wv, wo, g1, w1, w2,
+         g2) = ctx.saved_tensors
+        nh, eps, p_attn, p_hid, p_act, seeds = ctx.cfg
+        B, T, D = ctx.shape
+        dh = D // nh
+        NT = B * T
+        F = w1.shape[0]
+        dev = y1.device
+        ng = ctx.needs_input_grad
+        dout = dout.contiguous().view(NT, D)
+        w1_16, w2_16, wo16, wqkv16 = weight16(w1), weight16(w2), weight16(wo), weight16(wq, wk, wv)
+        # LN2 backward -> dy2 ; dz2 = dropout-mask(dy2) (output dropout of the FFN), bf16 copy dz2_16
+        db2 = torch.empty(D, device=dev) if ng[15] else None
+        dy2, dg2, dbe2, _dz2, dz2_16 = _ln_bwd16(dout, y2, g2, m2, r2, True, in_drop_p=p_hid, in_seed=seeds[3],
+                                                 dbias_in=db2)
+        del _dz2
+        dw2 = None
+        if ng[14]:
+            dw2 = torch.empty_like(w2)
+            gemm(D, F, NT, op(dz2_16, 0, D, False), op(f16, 0, F, False), dw2, F)
+        # dpre = (dz2 W2) * mask_act * gelu'(pre): fp32 for the bias sum, bf16 for the GEMMs
+        dpre = torch.empty(NT, F, device=dev)
+        dpre16 = torch.empty(NT, F, device=dev, dtype=BF16)
+        gemm(NT, F, D, op(dz2_16, 0, D, True), op(w2_16, 0, F, False), dpre, F, drop_p=p_act, seed=seeds[2],
+             act_bwd=ACT["gelu"], aux=pre, C16=dpre16)
+        dw1 = None
+        if ng[12]:
+            dw1 = torch.empty_like(w1)
+            gemm(F, D, NT, op(dpre16, 0, F, False), op(x1_16, 0, D, False), dw1, D)
+        db1 = torch.empty(F, device=dev) if ng[13] else None
+        if db1 is not None:
+            colsum(dpre, NT, F, db1)
+        del dpre
+        # dx1 = dpre W1 + dy2
+        dx1 = torch.empty(NT, D, device=dev)
+        gemm(NT, D, F, op(dpre16, 0, F, True), op(w1_16, 0, D, False), dx1, D, residual=dy2)
+        del dpre16
+        # LN1 backward -> dy1 ; dz1 = dropout-mask(dy1) (attention output dropout)
+        dbo = torch.empty(D, device=dev) if ng[9] else None
+        dy1, dg1, dbe1, _dz1, dz1_16 = _ln_bwd16(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1],
+                                                 dbias_in=dbo)
+        del _dz1
+        dwo = None
+        if ng[8]:
+            dwo = torch.empty_like(wo)
+            gemm(D, D, NT, op(dz1_16, 0, D, False), op(O16, 0, D, False), dwo, D)
+        dO = torch.empty(NT, D, device=dev)
+        gemm(NT, D, D, op(dz1_16, 0, D, True), op(wo16, 0, D, False), dO, D)
+        dqkv, dqkv16 = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seeds[0], want16=True)
+        del dO
+        grads_w = [None] * 6
+        if ng[2] or ng[4] or ng[6]:
+            dwqkv = torch.empty(3 * D, D, device=dev)
+            gemm(3 * D, D, NT, op(dqkv16, 0, 3 * D, False), op(x16, 0, D, False), dwqkv, D)
+            for i in range(3):
+                if ng[2 + 2 * i]:
+                    grads_w[2 * i] = dwqkv[i * D:(i + 1) * D]
+        if any(ctx.has_b[i] and ng[3 + 2 * i] for i in range(3)):
+            dbqkv = torch.empty(3 * D, device=dev)
+            colsum(dqkv, NT, 3 * D, dbqkv)
+            for i in range(3):
+                if ctx.has_b[i] and ng[3 + 2 * i]:
+                    grads_w[2 * i + 1] = dbqkv[i * D:(i + 1) * D]
+        dx = None
+        if ng[0]:
+            dx = torch.empty(NT, D, device=dev)
+            gemm(NT, D, 3 * D, op(dqkv16, 0, 3 * D, True), op(wqkv16, 0, D, False), dx, D, residual=dy1)
+            dx = dx.view(B, T, D)
+        return (dx, None, *grads_w, dwo, dbo, dg1, dbe1, dw1, db1, dw2, db2, dg2, dbe2)
+
+
 def encoder_layer(x, params, nh, eps, p_attn, p_hid, p_act, training):
     if not training:
         p_attn = p_hid = p_act = 0.0
     seeds = tuple(SEEDS.next() for _ in range(4)) if training else (0, 0, 0, 0)
     cfg = (nh, eps, float(p_attn), float(p_hid), float(p_act), seeds)
+    if bf16_mode():
+        return _EncoderLayer16.apply(x.contiguous(), cfg, *params)
     return _EncoderLayer.apply(x.contiguous(), cfg, *params)
 
 

@@ -10,6 +10,7 @@ import math
 import torch
 
 from . import _lib
+from . import functional as Fn
 
 
 class HipAdam(torch.optim.Optimizer):
@@ -66,4 +67,5 @@ class HipAdam(torch.optim.Optimizer):
                 _lib.check(lib.b2p_adam_multi(table.data_ptr(), len(ps), maxn, float(group["lr"]), float(b1),
                                               float(b2), float(group["eps"]), float(group["weight_decay"]),
                                               float(bc1), float(bc2s), stream), "b2p_adam_multi")
+                Fn.bump_param_epoch(ps)   # in-place writes invisible to torch: drop bf16 weight copies
         return loss
