@@ -213,6 +213,30 @@ int b2p_gru_fwd(const float* gi, const float* whh, const float* bhh, const float
 int b2p_gru_bwd(const float* dout, const float* whh, const float* out, const float* saved,
                 const float* h0, float* dgi, float* dgh, float* dh0, float* dhbuf, int64_t B,
                 int64_t T, int64_t H, int ndir, b2p_stream_t stream);
+/* Persistent bf16-MFMA recurrence (bf16 precision mode; csrc/gru16.hip): one workgroup runs the
+ * whole time loop of one direction for 16 batch rows with W_hh resident on the CU (registers +
+ * LDS) — one launch per layer instead of one per time step (replaces the cuDNN RNN behind
+ * nn.GRU, src/model/brain_feature_extractor.py:39-47). Per-step tensors are LANE-NATIVE ("LN"):
+ * for direction d, 16-row batch group bg, processing step s (= t forward, T-1-t reverse),
+ * 16-unit block ub and record r, float offset
+ *   (((((d*NBG + bg)*T + s)*(H/16) + ub)*R + r)*64 + lane)*4 + i,
+ *   lane = b%16 + 16*((j%16)/4), i = j%4   (NBG = ceil(B/16); b2p_gru16_lane_floats sizes it).
+ * fwd: giL = LN(R=3) of x W_ih^T + b_ih + [b_hr, b_hz, 0] (b_hh's r/z parts folded in; bhh is
+ *      read for b_hn only) -> hL = LN(R=1) of h, savL = LN(R=4) of (r, z, n, W_hn h + b_hn).
+ * bwd: doL = LN(R=1) of dOut, hL/savL from fwd -> dgL = LN(R=4) of (dar, daz, dan, dan*r)
+ *      (= dgi gates 0..2, dgh = records 0, 1, 3); dh0 [ndir][B][H] optional.
+ * b2p_gru_lane_permute: standard (B, T, ndir*Rs*H) <-> LN(Rl); rmap nibble k = standard record of
+ * LN record k (15 = skip), to_lane selects the direction. Supported H: b2p_gru16_supported(H) (32, 64, 128, 256). */
+int b2p_gru16_supported(int64_t H);
+int64_t b2p_gru16_lane_floats(int64_t B, int64_t T, int64_t H, int ndir, int R);
+int b2p_gru_lane_permute(const float* src, float* dst, int64_t B, int64_t T, int64_t H, int ndir,
+                         int Rl, int Rs, uint32_t rmap, int to_lane, b2p_stream_t stream);
+int b2p_gru_fwd16(const float* giL, const float* whh, const float* bhh, const float* h0,
+                  float* hL, float* savL, int64_t B, int64_t T, int64_t H, int ndir,
+                  b2p_stream_t stream);
+int b2p_gru_bwd16(const float* doL, const float* whh, const float* hL, const float* savL,
+                  const float* h0, float* dgL, float* dh0, int64_t B, int64_t T, int64_t H,
+                  int ndir, b2p_stream_t stream);
 /* h_prev sequence for the weight-gradient GEMM: hp[dir][b][t][j] = h_{t-1} in that direction's
  * processing order (h0 at the first step). */
 int b2p_gru_hprev(const float* out, const float* h0, float* hp, int64_t B, int64_t T, int64_t H,

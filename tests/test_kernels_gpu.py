@@ -130,6 +130,49 @@ def test_gru_layer(unfold, h0):
         assert _rel(a.cpu(), b) < 2e-4
 
 
+@pytest.mark.parametrize("H,B,T,h0,unfold", [(32, 3, 17, True, False), (64, 5, 23, True, False), (128, 20, 40, False, False),
+                                               (256, 33, 57, True, False), (256, 32, 249, False, True)])
+def test_gru_layer_bf16_persistent(H, B, T, h0, unfold):
+    """bf16 mode: the persistent MFMA recurrence (csrc/gru16.hip) vs the fp32 oracle GRU
+    (nn.GRU semantics). bf16 MFMA operands (W_hh, h) -> relative L2 tolerance 2e-2 on outputs and
+    every gradient; B not a multiple of the 16-row workgroup tile; both directions; optional h0."""
+    Fn = _fn()
+    from oracle.b2p2t_oracle import gru_direction, unfold as unfold_ref
+    torch.manual_seed(11)
+    if unfold:
+        C, k, s = 16, 32, 4
+        L = (T - 1) * s + k
+        xsrc = torch.randn(B, L, C)
+        x_ref_fn = lambda x: unfold_ref(x, k, s)
+    else:
+        IN = 48
+        xsrc = torch.randn(B, T, IN)
+        x_ref_fn = lambda x: x
+    IN = x_ref_fn(xsrc).shape[-1]
+    ws = []
+    for d in range(2):
+        ws += [torch.randn(3 * H, IN) / math.sqrt(IN), torch.randn(3 * H, H) / math.sqrt(H),
+               torch.randn(3 * H) * 0.1, torch.randn(3 * H) * 0.1]
+    hz = torch.randn(2, B, H) if h0 else None
+    wr = [w.clone().requires_grad_(True) for w in ws]
+    xr = xsrc.clone().requires_grad_(True)
+    hr = hz.clone().requires_grad_(True) if h0 else None
+    xin = x_ref_fn(xr)
+    ref = torch.cat([gru_direction(xin, *wr[4 * d:4 * d + 4], hr[d] if h0 else None, d == 1) for d in range(2)], -1)
+    dout = torch.randn_like(ref)
+    refg = torch.autograd.grad(ref, [xr, *wr] + ([hr] if h0 else []), dout)
+    with Fn.precision("bf16"):
+        wg = [w.cuda().requires_grad_(True) for w in ws]
+        xs = xsrc.cuda().requires_grad_(True)
+        x_in = Fn.Unfolded(xs, k, s) if unfold else xs
+        hg = hz.cuda().requires_grad_(True) if h0 else None
+        out = Fn.gru_layer(x_in, H, 2, wg, hg)
+        assert _rel(out.detach().cpu(), ref.detach()) < 2e-2
+        got = torch.autograd.grad(out, [xs, *wg] + ([hg] if h0 else []), dout.cuda())
+    for i, (a, b) in enumerate(zip(got, refg)):
+        assert _rel(a.cpu(), b) < 3e-2, i
+
+
 def test_front_end():
     Fn = _fn()
     from oracle.b2p2t_oracle import gaussian_taps, gaussian_smooth, day_linear_softsign

@@ -23,6 +23,7 @@ c_i32 = ctypes.c_int32
 c_f32 = ctypes.c_float
 c_f64 = ctypes.c_double
 c_u64 = ctypes.c_uint64
+c_u32 = ctypes.c_uint32
 c_p = ctypes.c_void_p
 
 
@@ -87,6 +88,11 @@ _SIGS = {
     "b2p_weight_norm_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p]),
     "b2p_gru_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_gru_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_gru16_supported": (c_i32, [c_i64]),
+    "b2p_gru16_lane_floats": (c_i64, [c_i64, c_i64, c_i64, c_i32, c_i32]),
+    "b2p_gru_lane_permute": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_u32, c_i32, c_p]),
+    "b2p_gru_fwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_gru_bwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_gru_hprev": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_ctc_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "b2p_ctc_fwd_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),

@@ -20,6 +20,8 @@ import ctypes
 import math
 import threading
 
+import os
+
 import torch
 
 from . import _lib
@@ -445,6 +447,14 @@ class Unfolded:
         return win.permute(0, 1, 3, 2).reshape(B, self.T, C * self.kernel)
 
 
+# persistent MFMA recurrence in bf16 mode (B2P_GRU16=0 selects the per-step fp32 kernels, for A/B checks)
+_GRU16 = [os.environ.get("B2P_GRU16", "1") != "0"]
+
+
+def _ln_floats(B, T, H, ndir, R):
+    return int(_lib.load().b2p_gru16_lane_floats(B, T, H, ndir, R))
+
+
 def _stack2(a, b):
     return a.unsqueeze(0) if b is None else torch.stack([a, b], 0)
 
@@ -469,6 +479,12 @@ class _GRULayer(torch.autograd.Function):
         for w in wih + whh:
             _chk(w, "gru.weight")
         gi = torch.empty(B, T, ndir * G3, device=dev)
+        # bf16 mode: persistent MFMA recurrence (csrc/gru16.hip), which wants b_hh's r/z parts folded
+        # into the input projection bias
+        use16 = bf16_mode() and _GRU16[0] and bool(_lib.load().b2p_gru16_supported(H))
+        if use16 and bhh[0] is not None:
+            bih = [(b if b is not None else torch.zeros(G3, device=dev))
+                   + torch.cat([bh[:2 * H], torch.zeros(H, device=dev)]) for b, bh in zip(bih, bhh)]
         if unf_meta is not None:
             # tap-major weight copy: W'[n][tap*C + c] = W[n][c*k + tap] for both directions
             wperm = torch.empty(ndir * G3, IN, device=dev)
@@ -488,27 +504,53 @@ class _GRULayer(torch.autograd.Function):
         whh_s = torch.stack(whh, 0).contiguous()
         bhh_s = torch.stack(bhh, 0).contiguous() if bhh[0] is not None else None
         out = torch.empty(B, T, ndir * H, device=dev)
-        saved = torch.empty(B, T, ndir, 4, H, device=dev)
+        saved = None if use16 else torch.empty(B, T, ndir, 4, H, device=dev)
         if h0 is not None:
             _chk(h0, "gru.h0")
-        _lib.call("b2p_gru_fwd", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved), B, T, H, ndir, _st())
-        ctx.save_for_backward(x, out, saved, whh_s, h0, wperm, *wih)
-        ctx.meta = (unf_meta, H, ndir, B, T, IN, bih[0] is not None, bhh[0] is not None)
+        if use16:
+            # lane-native per-step layouts (csrc/gru16.hip): gi -> giL, kernel, hL -> out
+            giL = torch.empty(_ln_floats(B, T, H, ndir, 3), device=dev)
+            _lib.call("b2p_gru_lane_permute", _p(gi), _p(giL), B, T, H, ndir, 3, 3, 0x210, 1, _st())
+            del gi
+            hL = torch.empty(_ln_floats(B, T, H, ndir, 1), device=dev)
+            saved = torch.empty(_ln_floats(B, T, H, ndir, 4), device=dev)
+            _lib.call("b2p_gru_fwd16", _p(giL), _p(whh_s), _p(bhh_s), _p(h0), _p(hL), _p(saved), B, T, H, ndir,
+                      _st())
+            del giL
+            _lib.call("b2p_gru_lane_permute", _p(hL), _p(out), B, T, H, ndir, 1, 1, 0x0, 0, _st())
+        else:
+            hL = None
+            _lib.call("b2p_gru_fwd", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved), B, T, H, ndir,
+                      _st())
+        ctx.save_for_backward(x, out, saved, whh_s, h0, wperm, hL, *wih)
+        ctx.meta = (unf_meta, H, ndir, B, T, IN, bih[0] is not None, bhh[0] is not None, use16)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, out, saved, whh_s, h0, wperm, *wih = ctx.saved_tensors
-        unf_meta, H, ndir, B, T, IN, has_bih, has_bhh = ctx.meta
+        x, out, saved, whh_s, h0, wperm, hL, *wih = ctx.saved_tensors
+        unf_meta, H, ndir, B, T, IN, has_bih, has_bhh, use16 = ctx.meta
         dev = out.device
         dout = dout.contiguous()
         G3 = 3 * H
         dgi = torch.empty(B, T, ndir * G3, device=dev)
         dgh = torch.empty(B, T, ndir * G3, device=dev)
-        dhbuf = torch.empty(ndir, B, H, device=dev)
         dh0 = torch.empty(ndir, B, H, device=dev) if (h0 is not None and ctx.needs_input_grad[4]) else None
-        _lib.call("b2p_gru_bwd", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi), _p(dgh), _p(dh0),
-                  _p(dhbuf), B, T, H, ndir, _st())
+        if use16:
+            doL = torch.empty(_ln_floats(B, T, H, ndir, 1), device=dev)
+            _lib.call("b2p_gru_lane_permute", _p(dout), _p(doL), B, T, H, ndir, 1, 1, 0x0, 1, _st())
+            dgL = torch.empty(_ln_floats(B, T, H, ndir, 4), device=dev)
+            _lib.call("b2p_gru_bwd16", _p(doL), _p(whh_s), _p(hL), _p(saved), _p(h0), _p(dgL), _p(dh0), B, T, H,
+                      ndir, _st())
+            del doL
+            # dgi = LN records (0, 1, 2), dgh = LN records (0, 1, 3)
+            _lib.call("b2p_gru_lane_permute", _p(dgL), _p(dgi), B, T, H, ndir, 4, 3, 0xF210, 0, _st())
+            _lib.call("b2p_gru_lane_permute", _p(dgL), _p(dgh), B, T, H, ndir, 4, 3, 0x2F10, 0, _st())
+            del dgL
+        else:
+            dhbuf = torch.empty(ndir, B, H, device=dev)
+            _lib.call("b2p_gru_bwd", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi), _p(dgh), _p(dh0),
+                      _p(dhbuf), B, T, H, ndir, _st())
         grads = [None] * (4 * ndir)
         # recurrent weights: dW_hh[d] = dgh[:, :, d]^T @ hprev[d]
         hp = torch.empty(ndir, B, T, H, device=dev)
