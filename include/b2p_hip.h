@@ -242,6 +242,21 @@ int b2p_gru_bwd16(const float* doL, const float* whh, const float* hL, const flo
 int b2p_gru_hprev(const float* out, const float* h0, float* hp, int64_t B, int64_t T, int64_t H,
                   int ndir, b2p_stream_t stream);
 
+/* ------------------------------------------------------------------ fused attention (bf16 mode)
+ * softmax(Q K^T * scale) -> dropout(p) -> @ V per (batch, head), no mask (HF Wav2Vec2Attention,
+ * TF w2v:438-463,529-545; the Conformer's rotary self-attention core, TF conf:458-470);
+ * csrc/attn16.hip. Head size 64, T <= 256 (whole K/V of a head in LDS, scores never in HBM).
+ * qkv16: bf16 [B*T][3*nh*64] (q | k | v, head-major), O16: bf16 [B*T][nh*64], lse2: f32 [B][nh][T]
+ * (row max + log2 sum of the log2e-scaled scores, saved for backward). Dropout keep mask =
+ * b2p_keep(seed, ((b*nh + h)*T + q)*T + key), identical to b2p_softmax_fwd's. bwd writes
+ * [dQ | dK | dV] into dqkv (f32, may be NULL) and/or dqkv16 (bf16, may be NULL), same layout as qkv;
+ * delta_ws: B*nh*T floats of workspace (row constants sum_key P_d dP_d). */
+int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
+                   int64_t dh, float scale, float drop_p, uint64_t drop_seed, b2p_stream_t stream);
+int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws,
+                   float* dqkv, void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh,
+                   float scale, float drop_p, uint64_t drop_seed, b2p_stream_t stream);
+
 /* ------------------------------------------------------------------ CTC
  * log_softmax + nn.CTCLoss(blank=0, reduction="mean", zero_infinity=True)
  * (src/model/w2v_custom_feat_extractor.py:59, 81-90). logits (B, T, C) batch-first; targets

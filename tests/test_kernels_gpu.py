@@ -173,6 +173,39 @@ def test_gru_layer_bf16_persistent(H, B, T, h0, unfold):
         assert _rel(a.cpu(), b) < 3e-2, i
 
 
+@pytest.mark.parametrize("B,T,nh,p", [(2, 249, 12, 0.0), (2, 249, 12, 0.1), (3, 100, 4, 0.1), (1, 17, 2, 0.0),
+                                       (2, 256, 3, 0.1)])
+def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p):
+    """csrc/attn16.hip (bf16 MFMA, scores on-chip) vs the unfused fp32 attention core (GEMM ->
+    softmax/dropout kernel -> GEMM) on the same bf16-rounded q/k/v and the SAME dropout mask
+    (both hash ((b*nh+h)*T+q)*T+key). Tolerance: relative L2 1e-2 on O, 2e-2 on dQ/dK/dV."""
+    Fn = _fn()
+    torch.manual_seed(7)
+    dh = 64
+    D = nh * dh
+    qkv = (torch.randn(B * T, 3 * D) * 0.7).to(torch.bfloat16).float().cuda()
+    dO = torch.randn(B * T, D).to(torch.bfloat16).float().cuda()
+    seed = 1234
+    with Fn.precision("fp32"):
+        P, Pd, O = Fn._attn_core_fwd(qkv, B, T, nh, dh, p, seed)
+        dref = Fn._attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p, seed)
+    q16 = qkv.to(torch.bfloat16)
+    O16, lse2 = Fn._attn16_fwd(q16, B, T, nh, dh, p, seed)
+    dq32, dq16 = Fn._attn16_bwd(q16, dO.to(torch.bfloat16), lse2, B, T, nh, dh, p, seed)
+    torch.cuda.synchronize()
+    rel = lambda a, b: float((a.float() - b).norm() / b.norm())
+    assert rel(O16, O) < 1e-2
+    for i, name in enumerate(("dQ", "dK", "dV")):
+        sl = slice(i * D, (i + 1) * D)
+        assert rel(dq32[:, sl], dref[:, sl]) < 2e-2, name
+        assert rel(dq16[:, sl], dref[:, sl]) < 2e-2, name
+    # lse2 = log2 sum exp(scale*s) per row
+    s = torch.einsum("bhqd,bhkd->bhqk", qkv[:, :D].view(B, T, nh, dh).permute(0, 2, 1, 3),
+                     qkv[:, D:2 * D].view(B, T, nh, dh).permute(0, 2, 1, 3)) * dh ** -0.5
+    ref_lse2 = torch.logsumexp(s, -1) / math.log(2.0)
+    assert float((lse2 - ref_lse2).abs().max()) < 2e-2
+
+
 def test_front_end():
     Fn = _fn()
     from oracle.b2p2t_oracle import gaussian_taps, gaussian_smooth, day_linear_softsign

@@ -77,6 +77,10 @@ def test_step_matches_reference_golden(name, mode):
         if mode == "fp32":
             scale = max(np.abs(r).max(), 1e-3 * gmax)
             assert np.abs(v - r).max() <= gtol * scale + 1e-5 * gmax, n
+        elif ref_norm < 1e-6 * gmax:
+            # analytically zero (attention k_proj.bias: softmax is invariant to a per-row shift, so
+            # sum_key dS = 0); in bf16 the rounded dS rows leave O(1e-5) residue
+            assert np.linalg.norm(v) <= 1e-4 * gmax, n
         else:
             # bf16 MFMA through 12+ layers: element errors are a few % of the entry scale, so the
             # check is on the relative L2 error of the stored (sampled) gradient entries

@@ -1,0 +1,35 @@
+"""Times the fused bf16 attention kernels at the bench shape (B=32, T=249, 12 heads x 64).
+usage: python tools/attn_bench.py [B] [T] [nh]"""
+import os
+import sys
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
+from wav2vec2forbrain_amd import functional as Fn
+
+
+def timeit(f, n=10):
+    for _ in range(2):
+        f()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(n):
+        f()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / n * 1e3
+
+
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
+T = int(sys.argv[2]) if len(sys.argv) > 2 else 249
+nh = int(sys.argv[3]) if len(sys.argv) > 3 else 12
+dh = 64
+q16 = (torch.randn(B * T, 3 * nh * dh, device="cuda") * 0.5).to(torch.bfloat16)
+dO = torch.randn(B * T, nh * dh, device="cuda").to(torch.bfloat16)
+fl = 4.0 * B * nh * T * T * dh
+for p in (0.0, 0.1):
+    O16, lse2 = Fn._attn16_fwd(q16, B, T, nh, dh, p, 5)
+    tf = timeit(lambda: Fn._attn16_fwd(q16, B, T, nh, dh, p, 5))
+    tb = timeit(lambda: Fn._attn16_bwd(q16, dO, lse2, B, T, nh, dh, p, 5))
+    print(f"attn16 B={B} T={T} nh={nh} p={p}: fwd {tf:.1f} us ({fl / tf / 1e6:.0f} TFLOP/s), "
+          f"bwd {tb:.1f} us ({2.5 * fl / tb / 1e6:.0f} TFLOP/s)", flush=True)

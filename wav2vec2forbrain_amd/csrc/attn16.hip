@@ -1,0 +1,429 @@
+// Fused bf16-MFMA self-attention (forward + backward) for the w2v / Conformer encoder layers:
+// softmax(Q K^T * scale) -> dropout -> @ V, no mask (reference: HF Wav2Vec2Attention / eager
+// attention, TF w2v:438-463,529-545; Conformer TF conf:458-470). bf16 precision mode only.
+//
+// T' (= 249 frames at the 1024-bin windows) <= 256 and head size 64, so one (batch, head)'s whole
+// K and V fit in 64 KB of LDS: no online softmax is needed. Scores never touch HBM (the unfused
+// path writes and re-reads a (B, heads, T', T') fp32 tensor ~6 times per layer).
+//   fwd   (b, h, 64-query block): S^T = K Q^T (keys in registers, query on the lane), in-register
+//         softmax (2 cross-lane shuffles per reduction), O^T = V^T P^T with P^T taken straight
+//         from the accumulators as the B operand and V^T read by ds_read_b64_tr_b16.
+//         Saves lse2[b][h][q] = max + log2(sum) in the log2 domain.
+//   dQ    (b, h, 64-query block, launched first): S^T, dP^T recomputed from lse2 (no stored
+//         probabilities); delta = sum_key P_d dP_d; dQ^T += K^T dS^T.
+//   dK/dV (b, h, 64-key block): S, dP = dO V^T with the key on the lane; dV^T += dO^T P_d and
+//         dK^T += Q^T dS with the dQ pass's delta.
+// Dropout: keep(b, h, q, key) = b2p_keep(seed, ((b*nh + h)*T + q)*T + key) — the same mask the
+// unfused softmax kernel draws, so both paths agree element for element.
+#include "common.h"
+#include "../../include/b2p_hip.h"
+
+namespace {
+constexpr int DH = 64;     // head size
+constexpr int TMAX = 256;  // max sequence length (keys / queries)
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+constexpr float LOG2E = 1.4426950408889634f;
+
+// [256 rows][64 bf16] LDS image, 16-byte chunks XOR-swizzled by row (conflict-light row reads)
+__device__ __forceinline__ int img_off(int row, int col) {
+  return row * 128 + ((((col >> 3) ^ row) & 7) << 4) + ((col & 7) << 1);
+}
+// A/B fragment of v_mfma_f32_16x16x32_bf16 read along a row: 8 bf16 at (row, col..col+7)
+__device__ __forceinline__ bf16x8 row_frag(const char* img, int row, int col) {
+  return *reinterpret_cast<const bf16x8*>(img + img_off(row, col));
+}
+// transposed fragment: element q (0..3) = img[r0 + q][c0 + lane%16] via ds_read_b64_tr_b16, for
+// the two 4-row blocks r0 and r1 (elements 0..3 and 4..7)
+__device__ __forceinline__ bf16x8 tr_frag(const char* img, int r0, int r1, int c0, int li) {
+  const int q = li >> 2, p = li & 3;
+  s16x4 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + img_off(r0 + q, c0 + 4 * p)));
+  s16x4 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(img + img_off(r1 + q, c0 + 4 * p)));
+  typedef short s16x8 __attribute__((ext_vector_type(8)));
+  s16x8 v = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+__device__ __forceinline__ bf16x8 pack_acc(const f32x4& a, const f32x4& b) {
+  bf16x8 r = {(__bf16)a[0], (__bf16)a[1], (__bf16)a[2], (__bf16)a[3],
+              (__bf16)b[0], (__bf16)b[1], (__bf16)b[2], (__bf16)b[3]};
+  return r;
+}
+__device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Load rows [0, 256) of a head slice (64 bf16 at column `col` of a row-major [B*T][ld] bf16
+// matrix) into an LDS image; rows >= T are zero. 256 threads, 8 chunks of 16 B each.
+__device__ __forceinline__ void load_image(char* img, const uint16_t* base, int64_t row0, int T, int64_t ld, int col,
+                                           int tid) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int idx = tid + 256 * k;
+    const int r = idx >> 3, c = idx & 7;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (r < T) v = *reinterpret_cast<const uint4*>(base + (row0 + r) * ld + col + 8 * c);
+    *reinterpret_cast<uint4*>(img + r * 128 + (((c ^ r) & 7) << 4)) = v;
+  }
+}
+__device__ __forceinline__ bf16x8 gload8(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+__device__ __forceinline__ void store_out(float* o32, uint16_t* o16, int64_t off, const f32x4& v, float s) {
+  const float4 f = make_float4(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
+  if (o32) *reinterpret_cast<float4*>(o32 + off) = f;
+  if (o16) *reinterpret_cast<uint2*>(o16 + off) = b2p_pack_bf16x4(f);
+}
+
+// XCD-aware block mapping: the hardware deals consecutive workgroups round-robin over the 8 XCDs
+// (private L2 each); remap so the blocks of one (batch, head) — which all stage the same K/V (or
+// Q/dO) — run on ONE XCD and hit its L2 instead of the Infinity Cache. Needs the block count to be
+// a multiple of 8 (else identity).
+__device__ __forceinline__ void block_coords(int& xb, int& h, int& b) {
+  const int nx = gridDim.x, ny = gridDim.y;
+  const int total = nx * ny * gridDim.z;
+  int L = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
+  if ((total & 7) == 0) L = (L & 7) * (total >> 3) + (L >> 3);
+  xb = L % nx;
+  h = (L / nx) % ny;
+  b = L / (nx * ny);
+}
+
+struct DropCfg {
+  uint64_t seed;
+  uint32_t thr;
+  float scale;   // 1 / (1 - p)
+};
+template <bool DROP>
+__device__ __forceinline__ float keep_scale(const DropCfg& dc, uint64_t idx) {
+  if (!DROP) return 1.f;
+  return b2p_keep(dc.seed, idx, dc.thr) ? dc.scale : 0.f;
+}
+
+// ------------------------------------------------------------------------------------------ forward
+// qkv16 [B*T][3*D] bf16 (q | k | v, head-major inside each); O16 [B*T][D] bf16; lse2 [B][nh][T]
+template <bool DROP>
+__global__ void __launch_bounds__(256) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
+                                                    float* __restrict__ lse2, int T, int nh, float scale, DropCfg dc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kimg = smem;
+  char* Vimg = smem + TMAX * 128;
+  int qb, h, b;
+  block_coords(qb, h, b);
+  const int D = nh * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
+  const int64_t row0 = (int64_t)b * T;
+  load_image(Kimg, qkv, row0, T, ld, D + h * DH, tid);
+  load_image(Vimg, qkv, row0, T, ld, 2 * D + h * DH, tid);
+  const int q = qb * 64 + w * 16 + lr;
+  const bool qok = q < T;
+  bf16x8 qf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    qf[ks] = bf16x8{};
+    if (qok) qf[ks] = gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g);
+  }
+  __syncthreads();
+
+  // S^T: tile kt = keys kt*16 + 4g + i (registers) x query q (lane)
+  f32x4 s[16];
+  const float c2 = scale * LOG2E;
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt) {
+    s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) s[kt] = mfma(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], s[kt]);
+  }
+  float m = -INFINITY;
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = kt * 16 + 4 * g + i;
+      const float v = key < T ? s[kt][i] * c2 : -INFINITY;
+      s[kt][i] = v;
+      m = fmaxf(m, v);
+    }
+  m = fmaxf(m, __shfl_xor(m, 16, 64));
+  m = fmaxf(m, __shfl_xor(m, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float e = exp2_fast(s[kt][i] - m);
+      s[kt][i] = e;
+      sum += e;
+    }
+  sum += __shfl_xor(sum, 16, 64);
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.f / sum;
+  const uint64_t rowidx = (((uint64_t)b * nh + h) * T + (qok ? q : 0)) * (uint64_t)T;
+  // O^T (d x q) = V^T (d x keys) . P_d^T (keys x q), 32 keys per k-step: normalisation and dropout
+  // of a k-step's probabilities are interleaved with its MFMAs (keeps the mask math off the
+  // register peak)
+  f32x4 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = (2 * c + half) * 16 + 4 * g + i;
+        s[2 * c + half][i] *= inv * (key < T ? keep_scale<DROP>(dc, rowidx + key) : 0.f);
+      }
+    const bf16x8 bp = pack_acc(s[2 * c], s[2 * c + 1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      o[dt] = mfma(tr_frag(Vimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, o[dt]);
+  }
+  const int64_t orow = (row0 + q) * D + h * DH;
+  if (qok) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) store_out(nullptr, O16, orow + dt * 16 + 4 * g, o[dt], 1.f);
+  }
+  if (qok && g == 0) lse2[((int64_t)b * nh + h) * T + q] = m + __log2f(sum);
+}
+
+// ------------------------------------------------------------------------------------ backward dK dV
+// dO16 [B*T][D] bf16; delta [B][nh][T] from the dQ kernel; writes dK, dV into dqkv (fp32 and/or
+// bf16) columns [D + h*64, ...) and [2D + h*64, ...).
+template <bool DROP>
+__global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restrict__ qkv, const float* __restrict__ delta,
+                                                        const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
+                                                        float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
+                                                        int nh, float scale, DropCfg dc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Qimg = smem;
+  char* dOimg = smem + TMAX * 128;
+  float* lse_s = reinterpret_cast<float*>(smem + 2 * TMAX * 128);
+  float* del_s = lse_s + TMAX;
+  int kb, h, b;
+  block_coords(kb, h, b);
+  const int D = nh * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
+  const int64_t row0 = (int64_t)b * T;
+  load_image(Qimg, qkv, row0, T, ld, h * DH, tid);
+  load_image(dOimg, dO16, row0, T, D, h * DH, tid);
+  {
+    const int qq = tid;   // one thread per query row: row constants lse2 and delta (from the dQ pass)
+    const int64_t o = ((int64_t)b * nh + h) * T + qq;
+    del_s[qq] = qq < T ? delta[o] : 0.f;
+    lse_s[qq] = qq < T ? lse2[o] : 0.f;
+  }
+  const int key = kb * 64 + w * 16 + lr;
+  const bool kok = key < T;
+  bf16x8 kf[2], vf[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    kf[ks] = vf[ks] = bf16x8{};
+    if (kok) {
+      kf[ks] = gload8(qkv + (row0 + key) * ld + D + h * DH + 32 * ks + 8 * g);
+      vf[ks] = gload8(qkv + (row0 + key) * ld + 2 * D + h * DH + 32 * ks + 8 * g);
+    }
+  }
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  const uint64_t bh = (uint64_t)b * nh + h;
+  f32x4 dv[4], dk[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dv[dt] = dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nchunk = (T + 31) >> 5;
+  for (int c = 0; c < nchunk; ++c) {
+    f32x4 pd[2], ds[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int qt = 2 * c + half;
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        sv = mfma(row_frag(Qimg, qt * 16 + lr, 32 * ks + 8 * g), kf[ks], sv);
+        dp = mfma(row_frag(dOimg, qt * 16 + lr, 32 * ks + 8 * g), vf[ks], dp);
+      }
+      // rows q = qt*16 + 4g + i, column key
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int qq = qt * 16 + 4 * g + i;
+        const bool ok = kok && qq < T;
+        const float p = ok ? exp2_fast(sv[i] * c2 - lse_s[qq]) : 0.f;
+        const float ksc = ok ? keep_scale<DROP>(dc, (bh * T + qq) * (uint64_t)T + key) : 0.f;
+        pd[half][i] = p * ksc;
+        ds[half][i] = p * (dp[i] * ksc - del_s[qq]);
+      }
+    }
+    const bf16x8 bp = pack_acc(pd[0], pd[1]), bs = pack_acc(ds[0], ds[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      dv[dt] = mfma(tr_frag(dOimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, dv[dt]);
+      dk[dt] = mfma(tr_frag(Qimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dk[dt]);
+    }
+  }
+  if (kok) {
+    const int64_t r = (row0 + key) * ld + h * DH;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      store_out(dqkv, dqkv16, r + D + dt * 16 + 4 * g, dk[dt], scale);
+      store_out(dqkv, dqkv16, r + 2 * D + dt * 16 + 4 * g, dv[dt], 1.f);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------------------- backward dQ
+// Runs BEFORE the dK/dV kernel: delta[q] = sum_key P_d dP_d is formed here from the very P and dP
+// the kernel recomputes (not as dO . O from the rounded bf16 O), so sum_key dS = 0 holds to fp32
+// rounding — otherwise the residual feeds a systematic, Q-correlated error into dK. Pass 1 keeps
+// P and dP*keep in registers, pass 2 forms dS and dQ^T += K^T dS^T.
+template <bool DROP>
+__global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restrict__ qkv, float* __restrict__ delta,
+                                                       const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
+                                                       float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
+                                                       int nh, float scale, DropCfg dc) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* Kimg = smem;
+  char* Vimg = smem + TMAX * 128;
+  int qb, h, b;
+  block_coords(qb, h, b);
+  const int D = nh * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
+  const int64_t row0 = (int64_t)b * T;
+  load_image(Kimg, qkv, row0, T, ld, D + h * DH, tid);
+  load_image(Vimg, qkv, row0, T, ld, 2 * D + h * DH, tid);
+  const int q = qb * 64 + w * 16 + lr;
+  const bool qok = q < T;
+  bf16x8 qf[2], df[2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks) {
+    qf[ks] = df[ks] = bf16x8{};
+    if (qok) {
+      qf[ks] = gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g);
+      df[ks] = gload8(dO16 + (row0 + q) * D + h * DH + 32 * ks + 8 * g);
+    }
+  }
+  const int64_t rowc = ((int64_t)b * nh + h) * T + (qok ? q : 0);
+  const float ls = qok ? lse2[rowc] : 0.f;
+  __syncthreads();
+  const float c2 = scale * LOG2E;
+  const uint64_t rowidx = (uint64_t)rowc * (uint64_t)T;
+  f32x4 P[16], PD[16];
+  float dl = 0.f;
+#pragma unroll
+  for (int kt = 0; kt < 16; ++kt) {
+    f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      sv = mfma(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], sv);
+      dp = mfma(row_frag(Vimg, kt * 16 + lr, 32 * ks + 8 * g), df[ks], dp);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int key = kt * 16 + 4 * g + i;
+      const bool ok = qok && key < T;
+      const float p = ok ? exp2_fast(sv[i] * c2 - ls) : 0.f;
+      const float pd = ok ? dp[i] * keep_scale<DROP>(dc, rowidx + key) : 0.f;
+      P[kt][i] = p;
+      PD[kt][i] = pd;
+      dl += p * pd;
+    }
+  }
+  dl += __shfl_xor(dl, 16, 64);
+  dl += __shfl_xor(dl, 32, 64);
+  if (qok && g == 0) delta[rowc] = dl;
+  f32x4 dq[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int c = 0; c < 8; ++c) {
+    f32x4 ds[2];
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ds[half][i] = P[2 * c + half][i] * (PD[2 * c + half][i] - dl);
+    const bf16x8 bs = pack_acc(ds[0], ds[1]);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+      dq[dt] = mfma(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dq[dt]);
+  }
+  if (qok) {
+    const int64_t r = (row0 + q) * ld + h * DH;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) store_out(dqkv, dqkv16, r + dt * 16 + 4 * g, dq[dt], scale);
+  }
+}
+
+DropCfg drop_cfg(float p, uint64_t seed) {
+  DropCfg d;
+  d.seed = seed;
+  d.thr = b2p_dropout_threshold(p);
+  d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  return d;
+}
+constexpr size_t FWD_LDS = 2 * TMAX * 128;
+constexpr size_t BWD_LDS = 2 * TMAX * 128 + 2 * TMAX * 4;
+
+template <typename K>
+int set_lds(K kern, size_t bytes) {
+  B2P_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+  return 0;
+}
+int init_attrs() {
+  static int done = -1;
+  if (done >= 0) return done;
+  int rc = 0;
+  rc |= set_lds(attn16_fwd_k<false>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<true>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<false>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<true>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<false>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<true>, FWD_LDS);
+  done = rc;
+  return rc;
+}
+}  // namespace
+
+extern "C" int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
+                              int64_t dh, float scale, float drop_p, uint64_t drop_seed, b2p_stream_t stream) {
+  B2P_CHECK_ARG(qkv16 && O16 && lse2, "attn16_fwd: NULL pointer");
+  B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_fwd: needs head size 64 and T <= 256");
+  if (B <= 0) return 0;
+  if (init_attrs()) return 2;
+  dim3 grid((unsigned)((T + 63) / 64), (unsigned)nh, (unsigned)B);
+  const DropCfg dc = drop_cfg(drop_p, drop_seed);
+  if (drop_p > 0.f)
+    hipLaunchKernelGGL(attn16_fwd_k<true>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
+                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc);
+  else
+    hipLaunchKernelGGL(attn16_fwd_k<false>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
+                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws, float* dqkv,
+                              void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh, float scale, float drop_p,
+                              uint64_t drop_seed, b2p_stream_t stream) {
+  B2P_CHECK_ARG(qkv16 && dO16 && lse2 && delta_ws && (dqkv || dqkv16), "attn16_bwd: NULL pointer");
+  B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_bwd: needs head size 64 and T <= 256");
+  if (B <= 0) return 0;
+  if (init_attrs()) return 2;
+  dim3 grid((unsigned)((T + 63) / 64), (unsigned)nh, (unsigned)B);
+  const DropCfg dc = drop_cfg(drop_p, drop_seed);
+  hipStream_t st = (hipStream_t)stream;
+  const uint16_t *q = (const uint16_t*)qkv16, *d = (const uint16_t*)dO16;
+  uint16_t* d16 = (uint16_t*)dqkv16;
+  if (drop_p > 0.f) {
+    hipLaunchKernelGGL(attn16_bwd_dq_k<true>, grid, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
+                       (int)nh, scale, dc);
+    hipLaunchKernelGGL(attn16_bwd_dkv_k<true>, grid, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
+                       (int)nh, scale, dc);
+  } else {
+    hipLaunchKernelGGL(attn16_bwd_dq_k<false>, grid, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
+                       (int)nh, scale, dc);
+    hipLaunchKernelGGL(attn16_bwd_dkv_k<false>, grid, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
+                       (int)nh, scale, dc);
+  }
+  B2P_CHECK_LAUNCH();
+  return 0;
+}

@@ -66,14 +66,21 @@ __device__ __forceinline__ float b2p_silu_grad(float x) {
   return s * (1.0f + x * (1.0f - s));
 }
 
-// Counter-based dropout mask (stateless, so backward regenerates the forward
-// mask from (seed, element index) instead of storing it). splitmix64 finaliser.
+// Counter-based dropout mask (stateless, so backward regenerates the forward mask from
+// (seed, element index) instead of storing it). lowbias32 (a 32-bit bijection with two
+// multiplies) applied twice over the index, keyed by the seed: ~4 v_mul per element instead of
+// splitmix64's 64-bit multiplies (the attention kernels draw ~24M masks per layer and pass).
+__device__ __forceinline__ uint32_t b2p_mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
 __device__ __forceinline__ uint32_t b2p_hash(uint64_t seed, uint64_t idx) {
-  uint64_t z = seed + 0x9E3779B97F4A7C15ull * (idx + 1);
-  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-  z = z ^ (z >> 31);
-  return (uint32_t)(z >> 32);
+  const uint32_t k = (uint32_t)seed ^ b2p_mix32((uint32_t)(seed >> 32) + 0x9E3779B9u);   // per-launch key
+  return b2p_mix32(b2p_mix32((uint32_t)idx ^ k) + (uint32_t)(idx >> 32) * 0x85EBCA6Bu + k);
 }
 // keep-probability threshold: keep iff hash >= thr, thr = round(p * 2^32)
 __device__ __forceinline__ bool b2p_keep(uint64_t seed, uint64_t idx, uint32_t thr) {

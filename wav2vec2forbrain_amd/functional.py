@@ -801,6 +801,32 @@ def _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seed, want16=False):
     return dqkv
 
 
+def attn16_ok(T, dh) -> bool:
+    """The fused bf16 attention kernels (csrc/attn16.hip) cover head size 64 and T' <= 256."""
+    return dh == 64 and 0 < T <= 256
+
+
+def _attn16_fwd(qkv16, B, T, nh, dh, p_attn, seed):
+    """qkv16 (B*T, 3D) bf16 -> O16 (B*T, D) bf16, lse2 (B, nh, T) f32 (fused, scores stay on-chip)."""
+    dev = qkv16.device
+    O16 = torch.empty(B * T, nh * dh, device=dev, dtype=BF16)
+    lse2 = torch.empty(B, nh, T, device=dev)
+    _lib.call("b2p_attn16_fwd", _p(qkv16), _p(O16), _p(lse2), B, T, nh, dh, float(dh ** -0.5), float(p_attn),
+              seed, _st())
+    return O16, lse2
+
+
+def _attn16_bwd(qkv16, dO16, lse2, B, T, nh, dh, p_attn, seed, want32=True):
+    """-> dqkv (B*T, 3D) f32 (or None) and its bf16 copy."""
+    dev = qkv16.device
+    dqkv = torch.empty(B * T, 3 * nh * dh, device=dev) if want32 else None
+    d16 = torch.empty(B * T, 3 * nh * dh, device=dev, dtype=BF16)
+    delta = torch.empty(B, nh, T, device=dev)
+    _lib.call("b2p_attn16_bwd", _p(qkv16), _p(dO16), _p(lse2), _p(delta), _p(dqkv), _p(d16), B, T, nh, dh,
+              float(dh ** -0.5), float(p_attn), seed, _st())
+    return dqkv, d16
+
+
 # =====================================================================================
 # post-LN transformer encoder layer (Wav2Vec2EncoderLayer)
 # =====================================================================================
@@ -920,10 +946,17 @@ class _EncoderLayer16(torch.autograd.Function):
         x16 = to16(x).view(NT, D)
         wqkv16 = weight16(wq, wk, wv)
         bqkv = bias_cat(bq, bk, bv) if any(b is not None for b in (bq, bk, bv)) else None
-        qkv = torch.empty(NT, 3 * D, device=dev)
-        gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), qkv, 3 * D, bias=bqkv)
-        P, Pd, _O, O16 = _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seeds[0], want16=True)
-        del _O
+        fused = attn16_ok(T, dh)
+        if fused:
+            qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16)     # bf16 only: attention operand
+            gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), None, 3 * D, bias=bqkv, C16=qkv)
+            O16, P = _attn16_fwd(qkv, B, T, nh, dh, p_attn, seeds[0])   # P slot holds lse2
+            Pd = None
+        else:
+            qkv = torch.empty(NT, 3 * D, device=dev)
+            gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), qkv, 3 * D, bias=bqkv)
+            P, Pd, _O, O16 = _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seeds[0], want16=True)
+            del _O
         # y1 = x + dropout(O Wo^T + bo)
         wo16 = weight16(wo)
         y1 = torch.empty(NT, D, device=dev)
@@ -945,6 +978,7 @@ class _EncoderLayer16(torch.autograd.Function):
                               wq, wk, wv, wo, g1, w1, w2, g2)
         ctx.cfg = cfg
         ctx.shape = (B, T, D)
+        ctx.fused = fused
         ctx.has_b = [b is not None for b in (bq, bk, bv, bo, b1, b2)]
         res = out.view(B, T, D)
         attach16(res, out16.view(B, T, D))
@@ -998,10 +1032,16 @@ class _EncoderLayer16(torch.autograd.Function):
         if ng[8]:
             dwo = torch.empty_like(wo)
             gemm(D, D, NT, op(dz1_16, 0, D, False), op(O16, 0, D, False), dwo, D)
-        dO = torch.empty(NT, D, device=dev)
-        gemm(NT, D, D, op(dz1_16, 0, D, True), op(wo16, 0, D, False), dO, D)
-        dqkv, dqkv16 = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seeds[0], want16=True)
-        del dO
+        if ctx.fused:
+            dO16 = torch.empty(NT, D, device=dev, dtype=BF16)
+            gemm(NT, D, D, op(dz1_16, 0, D, True), op(wo16, 0, D, False), None, D, C16=dO16)
+            dqkv, dqkv16 = _attn16_bwd(qkv, dO16, P, B, T, nh, dh, p_attn, seeds[0])
+            del dO16
+        else:
+            dO = torch.empty(NT, D, device=dev)
+            gemm(NT, D, D, op(dz1_16, 0, D, True), op(wo16, 0, D, False), dO, D)
+            dqkv, dqkv16 = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seeds[0], want16=True)
+            del dO
         grads_w = [None] * 6
         if ng[2] or ng[4] or ng[6]:
             dwqkv = torch.empty(3 * D, D, device=dev)
