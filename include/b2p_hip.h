@@ -90,6 +90,11 @@ typedef struct {
   int64_t ldr, rbs1, rbs2;
   uint16_t* C16;              /* optional bf16 copy of the final value (strides of C); C may be
                                * NULL when only the bf16 copy is wanted (then beta must be 0)    */
+  /* bf16 LDS-DMA kernel only (both operands bf16), nz1*nz2 == 1, no split-K:                   */
+  uint16_t* pre16;            /* optional bf16 pre-activation store (instead of pre_out)       */
+  const uint16_t* aux16;      /* act_bwd operand in bf16 (instead of aux; strides of aux)      */
+  float* colsum_part;         /* optional: per-128-row-tile column sums of the final value,
+                               * [ceil(M/128)][N] floats (fused bias gradient; b2p_colsum_parts) */
 } b2p_epilogue;
 
 typedef struct {
@@ -120,6 +125,10 @@ int b2p_colsum(const float* X, int64_t M, int64_t N, int64_t ld, float* out, int
 int b2p_colsum_batched(const float* X, const float* Y, int64_t batch, int64_t M, int64_t N, int64_t ld,
                        int64_t bstride, int mode, float* out, int accumulate, float* partial,
                        b2p_stream_t stream);
+
+/* out[n] (+)= sum_t part[t][n] over ntiles rows of a b2p_epilogue.colsum_part buffer */
+int b2p_colsum_parts(const float* part, int64_t ntiles, int64_t N, float* out, int accumulate,
+                     b2p_stream_t stream);
 
 /* dropout (forward and backward use the same mask): y = x * keep(seed, i) / (1-p) */
 int b2p_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, b2p_stream_t stream);
@@ -181,6 +190,11 @@ int b2p_day_reduce(const float* per_sample, const int64_t* day_idx, int64_t B, i
                    int64_t elems, float* out, b2p_stream_t stream);
 
 /* ------------------------------------------------------------------ layout transforms */
+/* Unfold((k,1), stride) of x (B, L, C) materialised tap-major in bf16: U[(b,t)][tap*C + c] =
+ * bf16(x[b][t*stride + tap][c]), T = (L-k)/stride + 1 (b2p2t_model.py:108-113,162-167). bf16
+ * mode's GRU layer-0 projection and weight-gradient operand. */
+int b2p_unfold16(const float* x, uint16_t* U, int64_t B, int64_t L, int64_t C, int64_t k,
+                 int64_t stride, b2p_stream_t stream);
 /* out[o][tap*I + i] = in[o][i*ntaps + tap]   (conv weight (O, I, taps) -> tap-major GEMM B)
  * inverse=1 does the opposite mapping; flip=1 reads tap (ntaps-1-tap). */
 int b2p_conv_weight_permute(const float* in, float* out, int64_t O, int64_t I, int64_t ntaps,

@@ -267,3 +267,34 @@ def test_bf16_implicit_unfold_view():
         out = torch.empty(B * T, N, device="cuda")
         Fn.gemm(B * T, N, k * C, Fn.conv_op(x, 0, C, T, L, s, 0, C, L * C, True), Fn.op(wp16, 0, k * C, True), out, N)
     _close16(out, (u.view(B * T, -1).double() @ w.to(torch.bfloat16).double().t()).float())
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 264, 96), (7968 // 8, 3072 // 4, 768 // 4), (1, 8, 8)])
+def test_bf16_epilogue_pre16_aux16_colsum(M, N, K):
+    """bf16-operand kernel epilogue extensions: bf16 pre-activation store (pre16), act' operand in
+    bf16 (aux16) and the fused per-tile column sums (colsum_part -> b2p_colsum_parts) used for the
+    FFN bias gradient, vs torch fp32 on the same bf16-rounded operands."""
+    Fn = _fn()
+    torch.manual_seed(3)
+    a = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+    w = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+    bias = torch.randn(N, device="cuda")
+    ref_pre = a.float() @ w.float().t() + bias
+    pre16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    out16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), None, N, bias=bias, pre16=pre16,
+            act=Fn.ACT["gelu"], C16=out16)
+    _close(pre16.float(), ref_pre, "bf16")
+    _close(out16.float(), F.gelu(ref_pre), "bf16")
+    # backward-style: C16 = (a w^T) * gelu'(aux16), colsum of the fp32 values
+    g = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    parts = Fn.colsum_parts_buf(M, N, "cuda")
+    Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), None, N, act_bwd=Fn.ACT["gelu"], aux16=pre16,
+            C16=g, colsum_part=parts)
+    x = pre16.float().requires_grad_(True)
+    gl = torch.autograd.grad(F.gelu(x).sum(), x)[0]
+    ref = (a.float() @ w.float().t()) * gl
+    _close(g.float(), ref, "bf16")
+    cs = Fn.colsum_from_parts(parts, torch.empty(N, device="cuda"))
+    ref_cs = ref.sum(0)
+    assert float((cs - ref_cs).abs().max()) <= 1e-3 * float(ref.abs().sum(0).max()) + 1e-4

@@ -1,3 +1,2 @@
 set -e
-timeout -k 5 120 python tools/attn_bench.py
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "attention" 2>&1 | tail -3
+bash tools/gpu_check.sh epi16 "gemm or gru or encoder_layer or step_matches or full_size or reduce_loss or attention"

@@ -43,6 +43,7 @@ class Epilogue(ctypes.Structure):
         ("act", c_i32), ("act_bwd", c_i32), ("aux", c_p), ("ldaux", c_i64), ("abs1", c_i64),
         ("abs2", c_i64), ("drop_p", c_f32), ("_pad0", c_i32), ("drop_seed", c_u64),
         ("residual", c_p), ("ldr", c_i64), ("rbs1", c_i64), ("rbs2", c_i64), ("C16", c_p),
+        ("pre16", c_p), ("aux16", c_p), ("colsum_part", c_p),
     ]
 
 
@@ -66,6 +67,7 @@ _SIGS = {
     "b2p_colsum_workspace": (c_i64, [c_i64, c_i64]),
     "b2p_colsum": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_p]),
     "b2p_colsum_batched": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32, c_p, c_p]),
+    "b2p_colsum_parts": (c_i32, [c_p, c_i64, c_i64, c_p, c_i32, c_p]),
     "b2p_dropout": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_p]),
     "b2p_layernorm_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_u64, c_p]),
     "b2p_layernorm_bwd_workspace": (c_i64, [c_i64, c_i64]),
@@ -81,6 +83,7 @@ _SIGS = {
     "b2p_gauss_smooth": (c_i32, [c_p, c_p, c_i32, c_p, c_i64, c_i64, c_i64, c_p]),
     "b2p_unfold_col2im": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i32, c_i32, c_p]),
     "b2p_day_reduce": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_p, c_p]),
+    "b2p_unfold16": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_conv_weight_permute": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_conv_weight_transpose_flip": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_weight_norm_workspace": (c_i64, [c_i64, c_i64, c_i64]),

@@ -61,6 +61,16 @@ int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_
   return 0;
 }
 
+extern "C" int b2p_colsum_parts(const float* part, int64_t ntiles, int64_t N, float* out, int accumulate,
+                                b2p_stream_t stream) {
+  B2P_CHECK_ARG(part && out, "colsum_parts: NULL pointer");
+  if (N <= 0 || ntiles <= 0) return 0;
+  dim3 g2((unsigned)((N + 255) / 256), 1);
+  hipLaunchKernelGGL(colsum_p2, g2, dim3(256), 0, (hipStream_t)stream, part, (int)ntiles, N, out, accumulate);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 namespace {
 
 // ------------------------------------------------------------------ dropout
@@ -534,6 +544,33 @@ extern "C" int b2p_cast_bf16(const float* x, uint16_t* y, int64_t n, b2p_stream_
   if (n <= 0) return 0;
   const int64_t n4 = n / 4;
   hipLaunchKernelGGL(cast_bf16_k, dim3(nblocks(n4 + 1)), dim3(256), 0, (hipStream_t)stream, x, y, n4, n);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+// Unfold((k, 1), stride) of a (B, L, C) tensor, tap-major (feature tap*C + c), materialised as
+// bf16 rows of k*C: row (b, t) is the contiguous slab x[b][t*stride .. t*stride+k)[.] cast to bf16
+// (the GRU layer-0 weight-gradient GEMM operand; b2p2t_model.py:108-113,162-167).
+__global__ void unfold16_k(const float* __restrict__ x, uint16_t* __restrict__ u, int64_t n4, int64_t L, int64_t C,
+                           int64_t T, int64_t row4, int64_t stride) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const int64_t row = i / row4, w = i - row * row4;
+  const int64_t b = row / T, t = row - b * T;
+  const float4 v = reinterpret_cast<const float4*>(x + (b * L + t * stride) * C)[w];
+  reinterpret_cast<uint2*>(u)[i] = b2p_pack_bf16x4(v);
+}
+
+extern "C" int b2p_unfold16(const float* x, uint16_t* u, int64_t B, int64_t L, int64_t C, int64_t k, int64_t stride,
+                            b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && u, "unfold16: NULL pointer");
+  B2P_CHECK_ARG(C % 4 == 0 && ((uintptr_t)x & 15u) == 0 && ((uintptr_t)u & 7u) == 0, "unfold16: alignment");
+  B2P_CHECK_ARG(L >= k && stride > 0, "unfold16: window longer than the sequence");
+  const int64_t T = (L - k) / stride + 1;
+  const int64_t n4 = B * T * k * C / 4;
+  if (n4 <= 0) return 0;
+  hipLaunchKernelGGL(unfold16_k, dim3(nblocks(n4)), dim3(256), 0, (hipStream_t)stream, x, u, n4, L, C, T, k * C / 4,
+                     stride);
   B2P_CHECK_LAUNCH();
   return 0;
 }

@@ -255,6 +255,7 @@ __global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(cons
   float* Cs = reinterpret_cast<float*>(smem);
   float* slab = ks > 1 ? d.workspace + ((int64_t)z * ks + ksl) * (int64_t)M * N : nullptr;
   const int cg = tid & 31, rbase = tid >> 5;
+  float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);   // fused bias-gradient column sums (colsum_part)
 #pragma clang loop unroll(full)
   for (int half = 0; half < 2; ++half) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -286,8 +287,21 @@ __global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(cons
           }
         }
       } else {
-        epilogue_store4(ea, z, z1, z2, m, n, v);
+        const float4 f = epilogue_store4(ea, z, z1, z2, m, n, v);
+        csum.x += f.x; csum.y += f.y; csum.z += f.z; csum.w += f.w;
       }
+    }
+  }
+  if (ea.e.colsum_part) {
+    // the 8 threads of a column group (rbase = 0..7) add their 16 rows: one 128-row tile partial
+    __syncthreads();
+    *reinterpret_cast<float4*>(Cs + rbase * CS_LD + 4 * cg) = csum;
+    __syncthreads();
+    if (tid < TILE && n0 + tid < N) {
+      float sacc = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) sacc += Cs[r * CS_LD + tid];
+      ea.e.colsum_part[(int64_t)tm * N + n0 + tid] = sacc;
     }
   }
 }
@@ -324,6 +338,10 @@ static void launch16(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st, 
 
 int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   const EpiArgs ea = make_epi_args(d);
+  if ((d.ep.colsum_part || d.ep.pre16 || d.ep.aux16) && !ea.vec4) {
+    b2p_set_error("gemm16: colsum_part / pre16 / aux16 need 16-B aligned C-shaped tensors and N %% 4 == 0");
+    return 1;
+  }
   const int ks = d.ksplit > 1 ? d.ksplit : 1;
   const int tm = (int)((d.M + TILE - 1) / TILE), tn = (int)((d.N + TILE - 1) / TILE);
   const int64_t nwg = (int64_t)tm * tn * d.nz1 * d.nz2 * ks;

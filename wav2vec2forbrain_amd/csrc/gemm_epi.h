@@ -53,14 +53,15 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, 
 }
 
 // Four consecutive columns n .. n+3 of row m (n % 4 == 0), vectorised when ea.vec4 is set.
-__device__ __forceinline__ void epilogue_store4(const EpiArgs& a, int z, int z1, int z2, int m, int n, float4 acc) {
-  if (m >= a.M || n >= a.N) return;
+// Returns the final values (0 outside the matrix) for the fused column sums.
+__device__ __forceinline__ float4 epilogue_store4(const EpiArgs& a, int z, int z1, int z2, int m, int n, float4 acc) {
+  if (m >= a.M || n >= a.N) return make_float4(0.f, 0.f, 0.f, 0.f);
   if (!a.vec4 || n + 4 > a.N) {
     epilogue_store(a, z, z1, z2, m, n, acc.x);
     if (n + 1 < a.N) epilogue_store(a, z, z1, z2, m, n + 1, acc.y);
     if (n + 2 < a.N) epilogue_store(a, z, z1, z2, m, n + 2, acc.z);
     if (n + 3 < a.N) epilogue_store(a, z, z1, z2, m, n + 3, acc.w);
-    return;
+    return make_float4(0.f, 0.f, 0.f, 0.f);   // (colsum_part requires vec4, checked on the host)
   }
   const b2p_epilogue& e = a.e;
   const int64_t coff = (int64_t)z1 * e.cbs1 + (int64_t)z2 * e.cbs2 + (int64_t)m * e.ldc + n;
@@ -75,6 +76,7 @@ __device__ __forceinline__ void epilogue_store4(const EpiArgs& a, int z, int z1,
     v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
   }
   if (e.pre_out) *reinterpret_cast<float4*>(e.pre_out + coff) = make_float4(v[0], v[1], v[2], v[3]);
+  if (e.pre16) *reinterpret_cast<uint2*>(e.pre16 + coff) = b2p_pack_bf16x4(make_float4(v[0], v[1], v[2], v[3]));
   if (e.act != B2P_ACT_NONE) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], e.act);
@@ -85,8 +87,15 @@ __device__ __forceinline__ void epilogue_store4(const EpiArgs& a, int z, int z1,
     for (int q = 0; q < 4; ++q) v[q] = b2p_keep(e.drop_seed, idx + q, a.drop_thr) ? v[q] * a.drop_scale : 0.0f;
   }
   if (e.act_bwd != B2P_ACT_NONE) {
-    const float4 x = *reinterpret_cast<const float4*>(
-        e.aux + (int64_t)z1 * e.abs1 + (int64_t)z2 * e.abs2 + (int64_t)m * e.ldaux + n);
+    const int64_t ao = (int64_t)z1 * e.abs1 + (int64_t)z2 * e.abs2 + (int64_t)m * e.ldaux + n;
+    float4 x;
+    if (e.aux16) {
+      const uint2 h = *reinterpret_cast<const uint2*>(e.aux16 + ao);
+      x = make_float4(b2p_bf16_to_f32((uint16_t)(h.x & 0xffffu)), b2p_bf16_to_f32((uint16_t)(h.x >> 16)),
+                      b2p_bf16_to_f32((uint16_t)(h.y & 0xffffu)), b2p_bf16_to_f32((uint16_t)(h.y >> 16)));
+    } else {
+      x = *reinterpret_cast<const float4*>(e.aux + ao);
+    }
     v[0] *= act_grad(x.x, e.act_bwd); v[1] *= act_grad(x.y, e.act_bwd);
     v[2] *= act_grad(x.z, e.act_bwd); v[3] *= act_grad(x.w, e.act_bwd);
   }
@@ -101,6 +110,7 @@ __device__ __forceinline__ void epilogue_store4(const EpiArgs& a, int z, int z1,
     const uint32_t hi = (uint32_t)b2p_bf16_bits(v[2]) | ((uint32_t)b2p_bf16_bits(v[3]) << 16);
     *reinterpret_cast<uint2*>(e.C16 + coff) = make_uint2(lo, hi);
   }
+  return make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // C[z](m,n) = alpha * sum_s slab[z][s](m,n) + beta * C_old ; deterministic slice order
@@ -136,7 +146,9 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
   bool v = d.N % 4 == 0 && s4(e.ldc) && s4(e.cbs1) && s4(e.cbs2) && a16(e.C) && a16(e.pre_out) &&
            ((uintptr_t)e.C16 & 7u) == 0;
   if (e.bias) v = v && a16(e.bias) && s4(e.biasbs1);
-  if (e.act_bwd != B2P_ACT_NONE) v = v && a16(e.aux) && s4(e.ldaux) && s4(e.abs1) && s4(e.abs2);
+  if (e.act_bwd != B2P_ACT_NONE)
+    v = v && (e.aux16 ? ((uintptr_t)e.aux16 & 7u) == 0 : a16(e.aux)) && s4(e.ldaux) && s4(e.abs1) && s4(e.abs2);
+  if (e.pre16) v = v && ((uintptr_t)e.pre16 & 7u) == 0;
   if (e.residual) v = v && a16(e.residual) && s4(e.ldr) && s4(e.rbs1) && s4(e.rbs2);
   ea.vec4 = v ? 1 : 0;
   return ea;

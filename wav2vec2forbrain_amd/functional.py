@@ -135,7 +135,8 @@ def conv_op(t, off, ld, T_out, T_in, stride, pad, Cg, sample_stride, k_inner=Tru
 
 def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1, nz2=1, alpha=1.0,
          beta=0.0, bias=None, biasbs1=0, bias_gather=None, pre_out=None, act=0, act_bwd=0, aux=None, ldaux=0, abs1=0, abs2=0,
-         drop_p=0.0, seed=0, residual=None, r_off=0, ldr=0, rbs1=0, rbs2=0, timing=0, C16=None):
+         drop_p=0.0, seed=0, residual=None, r_off=0, ldr=0, rbs1=0, rbs2=0, timing=0, C16=None, pre16=None,
+         aux16=None, colsum_part=None):
     """C may be None when only the bf16 copy C16 (same strides) is wanted. Both operands bf16
     (Operand.dtype 1) selects the LDS-DMA kernel (gemm16.hip)."""
     d = GemmDesc()
@@ -159,12 +160,16 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     e.drop_seed = seed
     e.residual = _p(residual, r_off) if residual is not None else None
     e.ldr, e.rbs1, e.rbs2 = ldr or ldc, rbs1 or cbs1, rbs2 or cbs2
+    e.pre16 = _p(pre16, c_off) if pre16 is not None else None
+    e.aux16 = _p(aux16, c_off) if aux16 is not None else None
+    e.colsum_part = _p(colsum_part)
     d.ep = e
     d.precision = _prec()
     d.timing_family = timing or _GEMM_TIMING[0]
     d.flops = 2.0 * M * N * K * nz1 * nz2
     ws = None
-    plain = (bias is None and pre_out is None and act == 0 and act_bwd == 0 and drop_p == 0.0 and residual is None)
+    plain = (bias is None and pre_out is None and act == 0 and act_bwd == 0 and drop_p == 0.0 and residual is None
+             and colsum_part is None and pre16 is None)
     if plain and K >= 2048:
         b16 = A.dtype == 1
         bn = 64 if (N <= 64 and not b16) else 128
@@ -181,7 +186,17 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
                 d.ksplit, d.kchunk = ks, kchunk
                 d.workspace = ws.data_ptr()
                 d.workspace_floats = ws.numel()
+    if GEMM_LOG is not None:
+        GEMM_LOG.append(dict(M=M, N=N, K=K, nz=nz1 * nz2, a16=int(A.dtype), ak=int(A.inner_is_k), bk=int(B.inner_is_k),
+                             aconv=int(A.conv), bconv=int(B.conv), ksplit=int(d.ksplit),
+                             epi="".join(c for c, f in (("b", bias is not None), ("a", act != 0), ("g", act_bwd != 0),
+                                                        ("d", drop_p > 0), ("r", residual is not None),
+                                                        ("h", C16 is not None), ("f", C is not None)) if f)))
     _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
+
+
+# tools/gemm_census.py: when a list, every gemm() call appends its shape record
+GEMM_LOG = None
 
 
 def mm_nt(x, W, out, bias=None, act=0, pre_out=None, drop_p=0.0, seed=0, residual=None, alpha=1.0, beta=0.0,
@@ -216,6 +231,16 @@ _WS = {}
 def _colsum_ws(M, N, device):
     n = int(_lib.load().b2p_colsum_workspace(M, N))
     return torch.empty(max(n, 1), device=device, dtype=torch.float32)
+
+
+def colsum_parts_buf(M, N, device):
+    """Workspace for a GEMM epilogue's fused column sums (one row per 128-row tile)."""
+    return torch.empty(-(-M // 128), N, device=device)
+
+
+def colsum_from_parts(parts, out):
+    _lib.call("b2p_colsum_parts", _p(parts), parts.shape[0], parts.shape[1], _p(out), 0, _st())
+    return out
 
 
 def colsum(x2d_ptr_tensor, M, N, out, ld=None, accumulate=False):
@@ -492,12 +517,21 @@ class _GRULayer(torch.autograd.Function):
                 _lib.call("b2p_conv_weight_permute", _p(wih[d]), _p(wperm, d * G3 * IN), G3, C, ktaps, 0, _st())
             bias_cat = torch.cat([b if b is not None else torch.zeros(G3, device=dev) for b in bih]) \
                 if any(b is not None for b in bih) else None
-            A = conv_op(x, 0, C, T, L, stride, 0, C * ktaps, L * C, True)
-            A.conv_Cg = C  # inner j = tap*C + c
-            gemm(B * T, ndir * G3, IN, A, op(wperm, 0, IN, True), gi, ndir * G3, bias=bias_cat)
+            if bf16_mode():
+                # bf16 operands: the tap-major unfold materialised once in bf16 (it is also the
+                # weight-gradient operand) and a bf16 copy of the permuted weight
+                U16 = torch.empty(B * T, IN, device=dev, dtype=BF16)
+                _lib.call("b2p_unfold16", _p(x), _p(U16), B, L, C, ktaps, stride, _st())
+                wperm = cast16(wperm)
+                gemm(B * T, ndir * G3, IN, op(U16, 0, IN, True), op(wperm, 0, IN, True), gi, ndir * G3, bias=bias_cat)
+            else:
+                U16 = None
+                A = conv_op(x, 0, C, T, L, stride, 0, C * ktaps, L * C, True)
+                A.conv_Cg = C  # inner j = tap*C + c
+                gemm(B * T, ndir * G3, IN, A, op(wperm, 0, IN, True), gi, ndir * G3, bias=bias_cat)
         else:
             _chk(x, "gru.x")
-            wperm = None
+            wperm = U16 = None
             for d in range(ndir):
                 gemm(B * T, G3, IN, op(x, 0, IN, True), op(wih[d], 0, IN, True), gi, ndir * G3, c_off=d * G3,
                      bias=bih[d])
@@ -522,13 +556,13 @@ class _GRULayer(torch.autograd.Function):
             hL = None
             _lib.call("b2p_gru_fwd", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved), B, T, H, ndir,
                       _st())
-        ctx.save_for_backward(x, out, saved, whh_s, h0, wperm, hL, *wih)
+        ctx.save_for_backward(x, out, saved, whh_s, h0, wperm, hL, U16, *wih)
         ctx.meta = (unf_meta, H, ndir, B, T, IN, bih[0] is not None, bhh[0] is not None, use16)
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        x, out, saved, whh_s, h0, wperm, hL, *wih = ctx.saved_tensors
+        x, out, saved, whh_s, h0, wperm, hL, U16, *wih = ctx.saved_tensors
         unf_meta, H, ndir, B, T, IN, has_bih, has_bhh, use16 = ctx.meta
         dev = out.device
         dout = dout.contiguous()
@@ -572,17 +606,24 @@ class _GRULayer(torch.autograd.Function):
         if unf_meta is not None:
             ktaps, stride = unf_meta
             _, L, C = x.shape
+            dgi16 = cast16(dgi) if U16 is not None else None
             if any(ctx.needs_input_grad[5 + 4 * d] for d in range(ndir)):
                 dwp = torch.empty(ndir * G3, IN, device=dev)
-                Bop = conv_op(x, 0, C, T, L, stride, 0, C, L * C, False)
-                gemm(ndir * G3, IN, B * T, op(dgi, 0, ndir * G3, False), Bop, dwp, IN)
+                if U16 is not None:
+                    gemm(ndir * G3, IN, B * T, op(dgi16, 0, ndir * G3, False), op(U16, 0, IN, False), dwp, IN)
+                else:
+                    Bop = conv_op(x, 0, C, T, L, stride, 0, C, L * C, False)
+                    gemm(ndir * G3, IN, B * T, op(dgi, 0, ndir * G3, False), Bop, dwp, IN)
                 for d in range(ndir):
                     dw = torch.empty(G3, IN, device=dev)
                     _lib.call("b2p_conv_weight_permute", _p(dwp, d * G3 * IN), _p(dw), G3, C, ktaps, 1, _st())
                     grads[4 * d] = dw
             if ctx.needs_input_grad[0]:
                 dA = torch.empty(B * T, IN, device=dev)
-                gemm(B * T, IN, ndir * G3, op(dgi, 0, ndir * G3, True), op(wperm, 0, IN, False), dA, IN)
+                if U16 is not None:
+                    gemm(B * T, IN, ndir * G3, op(dgi16, 0, ndir * G3, True), op(wperm, 0, IN, False), dA, IN)
+                else:
+                    gemm(B * T, IN, ndir * G3, op(dgi, 0, ndir * G3, True), op(wperm, 0, IN, False), dA, IN)
                 dx = torch.empty(B, L, C, device=dev)
                 _lib.call("b2p_unfold_col2im", _p(dA), None, _p(dx), B, L, C, T, ktaps, stride, _st())
         else:
@@ -965,9 +1006,9 @@ class _EncoderLayer16(torch.autograd.Function):
         x1, x1_16, m1, r1 = _ln_fwd16(y1, g1, be1, eps)
         # FFN: f = dropout(gelu(x1 W1^T + b1)) (bf16 only: it is a GEMM operand and nothing else)
         w1_16, w2_16 = weight16(w1), weight16(w2)
-        pre = torch.empty(NT, F, device=dev)
+        pre = torch.empty(NT, F, device=dev, dtype=BF16)      # bf16 pre-activation: GELU' operand
         f16 = torch.empty(NT, F, device=dev, dtype=BF16)
-        gemm(NT, F, D, op(x1_16, 0, D, True), op(w1_16, 0, D, True), None, F, bias=b1, pre_out=pre,
+        gemm(NT, F, D, op(x1_16, 0, D, True), op(w1_16, 0, D, True), None, F, bias=b1, pre16=pre,
              act=ACT["gelu"], drop_p=p_act, seed=seeds[2], C16=f16)
         y2 = torch.empty(NT, D, device=dev)
         gemm(NT, D, F, op(f16, 0, F, True), op(w2_16, 0, F, True), y2, D, bias=b2, drop_p=p_hid, seed=seeds[3],
@@ -1006,19 +1047,17 @@ class _EncoderLayer16(torch.autograd.Function):
         if ng[14]:
             dw2 = torch.empty_like(w2)
             gemm(D, F, NT, op(dz2_16, 0, D, False), op(f16, 0, F, False), dw2, F)
-        # dpre = (dz2 W2) * mask_act * gelu'(pre): fp32 for the bias sum, bf16 for the GEMMs
-        dpre = torch.empty(NT, F, device=dev)
+        # dpre = (dz2 W2) * mask_act * gelu'(pre): bf16 for the GEMMs; its column sums (the FFN1 bias
+        # gradient) are reduced inside the epilogue from the fp32 values
         dpre16 = torch.empty(NT, F, device=dev, dtype=BF16)
-        gemm(NT, F, D, op(dz2_16, 0, D, True), op(w2_16, 0, F, False), dpre, F, drop_p=p_act, seed=seeds[2],
-             act_bwd=ACT["gelu"], aux=pre, C16=dpre16)
+        parts = colsum_parts_buf(NT, F, dev) if ng[13] else None
+        gemm(NT, F, D, op(dz2_16, 0, D, True), op(w2_16, 0, F, False), None, F, drop_p=p_act, seed=seeds[2],
+             act_bwd=ACT["gelu"], aux16=pre, C16=dpre16, colsum_part=parts)
         dw1 = None
         if ng[12]:
             dw1 = torch.empty_like(w1)
             gemm(F, D, NT, op(dpre16, 0, F, False), op(x1_16, 0, D, False), dw1, D)
-        db1 = torch.empty(F, device=dev) if ng[13] else None
-        if db1 is not None:
-            colsum(dpre, NT, F, db1)
-        del dpre
+        db1 = colsum_from_parts(parts, torch.empty(F, device=dev)) if ng[13] else None
         # dx1 = dpre W1 + dy2
         dx1 = torch.empty(NT, D, device=dev)
         gemm(NT, D, F, op(dpre16, 0, F, True), op(w1_16, 0, D, False), dx1, D, residual=dy2)
