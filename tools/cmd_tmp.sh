@@ -1,2 +1,2 @@
 set -e
-bash tools/gpu_check.sh epi16 "gemm or gru or encoder_layer or step_matches or full_size or reduce_loss or attention"
+bash tools/gpu_check.sh ctc3 "ctc or colsum or step_matches or full_size or reduce_loss or front_end or layernorm or conformer or gemm"

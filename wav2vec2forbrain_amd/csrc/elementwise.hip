@@ -34,16 +34,56 @@ __global__ void __launch_bounds__(256) colsum_p1(const float* __restrict__ X, co
   if (rl == 0 && n < N) part[((int64_t)b * nblk + blk) * N + n] = red[0][c] + red[1][c] + red[2][c] + red[3][c];
 }
 
-__global__ void colsum_p2(const float* __restrict__ part, int nblk, int64_t N, float* __restrict__ out,
-                          int accumulate) {
-  const int64_t n = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+// mode 0 with 16-B aligned rows: 128 columns (float4 per thread) x 8 row lanes per block
+__global__ void __launch_bounds__(256) colsum_p1v(const float* __restrict__ X, int64_t M, int64_t N, int64_t ld,
+                                                  int64_t bstride, float* __restrict__ part, int nblk) {
+  __shared__ float4 red[8][32];
+  const int c4 = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int64_t n = (int64_t)blockIdx.x * 128 + 4 * c4;
+  const int blk = blockIdx.y, b = blockIdx.z;
+  const int64_t m0 = (int64_t)blk * kColsumRows;
+  const int64_t m1 = m0 + kColsumRows < M ? m0 + kColsumRows : M;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n < N) {
+    const float* xp = X + b * bstride + n;
+#pragma unroll 4
+    for (int64_t m = m0 + rl; m < m1; m += 8) {
+      const float4 x = *reinterpret_cast<const float4*>(xp + m * ld);
+      s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+    }
+  }
+  red[rl][c4] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    float4 t = red[0][c4];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) {
+      const float4 u = red[r][c4];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    *reinterpret_cast<float4*>(part + ((int64_t)b * nblk + blk) * N + n) = t;
+  }
+}
+
+// 64 columns x 4 row groups per 256-thread block (the partial rows are summed 4-wide, then in LDS)
+__global__ void __launch_bounds__(256) colsum_p2(const float* __restrict__ part, int nblk, int64_t N,
+                                                 float* __restrict__ out, int accumulate) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + c;
   const int b = blockIdx.y;
-  if (n >= N) return;
-  const float* p = part + (int64_t)b * nblk * N + n;
   float s = 0.f;
-  for (int i = 0; i < nblk; ++i) s += p[(int64_t)i * N];
-  float* o = out + (int64_t)b * N + n;
-  *o = accumulate ? *o + s : s;
+  if (n < N) {
+    const float* p = part + (int64_t)b * nblk * N + n;
+    for (int i = rg; i < nblk; i += 4) s += p[(int64_t)i * N];
+  }
+  red[rg][c] = s;
+  __syncthreads();
+  if (rg == 0 && n < N) {
+    s = red[0][c] + red[1][c] + red[2][c] + red[3][c];
+    float* o = out + (int64_t)b * N + n;
+    *o = accumulate ? *o + s : s;
+  }
 }
 
 }  // namespace
@@ -53,9 +93,16 @@ int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_
                 int64_t bstride, int mode, float* out, int accumulate, float* part, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   const int nblk = (int)((M + kColsumRows - 1) / kColsumRows);
-  dim3 g1((unsigned)((N + 63) / 64), nblk, (unsigned)batch);
-  hipLaunchKernelGGL(colsum_p1, g1, dim3(256), 0, st, X, Y, M, N, ld, bstride, mode, part, nblk);
-  dim3 g2((unsigned)((N + 255) / 256), (unsigned)batch);
+  const bool vec = mode == 0 && N % 4 == 0 && ld % 4 == 0 && bstride % 4 == 0 && ((uintptr_t)X & 15u) == 0 &&
+                   ((uintptr_t)part & 15u) == 0;
+  if (vec) {
+    dim3 g1((unsigned)((N + 127) / 128), nblk, (unsigned)batch);
+    hipLaunchKernelGGL(colsum_p1v, g1, dim3(256), 0, st, X, M, N, ld, bstride, part, nblk);
+  } else {
+    dim3 g1((unsigned)((N + 63) / 64), nblk, (unsigned)batch);
+    hipLaunchKernelGGL(colsum_p1, g1, dim3(256), 0, st, X, Y, M, N, ld, bstride, mode, part, nblk);
+  }
+  dim3 g2((unsigned)((N + 63) / 64), (unsigned)batch);
   hipLaunchKernelGGL(colsum_p2, g2, dim3(256), 0, st, part, nblk, N, out, accumulate);
   B2P_CHECK_LAUNCH();
   return 0;
@@ -65,7 +112,7 @@ extern "C" int b2p_colsum_parts(const float* part, int64_t ntiles, int64_t N, fl
                                 b2p_stream_t stream) {
   B2P_CHECK_ARG(part && out, "colsum_parts: NULL pointer");
   if (N <= 0 || ntiles <= 0) return 0;
-  dim3 g2((unsigned)((N + 255) / 256), 1);
+  dim3 g2((unsigned)((N + 63) / 64), 1);
   hipLaunchKernelGGL(colsum_p2, g2, dim3(256), 0, (hipStream_t)stream, part, (int)ntiles, N, out, accumulate);
   B2P_CHECK_LAUNCH();
   return 0;

@@ -53,6 +53,19 @@ def precision(mode: str):
         _state.prec = old
 
 
+# error attribution (tools/bf16_err.py): blocks listed in B2P_FP32_OPS run their forward in exact fp32
+_FP32_OPS = set(filter(None, os.environ.get("B2P_FP32_OPS", "").split(",")))
+
+
+@contextlib.contextmanager
+def _fp32_if(name: str):
+    if name in _FP32_OPS:
+        with precision("fp32"):
+            yield
+    else:
+        yield
+
+
 def set_precision(mode: str) -> None:
     _state.prec = {"bf16": 0, "fp32": 1}[mode]
 
@@ -657,9 +670,10 @@ def _view_off(t, off):
 def gru_layer(x, H, ndir, weights, h0=None):
     """One nn.GRU layer (both directions) — brain_feature_extractor.py:39-47,61-65.
     x: (B,T,IN) tensor or Unfolded; weights: [w_ih, w_hh, b_ih, b_hh] per direction."""
-    if isinstance(x, Unfolded):
-        return _GRULayer.apply(x.src, (x.kernel, x.stride), H, ndir, h0, *weights)
-    return _GRULayer.apply(x, None, H, ndir, h0, *weights)
+    with _fp32_if("gru"):
+        if isinstance(x, Unfolded):
+            return _GRULayer.apply(x.src, (x.kernel, x.stride), H, ndir, h0, *weights)
+        return _GRULayer.apply(x, None, H, ndir, h0, *weights)
 
 
 # =====================================================================================
@@ -700,7 +714,8 @@ class _Linear(torch.autograd.Function):
 
 
 def linear(x, W, b=None, act=0):
-    return _Linear.apply(x.contiguous(), W, b, act)
+    with _fp32_if("linear"):
+        return _Linear.apply(x.contiguous(), W, b, act)
 
 
 class _Dropout(torch.autograd.Function):
@@ -1411,7 +1426,8 @@ def conformer_ffn(x, ln, w1, b1, w2, b2, act, p_act, p_hid, training, scale=0.5)
         p_act = p_hid = 0.0
     cfg = (act, float(ln.eps), float(p_act), float(p_hid), SEEDS.next() if p_act > 0 else 0,
            SEEDS.next() if p_hid > 0 else 0, float(scale))
-    return _FFNBlock.apply(x.contiguous(), ln.weight, ln.bias, w1, b1, w2, b2, cfg)
+    with _fp32_if("ffn"):
+        return _FFNBlock.apply(x.contiguous(), ln.weight, ln.bias, w1, b1, w2, b2, cfg)
 
 
 def conformer_attention(x, ln, q, k, v, o, nh, rotary, p_attn, p_out, training):
@@ -1423,8 +1439,9 @@ def conformer_attention(x, ln, q, k, v, o, nh, rotary, p_attn, p_out, training):
         cos_t, sin_t = rotary_tables(T, D // nh, rotary, x.device)
     seeds = (SEEDS.next() if p_attn > 0 else 0, SEEDS.next() if p_out > 0 else 0)
     cfg = (nh, float(ln.eps), float(p_attn), float(p_out), seeds)
-    return _ConformerAttnBlock.apply(x.contiguous(), ln.weight, ln.bias, q.weight, q.bias, k.weight, k.bias, v.weight,
-                                     v.bias, o.weight, o.bias, cos_t, sin_t, cfg)
+    with _fp32_if("attn"):
+        return _ConformerAttnBlock.apply(x.contiguous(), ln.weight, ln.bias, q.weight, q.bias, k.weight, k.bias,
+                                         v.weight, v.bias, o.weight, o.bias, cos_t, sin_t, cfg)
 
 
 def conformer_conv_module(x, cm, act, p, training):
@@ -1435,6 +1452,7 @@ def conformer_conv_module(x, cm, act, p, training):
            float(p), SEEDS.next() if p > 0 else 0, bool(training))
     if training and bn.num_batches_tracked is not None:
         bn.num_batches_tracked.add_(1)
-    return _ConvModule.apply(x.contiguous(), cm.layer_norm.weight, cm.layer_norm.bias, cm.pointwise_conv1.weight,
-                             cm.depthwise_conv.weight, bn.weight, bn.bias, cm.pointwise_conv2.weight, bn.running_mean,
-                             bn.running_var, cfg)
+    with _fp32_if("conv"):
+        return _ConvModule.apply(x.contiguous(), cm.layer_norm.weight, cm.layer_norm.bias, cm.pointwise_conv1.weight,
+                                 cm.depthwise_conv.weight, bn.weight, bn.bias, cm.pointwise_conv2.weight,
+                                 bn.running_mean, bn.running_var, cfg)
