@@ -298,3 +298,46 @@ def test_bf16_epilogue_pre16_aux16_colsum(M, N, K):
     cs = Fn.colsum_from_parts(parts, torch.empty(N, device="cuda"))
     ref_cs = ref.sum(0)
     assert float((cs - ref_cs).abs().max()) <= 1e-3 * float(ref.abs().sum(0).max()) + 1e-4
+
+
+@pytest.mark.parametrize("layout", ["AB", "Ab", "ab"])
+@pytest.mark.parametrize("M,N,K", [(4096, 1536, 512), (3000, 1544, 776)])
+@pytest.mark.parametrize("big", ["0", "1"])
+def test_bf16_big_tile_vs_small_tile(layout, M, N, K, big):
+    """Both bf16 tile configurations (128x128x32 4-wave default; 256x128x64 8-wave via
+    B2P_GEMM16_BIG, read once per process -> run in a subprocess) against torch fp32 on the same bf16
+    operands, with a full epilogue (bias, GELU, residual, bf16 copy, fused column sums).
+    (mn-contiguous operands need ld % 8 == 0, so M, N are multiples of 8.)"""
+    if big == "1":
+        import os
+        import subprocess
+        import sys
+        env = dict(os.environ, B2P_GEMM16_BIG="1")
+        code = (f"import tests.test_gemm_gpu as t; t.test_bf16_big_tile_vs_small_tile('{layout}', {M}, {N}, {K}, 'in')")
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=240)
+        assert r.returncode == 0, r.stderr[-2000:]
+        return
+    Fn = _fn()
+    torch.manual_seed(5)
+    bf = torch.bfloat16
+    if layout == "AB":
+        a, w = torch.randn(M, K, device="cuda").to(bf), torch.randn(N, K, device="cuda").to(bf)
+        A, Bo, ref = Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), a.float() @ w.float().t()
+    elif layout == "Ab":
+        a, w = torch.randn(M, K, device="cuda").to(bf), torch.randn(K, N, device="cuda").to(bf)
+        A, Bo, ref = Fn.op(a, 0, K, True), Fn.op(w, 0, N, False), a.float() @ w.float()
+    else:
+        a, w = torch.randn(K, M, device="cuda").to(bf), torch.randn(K, N, device="cuda").to(bf)
+        A, Bo, ref = Fn.op(a, 0, M, False), Fn.op(w, 0, N, False), a.float().t() @ w.float()
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda")
+    out = torch.empty(M, N, device="cuda")
+    o16 = torch.empty(M, N, device="cuda", dtype=bf)
+    parts = Fn.colsum_parts_buf(M, N, "cuda")
+    Fn.gemm(M, N, K, A, Bo, out, N, bias=bias, act=Fn.ACT["gelu"], residual=res, C16=o16, colsum_part=parts)
+    want = F.gelu(ref + bias) + res
+    _close(out, want, "bf16", scale=want.abs().max().item())
+    _close(o16.float(), want, "bf16", scale=want.abs().max().item())
+    cs = Fn.colsum_from_parts(parts, torch.empty(N, device="cuda"))
+    assert float((cs - want.sum(0)).abs().max()) <= 1e-4 * float(want.abs().sum(0).max())

@@ -1,2 +1,3 @@
 set -e
-bash tools/gpu_check.sh ctc3 "ctc or colsum or step_matches or full_size or reduce_loss or front_end or layernorm or conformer or gemm"
+timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "gemm" 2>&1 | tail -3
+timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline 2>/dev/null | tail -1

@@ -53,13 +53,16 @@ __device__ __forceinline__ int swz_k(int r) {
 // swizzle of an mn-contiguous image with 256-B rows (128 bf16), for ds_read_b64_tr_b16
 __device__ __forceinline__ int swz_t(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
-// per-lane source state of one 128 x KT operand tile: NI glds wave-instructions per wave per tile
-template <int KT, bool INNER_K, bool CONV>
+// per-lane source state of one ROWS x KT operand tile (NWAVES waves issue it together)
+template <int ROWS, int KT, bool INNER_K, bool CONV, int NWAVES>
 struct Src {
-  static constexpr int NJ = TILE * KT * 2 / 1024;   // instructions per tile (all waves)
-  static constexpr int NI = NJ / 4;                 // per wave
+  static constexpr int NJ = ROWS * KT * 2 / 1024;   // glds wave-instructions per tile (all waves)
+  static constexpr int NI = NJ / NWAVES;            // per wave
   static constexpr int RPI = 1024 / (2 * KT);       // INNER_K: rows per instruction
   static constexpr int LPR = KT / 8;                // INNER_K: lanes per row
+  static constexpr int CPR = ROWS / 8;              // !INNER_K: 16-B chunks per k-row
+  static constexpr int KPI = 64 / CPR;              // !INNER_K: k-rows per instruction
+  static_assert(NI * NWAVES == NJ && NI >= 1, "tile not divisible over the waves");
   const uint16_t* p[NI];
   int kofs[NI];
   bool ok[NI];
@@ -97,8 +100,8 @@ struct Src {
           p[i] = base + (int64_t)(ok[i] ? row : 0) * ld + kbeg + 8 * c;
         }
       } else {
-        const int r = 4 * j + (lane >> 4);
-        const int c = (lane & 15) ^ swz_t(r);
+        const int r = KPI * j + lane / CPR;
+        const int c = (lane % CPR) ^ swz_t(r);
         const int mn = mn0 + 8 * c;
         ok[i] = mn < MN;
         kofs[i] = r;
@@ -140,7 +143,9 @@ __device__ __forceinline__ bf16x8 frag_k(const char* img, int row0, int kk, int 
   const int c = (4 * kk + (lane >> 4)) ^ swz_k<KT>(r);
   return *reinterpret_cast<const bf16x8*>(img + r * (2 * KT) + c * 16);
 }
-// mn-contiguous image: columns col0 .. col0+15 (lane & 15) x k = 32*kk + 8*(lane>>4) .. +7
+// mn-contiguous image (ROWS mn-values per k-row): columns col0 .. col0+15 (lane & 15) x
+// k = 32*kk + 8*(lane>>4) .. +7
+template <int ROWS>
 __device__ __forceinline__ bf16x8 frag_t(const char* img, int col0, int kk, int lane) {
   const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
   const int chunk = (col0 >> 3) + (p >> 1);
@@ -148,7 +153,7 @@ __device__ __forceinline__ bf16x8 frag_t(const char* img, int col0, int kk, int 
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
     const int row = 32 * kk + 8 * g + 4 * hh + q;
-    const char* a = img + row * 256 + ((chunk ^ swz_t(row)) << 4) + 8 * (p & 1);
+    const char* a = img + row * (2 * ROWS) + ((chunk ^ swz_t(row)) << 4) + 8 * (p & 1);
     h[hh] = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4*)(a));
   }
   typedef short s16x8 __attribute__((ext_vector_type(8)));
@@ -156,24 +161,38 @@ __device__ __forceinline__ bf16x8 frag_t(const char* img, int col0, int kk, int 
   return __builtin_bit_cast(bf16x8, v);
 }
 
-constexpr int blocks_per_cu(int kt, int s) { return s * 2 * TILE * kt * 2 > 80 * 1024 ? 1 : 2; }
+// Tile configurations: BM x BN output tile, WGM x WGN waves of 64 x 64 each (4 x 4 MFMA tiles),
+// KT-deep k-tiles, S LDS stages (S-1 tiles in flight behind counted vmcnt waits + raw barriers).
+template <int BM_, int BN_, int KT_, int S_>
+struct Cfg {
+  static constexpr int BM = BM_, BN = BN_, KT = KT_, S = S_;
+  static constexpr int WGM = BM / 64, WGN = BN / 64, NW = WGM * WGN, NT = NW * 64;
+  static constexpr int STAGE = (BM + BN) * KT * 2;
+  static constexpr int LDS_MAIN = S * STAGE;
+  static constexpr int CS_LD = BN + 4;                          // epilogue staging row (floats)
+  static constexpr int LDS_EPI = 64 * CS_LD * 4;
+  static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
+  static constexpr int OCC = LDS > 80 * 1024 ? 1 : 2;           // workgroups per CU
+};
+using CfgSmall = Cfg<128, 128, 32, 3>;   // 4 waves, 2 workgroups/CU (default)
+using CfgBig = Cfg<256, 128, 64, 3>;     // 8 waves, 1 workgroup/CU (measured slower on the step's shapes:
+                                         // lock-stepped waves leave the MFMA pipe idle at every barrier)
 
-// KT: k-tile (32 or 64); S: LDS stages (S-1 tiles in flight while one is computed)
-template <int KT, int S, bool AK, bool BK, bool ACONV>
-__global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(const b2p_gemm_desc d, const EpiArgs ea, int tiles_m,
-                                                         int tiles_n) {
-  constexpr int OP_BYTES = TILE * KT * 2;
-  constexpr int STAGE_BYTES = 2 * OP_BYTES;
-  constexpr int CS_LD = TILE + 4;                       // epilogue staging row (floats)
-  constexpr int LDS_MAIN = S * STAGE_BYTES;
-  constexpr int LDS_EPI = 64 * CS_LD * 4;
-  constexpr int LDS_BYTES = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
-  constexpr int PT = 2 * Src<KT, AK, ACONV>::NI;        // glds per wave per tile (A + B)
-  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+template <class CF, bool AK, bool BK, bool ACONV>
+__global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_desc d, const EpiArgs ea, int tiles_m,
+                                                                int tiles_n) {
+  constexpr int BM = CF::BM, BN = CF::BN, KT = CF::KT, S = CF::S, NT = CF::NT;
+  constexpr int A_BYTES = BM * KT * 2;
+  constexpr int STAGE_BYTES = CF::STAGE;
+  constexpr int CS_LD = CF::CS_LD;
+  using SA = Src<BM, KT, AK, ACONV, CF::NW>;
+  using SB = Src<BN, KT, BK, false, CF::NW>;
+  constexpr int PT = SA::NI + SB::NI;                          // glds per wave per tile (A + B)
+  __shared__ __attribute__((aligned(1024))) char smem[CF::LDS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / CF::WGN, wn = wave % CF::WGN;
 
   // XCD-aware remap (bijective): blocks with equal blockIdx.x % 8 share an XCD and its L2, so
   // give each such group a contiguous range of tiles (neighbouring tiles share A rows).
@@ -189,15 +208,15 @@ __global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(cons
   const int ks = d.ksplit > 1 ? d.ksplit : 1;
   const int z = zz / ks, ksl = zz - z * ks;
   const int z1 = z / d.nz2, z2 = z - z1 * d.nz2;
-  const int m0 = tm * TILE, n0 = tn * TILE;
+  const int m0 = tm * BM, n0 = tn * BN;
   const int M = (int)d.M, N = (int)d.N;
   const int kchunk = ks > 1 ? (int)d.kchunk : (int)d.K;
   const int kbeg = ksl * kchunk;
   const int K = ((int)d.K < kbeg + kchunk) ? (int)d.K : kbeg + kchunk;
   const int nk = K > kbeg ? (K - kbeg + KT - 1) / KT : 0;
 
-  Src<KT, AK, ACONV> sa;
-  Src<KT, BK, false> sb;
+  SA sa;
+  SB sb;
   sa.init(d.A, z1, z2, wave, lane, m0, M, kbeg);
   sb.init(d.B, z1, z2, wave, lane, n0, N, kbeg);
 
@@ -212,7 +231,7 @@ __global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(cons
   for (int s = 0; s < S - 1; ++s) {
     if (s < nk) {
       sa.issue(smem + s * STAGE_BYTES, wave, kbeg + s * KT, K);
-      sb.issue(smem + s * STAGE_BYTES + OP_BYTES, wave, kbeg + s * KT, K);
+      sb.issue(smem + s * STAGE_BYTES + A_BYTES, wave, kbeg + s * KT, K);
     }
   }
   int cur = 0;              // stage of tile kt
@@ -227,19 +246,19 @@ __global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(cons
     if (kt + S - 1 < nk) {
       char* img = smem + nxt * STAGE_BYTES;
       sa.issue(img, wave, kbeg + (kt + S - 1) * KT, K);
-      sb.issue(img + OP_BYTES, wave, kbeg + (kt + S - 1) * KT, K);
+      sb.issue(img + A_BYTES, wave, kbeg + (kt + S - 1) * KT, K);
     }
     const char* As = smem + cur * STAGE_BYTES;
-    const char* Bs = As + OP_BYTES;
+    const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < KT / 32; ++kk) {
       bf16x8 af[4], bfr[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        af[i] = AK ? frag_k<KT>(As, wm * 64 + i * 16, kk, lane) : frag_t(As, wm * 64 + i * 16, kk, lane);
+        af[i] = AK ? frag_k<KT>(As, wm * 64 + i * 16, kk, lane) : frag_t<BM>(As, wm * 64 + i * 16, kk, lane);
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        bfr[j] = BK ? frag_k<KT>(Bs, wn * 64 + j * 16, kk, lane) : frag_t(Bs, wn * 64 + j * 16, kk, lane);
+        bfr[j] = BK ? frag_k<KT>(Bs, wn * 64 + j * 16, kk, lane) : frag_t<BN>(Bs, wn * 64 + j * 16, kk, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -250,17 +269,19 @@ __global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(cons
     nxt = nxt + 1 == S ? 0 : nxt + 1;
   }
 
-  // epilogue, staged through LDS in two 64-row halves so that every thread then handles 4
-  // consecutive columns (16-B loads/stores of C, bias, aux, residual; 8-B bf16 copy)
+  // epilogue, staged through LDS one 64-row wave band at a time so that every thread then handles
+  // 4 consecutive columns (16-B loads/stores of C, bias, aux, residual; 8-B bf16 copy)
+  constexpr int CG = BN / 4;                 // column groups (4 columns each)
+  constexpr int RPP = NT / CG;               // rows per pass
   float* Cs = reinterpret_cast<float*>(smem);
   float* slab = ks > 1 ? d.workspace + ((int64_t)z * ks + ksl) * (int64_t)M * N : nullptr;
-  const int cg = tid & 31, rbase = tid >> 5;
+  const int cg = tid % CG, rbase = tid / CG;
   float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);   // fused bias-gradient column sums (colsum_part)
 #pragma clang loop unroll(full)
-  for (int half = 0; half < 2; ++half) {
+  for (int band = 0; band < CF::WGM; ++band) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    if (wm == half) {
+    if (wm == band) {
 #pragma clang loop unroll(full)
       for (int i = 0; i < 4; ++i)
 #pragma clang loop unroll(full)
@@ -271,10 +292,10 @@ __global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(cons
     }
     __syncthreads();
 #pragma clang loop unroll(full)
-    for (int i = 0; i < 8; ++i) {
-      const int rl = rbase + 8 * i;
+    for (int i = 0; i < 64 / RPP; ++i) {
+      const int rl = rbase + RPP * i;
       const float4 v = *reinterpret_cast<const float4*>(Cs + rl * CS_LD + 4 * cg);
-      const int m = m0 + half * 64 + rl, n = n0 + 4 * cg;
+      const int m = m0 + band * 64 + rl, n = n0 + 4 * cg;
       if (ks > 1) {
         if (m < M) {
           float* dst = slab + (int64_t)m * N + n;
@@ -293,46 +314,38 @@ __global__ void __launch_bounds__(NT16, blocks_per_cu(KT, S)) gemm16_kernel(cons
     }
   }
   if (ea.e.colsum_part) {
-    // the 8 threads of a column group (rbase = 0..7) add their 16 rows: one 128-row tile partial
+    // the RPP threads of a column group add their rows: one BM-row tile partial
     __syncthreads();
     *reinterpret_cast<float4*>(Cs + rbase * CS_LD + 4 * cg) = csum;
     __syncthreads();
-    if (tid < TILE && n0 + tid < N) {
+    if (tid < BN && n0 + tid < N) {
       float sacc = 0.f;
 #pragma unroll
-      for (int r = 0; r < 8; ++r) sacc += Cs[r * CS_LD + tid];
-      ea.e.colsum_part[(int64_t)tm * N + n0 + tid] = sacc;
+      for (int r = 0; r < RPP; ++r) sacc += Cs[r * CS_LD + tid];
+      // partial rows are 128-row granular: a BM-row tile fills its first row, zeroes the others
+      const int prow = tm * (BM / 128), nprow = (M + 127) / 128;
+      ea.e.colsum_part[(int64_t)prow * N + n0 + tid] = sacc;
+#pragma unroll
+      for (int r2 = 1; r2 < BM / 128; ++r2)
+        if (prow + r2 < nprow) ea.e.colsum_part[(int64_t)(prow + r2) * N + n0 + tid] = 0.f;
     }
   }
 }
 
 }  // namespace
 
-// K-tile / stage selection (B2P_GEMM16=KT,S for experiments; default 64,2)
-static void cfg16(int* kt, int* st) {
-  static int v[2] = {0, 0};
-  if (!v[0]) {
-    int a = 64, b = 2;
-    if (const char* e = getenv("B2P_GEMM16")) sscanf(e, "%d,%d", &a, &b);
-    if (!((a == 64 && (b == 2 || b == 3)) || (a == 32 && (b == 2 || b == 3 || b == 4)))) { a = 64; b = 2; }
-    v[0] = a; v[1] = b;
-  }
-  *kt = v[0];
-  *st = v[1];
-}
-
-template <int KT, int S>
-static void launch16(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st, dim3 grid, int tm, int tn) {
-  const dim3 block(NT16);
+template <class CF>
+static void launch_cfg(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st, dim3 grid, int tm, int tn) {
+  const dim3 block(CF::NT);
   const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
   if (AK && BK) {
-    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<KT, S, true, true, true>), grid, block, 0, st, d, ea, tm, tn);
-    else hipLaunchKernelGGL((gemm16_kernel<KT, S, true, true, false>), grid, block, 0, st, d, ea, tm, tn);
+    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<CF, true, true, true>), grid, block, 0, st, d, ea, tm, tn);
+    else hipLaunchKernelGGL((gemm16_kernel<CF, true, true, false>), grid, block, 0, st, d, ea, tm, tn);
   } else if (AK && !BK) {
-    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<KT, S, true, false, true>), grid, block, 0, st, d, ea, tm, tn);
-    else hipLaunchKernelGGL((gemm16_kernel<KT, S, true, false, false>), grid, block, 0, st, d, ea, tm, tn);
+    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<CF, true, false, true>), grid, block, 0, st, d, ea, tm, tn);
+    else hipLaunchKernelGGL((gemm16_kernel<CF, true, false, false>), grid, block, 0, st, d, ea, tm, tn);
   } else {
-    hipLaunchKernelGGL((gemm16_kernel<KT, S, false, false, false>), grid, block, 0, st, d, ea, tm, tn);
+    hipLaunchKernelGGL((gemm16_kernel<CF, false, false, false>), grid, block, 0, st, d, ea, tm, tn);
   }
 }
 
@@ -343,30 +356,27 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
     return 1;
   }
   const int ks = d.ksplit > 1 ? d.ksplit : 1;
-  const int tm = (int)((d.M + TILE - 1) / TILE), tn = (int)((d.N + TILE - 1) / TILE);
-  const int64_t nwg = (int64_t)tm * tn * d.nz1 * d.nz2 * ks;
+  const int64_t nz = (int64_t)d.nz1 * d.nz2 * ks;
+  // big tile (opt-in, B2P_GEMM16_BIG=1): one unsplit, unbatched, plain (non-conv) operand pair with a
+  // grid that still fills the chip
+  static int big_ok = getenv("B2P_GEMM16_BIG") ? atoi(getenv("B2P_GEMM16_BIG")) : 0;
+  const int64_t tiles_big = ((d.M + 255) / 256) * ((d.N + 127) / 128);
+  const bool big = big_ok && ks == 1 && nz == 1 && !d.A.conv && d.K >= 512 && tiles_big >= 192;
+  if (big) {
+    const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 127) / 128);
+    launch_cfg<CfgBig>(d, ea, st, dim3((unsigned)((int64_t)tm * tn)), tm, tn);
+    return 0;
+  }
+  const int tm = (int)((d.M + 127) / 128), tn = (int)((d.N + 127) / 128);
+  const int64_t nwg = (int64_t)tm * tn * nz;
   if (nwg >= (1ll << 31)) {
     b2p_set_error("gemm16: grid too large");
     return 1;
   }
-  int kt, stg;
-  cfg16(&kt, &stg);
-  if (!getenv("B2P_GEMM16")) {
-    // measured (tools/bench_gemm.py b16): 64-deep k-tiles win on long unsplit plain K (fewer
-    // barriers per FLOP), 32-deep on short K, split-K slices and the implicit-conv operand
-    const int64_t kblk = ks > 1 ? d.kchunk : d.K;
-    kt = (kblk >= 2048 && ks == 1 && !d.A.conv) ? 64 : 32;
-    stg = 2;
+  if (ks > 1 && d.kchunk % 32 != 0) {
+    b2p_set_error("gemm16: split-K chunk must be a multiple of 32");
+    return 1;
   }
-  if (ks > 1 && d.kchunk % kt != 0) kt = 32;
-  const dim3 grid((unsigned)nwg);
-  if (kt == 64) {
-    if (stg == 3) launch16<64, 3>(d, ea, st, grid, tm, tn);
-    else launch16<64, 2>(d, ea, st, grid, tm, tn);
-  } else {
-    if (stg == 4) launch16<32, 4>(d, ea, st, grid, tm, tn);
-    else if (stg == 3) launch16<32, 3>(d, ea, st, grid, tm, tn);
-    else launch16<32, 2>(d, ea, st, grid, tm, tn);
-  }
+  launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   return 0;
 }
