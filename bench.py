@@ -196,8 +196,9 @@ def main():
         "step_mfma_frac": round(step_tflop * steps_per_s / BF16_DENSE_PEAK_TFLOPS, 4),
         "roofline": {"bound": "mfma", "kernel": "b2p_gemm (all GEMM launches of the step)",
                      "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": None,
-                     "launches": gemm_n, "avg_launch_us": round(gemm_ms * 1e3 / max(gemm_n, 1), 2)},
+                     "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": gemm_traffic(),
+                     "launches": gemm_n, "avg_launch_us": round(gemm_ms * 1e3 / max(gemm_n, 1), 2),
+                     "algorithmic_flop_per_launch": round(gemm_flops / max(gemm_n, 1), 1)},
     }
     if args.config != "base":
         res["metric"] = "train steps/sec + CTC loss, b2p2t_gru+w2v_conformer bs=32 seq=1024"
@@ -206,6 +207,18 @@ def main():
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def gemm_traffic():
+    """HBM bytes per GEMM launch from the newest committed PMC measurement of this same bench command
+    (profiles/*_gemm_traffic.json, written by tools/round_profile.sh: FETCH_SIZE x2 + WRITE_SIZE)."""
+    import glob
+    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic.json")), key=os.path.getmtime)
+    if not fs:
+        return None
+    d = json.load(open(fs[-1]))
+    return {"bytes_per_launch": round(d["traffic_bytes_per_launch"]), "source": os.path.relpath(fs[-1], ROOT),
+            "method": d["method"]}
 
 
 def ctypes_read_timing():
