@@ -134,12 +134,15 @@ def main():
     brain_params = [p for n, p in model.named_parameters() if n.startswith("brain_encoder.") and n not in skip]
     opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
     reducer = GradBucketReducer(brain_params) if world > 1 else None
+    # the frozen w2v's weight gradients (computed, as the reference does) run beside the GRU backward
+    Fn.set_deferred_wgrad([p for n, p in model.named_parameters() if not n.startswith("brain_encoder.")])
     batch = batch_on(cfg, device)
 
     def step():
         opt.zero_grad()
         out = model(batch)            # forward incl. ctc_loss.item() (reference :94)
         out.loss.backward()
+        Fn.join_wgrad()
         if reducer is not None:
             reducer.finish()
         opt.step()

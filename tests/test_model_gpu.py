@@ -128,3 +128,30 @@ def test_train_steps_reduce_loss():
         losses.append(out.metrics["ctc_loss"])
     assert all(np.isfinite(losses))
     assert min(losses[-3:]) < losses[0]
+
+
+def test_deferred_frozen_wgrad_matches_immediate():
+    """Frozen-parameter gradients deferred onto the side stream (flushed beside the GRU backward,
+    accumulated into .grad in the GEMM epilogue) equal the immediate path, and accumulate over steps
+    like autograd's AccumulateGrad."""
+    from wav2vec2forbrain_amd import functional as Fn
+    cfg = CFG["plumbing_base"]
+    res = []
+    for defer in (False, True):
+        model = build_model(cfg)
+        model.train()
+        frozen = [p for n, p in model.named_parameters() if not n.startswith("brain_encoder.")]
+        Fn.set_deferred_wgrad(frozen if defer else [])
+        with Fn.precision("bf16"):
+            for _ in range(2):   # two steps: the second accumulates into existing .grad
+                out = model(_batch(cfg))
+                out.loss.backward()
+                Fn.join_wgrad()
+        torch.cuda.synchronize()
+        res.append({n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None})
+        Fn.set_deferred_wgrad([])
+    a, b = res
+    assert set(a) == set(b)
+    for n in a:
+        d = float((a[n] - b[n]).norm())
+        assert d <= 1e-5 * float(a[n].norm()) + 1e-7, n

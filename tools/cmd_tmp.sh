@@ -1,3 +1,2 @@
 set -e
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread -k "gemm" 2>&1 | tail -3
-timeout -k 10 300 python bench.py --steps 10 --warmup 3 --no-cpu-baseline 2>/dev/null | tail -1
+bash tools/gpu_check.sh defer "deferred or step_matches or full_size or reduce_loss"

@@ -66,6 +66,133 @@ def _fp32_if(name: str):
         yield
 
 
+# -------------------------------------------------------------------------------------------
+# Deferred gradients of FROZEN parameters (reference semantics: the frozen w2v still gets weight
+# gradients accumulated into .grad every step, src/train/train_loop.py:44,66 — they feed nothing
+# in the step). Their GEMMs are queued during the encoder backward and flushed onto a side stream
+# when the (4-CU) GRU recurrence backward starts, so they fill the otherwise idle chip; they
+# accumulate into p.grad in the GEMM epilogue (beta = 1) instead of autograd's separate add.
+# join_wgrad() orders the side stream back into the main stream (train step, optimizer).
+class _Deferred:
+    ids: set = set()
+    queue: list = []
+    side = None
+    pending = False
+
+
+def set_deferred_wgrad(params) -> None:
+    """Parameters whose gradients may be deferred (frozen: not optimised, not all-reduced)."""
+    _Deferred.ids = {id(p) for p in params if p is not None}
+
+
+def _defer_ok(p) -> bool:
+    return p is not None and id(p) in _Deferred.ids
+
+
+def _acc_param(p, g) -> None:
+    if p.grad is None:
+        p.grad = g
+    else:
+        p.grad.add_(g)
+
+
+def _defer_acc(p, g) -> None:
+    """Accumulate a ready gradient tensor into p.grad on the side stream."""
+    _Deferred.queue.append((lambda: _acc_param(p, g), (g,)))
+
+
+def _defer_wgemm_rows(ps, fn, *tensors) -> None:
+    """Like _defer_wgemm for parameters whose gradients are row blocks of ONE GEMM output (Q, K, V
+    weights of the fused QKV projection): their .grad are views of one buffer, so a single GEMM
+    writes or accumulates all of them."""
+    prec = _prec()
+
+    def run():
+        old = _state.prec
+        _state.prec = prec
+        try:
+            rows = [p.shape[0] for p in ps]
+            g0 = ps[0].grad
+            fused = g0 is not None and all(p.grad is not None for p in ps)
+            if fused:
+                base = g0.untyped_storage().data_ptr()
+                off = g0.storage_offset()
+                for p in ps:
+                    fused = fused and p.grad.is_contiguous() and p.grad.untyped_storage().data_ptr() == base \
+                        and p.grad.storage_offset() == off
+                    off += p.numel()
+            if fused:
+                buf = torch.as_strided(g0, (sum(rows),) + tuple(ps[0].shape[1:]), g0.stride())
+                fn(buf, 1.0)
+            elif all(p.grad is None for p in ps):
+                buf = torch.empty((sum(rows),) + tuple(ps[0].shape[1:]), device=ps[0].device)
+                fn(buf, 0.0)
+                r = 0
+                for p, n in zip(ps, rows):
+                    p.grad = buf[r:r + n]
+                    r += n
+            else:   # mixed state: compute, then accumulate per parameter
+                buf = torch.empty((sum(rows),) + tuple(ps[0].shape[1:]), device=ps[0].device)
+                fn(buf, 0.0)
+                r = 0
+                for p, n in zip(ps, rows):
+                    _acc_param(p, buf[r:r + n])
+                    r += n
+        finally:
+            _state.prec = old
+    _Deferred.queue.append((run, tensors))
+
+
+def _defer_wgemm(p, fn, *tensors) -> None:
+    """Queue fn(out, beta): a weight-gradient GEMM writing (beta 0) or accumulating (beta 1) p.grad."""
+    prec = _prec()
+
+    def run():
+        old = _state.prec
+        _state.prec = prec
+        try:
+            if p.grad is None:
+                p.grad = torch.empty_like(p)
+                fn(p.grad, 0.0)
+            else:
+                fn(p.grad, 1.0)
+        finally:
+            _state.prec = old
+    _Deferred.queue.append((run, tensors))
+
+
+def flush_wgrad(after=None) -> None:
+    """Launch the queued frozen-parameter gradient work on the side stream, ordered after the event
+    `after` (recorded by the caller before a long kernel it wants to run beside) or after everything
+    the main stream has queued so far."""
+    if not _Deferred.queue:
+        return
+    main = torch.cuda.current_stream()
+    if _Deferred.side is None:
+        _Deferred.side = torch.cuda.Stream(device=main.device)
+    side = _Deferred.side
+    if after is not None:
+        side.wait_event(after)
+    else:
+        side.wait_stream(main)
+    with torch.cuda.stream(side):
+        for fn, _ in _Deferred.queue:
+            fn()
+    for _, ts in _Deferred.queue:
+        for t in ts:
+            t.record_stream(side)
+    _Deferred.queue.clear()
+    _Deferred.pending = True
+
+
+def join_wgrad() -> None:
+    """Flush, then make the current stream wait for the side stream."""
+    flush_wgrad()
+    if _Deferred.pending:
+        torch.cuda.current_stream().wait_stream(_Deferred.side)
+        _Deferred.pending = False
+
+
 def set_precision(mode: str) -> None:
     _state.prec = {"bf16": 0, "fp32": 1}[mode]
 
@@ -587,8 +714,11 @@ class _GRULayer(torch.autograd.Function):
             doL = torch.empty(_ln_floats(B, T, H, ndir, 1), device=dev)
             _lib.call("b2p_gru_lane_permute", _p(dout), _p(doL), B, T, H, ndir, 1, 1, 0x0, 1, _st())
             dgL = torch.empty(_ln_floats(B, T, H, ndir, 4), device=dev)
+            ev = torch.cuda.Event()
+            ev.record()
             _lib.call("b2p_gru_bwd16", _p(doL), _p(whh_s), _p(hL), _p(saved), _p(h0), _p(dgL), _p(dh0), B, T, H,
                       ndir, _st())
+            flush_wgrad(ev)   # frozen-parameter gradient GEMMs fill the chip beside the 4-CU recurrence
             del doL
             # dgi = LN records (0, 1, 2), dgh = LN records (0, 1, 3)
             _lib.call("b2p_gru_lane_permute", _p(dgL), _p(dgi), B, T, H, ndir, 4, 3, 0xF210, 0, _st())
@@ -596,8 +726,11 @@ class _GRULayer(torch.autograd.Function):
             del dgL
         else:
             dhbuf = torch.empty(ndir, B, H, device=dev)
+            ev = torch.cuda.Event()
+            ev.record()
             _lib.call("b2p_gru_bwd", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi), _p(dgh), _p(dh0),
                       _p(dhbuf), B, T, H, ndir, _st())
+            flush_wgrad(ev)
         grads = [None] * (4 * ndir)
         # recurrent weights: dW_hh[d] = dgh[:, :, d]^T @ hprev[d]
         hp = torch.empty(ndir, B, T, H, device=dev)
@@ -1035,6 +1168,7 @@ class _EncoderLayer16(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.shape = (B, T, D)
         ctx.fused = fused
+        ctx.prm = (wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2)
         ctx.has_b = [b is not None for b in (bq, bk, bv, bo, b1, b2)]
         res = out.view(B, T, D)
         attach16(res, out16.view(B, T, D))
@@ -1058,10 +1192,15 @@ class _EncoderLayer16(torch.autograd.Function):
         dy2, dg2, dbe2, _dz2, dz2_16 = _ln_bwd16(dout, y2, g2, m2, r2, True, in_drop_p=p_hid, in_seed=seeds[3],
                                                  dbias_in=db2)
         del _dz2
+        prm = ctx.prm
         dw2 = None
         if ng[14]:
-            dw2 = torch.empty_like(w2)
-            gemm(D, F, NT, op(dz2_16, 0, D, False), op(f16, 0, F, False), dw2, F)
+            if _defer_ok(w2):
+                _defer_wgemm(prm[12], lambda o, bt, a=dz2_16, b=f16: gemm(D, F, NT, op(a, 0, D, False), op(b, 0, F, False),
+                                                                        o, F, beta=bt), dz2_16, f16)
+            else:
+                dw2 = torch.empty_like(w2)
+                gemm(D, F, NT, op(dz2_16, 0, D, False), op(f16, 0, F, False), dw2, F)
         # dpre = (dz2 W2) * mask_act * gelu'(pre): bf16 for the GEMMs; its column sums (the FFN1 bias
         # gradient) are reduced inside the epilogue from the fp32 values
         dpre16 = torch.empty(NT, F, device=dev, dtype=BF16)
@@ -1070,8 +1209,13 @@ class _EncoderLayer16(torch.autograd.Function):
              act_bwd=ACT["gelu"], aux16=pre, C16=dpre16, colsum_part=parts)
         dw1 = None
         if ng[12]:
-            dw1 = torch.empty_like(w1)
-            gemm(F, D, NT, op(dpre16, 0, F, False), op(x1_16, 0, D, False), dw1, D)
+            if _defer_ok(w1):
+                _defer_wgemm(prm[10], lambda o, bt, a=dpre16, b=x1_16: gemm(F, D, NT, op(a, 0, F, False),
+                                                                          op(b, 0, D, False), o, D, beta=bt),
+                             dpre16, x1_16)
+            else:
+                dw1 = torch.empty_like(w1)
+                gemm(F, D, NT, op(dpre16, 0, F, False), op(x1_16, 0, D, False), dw1, D)
         db1 = colsum_from_parts(parts, torch.empty(F, device=dev)) if ng[13] else None
         # dx1 = dpre W1 + dy2
         dx1 = torch.empty(NT, D, device=dev)
@@ -1084,8 +1228,12 @@ class _EncoderLayer16(torch.autograd.Function):
         del _dz1
         dwo = None
         if ng[8]:
-            dwo = torch.empty_like(wo)
-            gemm(D, D, NT, op(dz1_16, 0, D, False), op(O16, 0, D, False), dwo, D)
+            if _defer_ok(wo):
+                _defer_wgemm(prm[6], lambda o, bt, a=dz1_16, b=O16: gemm(D, D, NT, op(a, 0, D, False), op(b, 0, D, False),
+                                                                       o, D, beta=bt), dz1_16, O16)
+            else:
+                dwo = torch.empty_like(wo)
+                gemm(D, D, NT, op(dz1_16, 0, D, False), op(O16, 0, D, False), dwo, D)
         if ctx.fused:
             dO16 = torch.empty(NT, D, device=dev, dtype=BF16)
             gemm(NT, D, D, op(dz1_16, 0, D, True), op(wo16, 0, D, False), None, D, C16=dO16)
@@ -1097,7 +1245,12 @@ class _EncoderLayer16(torch.autograd.Function):
             dqkv, dqkv16 = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seeds[0], want16=True)
             del dO
         grads_w = [None] * 6
-        if ng[2] or ng[4] or ng[6]:
+        if all(_defer_ok(w) for w in (wq, wk, wv)) and ng[2] and ng[4] and ng[6]:
+            _defer_wgemm_rows((prm[0], prm[2], prm[4]),
+                              lambda o, bt, a=dqkv16, b=x16: gemm(3 * D, D, NT, op(a, 0, 3 * D, False),
+                                                                  op(b, 0, D, False), o, D, beta=bt),
+                              dqkv16, x16)
+        elif ng[2] or ng[4] or ng[6]:
             dwqkv = torch.empty(3 * D, D, device=dev)
             gemm(3 * D, D, NT, op(dqkv16, 0, 3 * D, False), op(x16, 0, D, False), dwqkv, D)
             for i in range(3):
@@ -1114,7 +1267,17 @@ class _EncoderLayer16(torch.autograd.Function):
             dx = torch.empty(NT, D, device=dev)
             gemm(NT, D, 3 * D, op(dqkv16, 0, 3 * D, True), op(wqkv16, 0, D, False), dx, D, residual=dy1)
             dx = dx.view(B, T, D)
-        return (dx, None, *grads_w, dwo, dbo, dg1, dbe1, dw1, db1, dw2, db2, dg2, dbe2)
+        rest = [dwo, dbo, dg1, dbe1, dw1, db1, dw2, db2, dg2, dbe2]
+        # small gradients of frozen parameters: accumulated on the side stream too
+        for k, g in enumerate(grads_w):
+            if g is not None and k % 2 == 1 and _defer_ok(prm[k]):
+                _defer_acc(prm[k], g)
+                grads_w[k] = None
+        for k, g in enumerate(rest):
+            if g is not None and _defer_ok(prm[6 + k]):
+                _defer_acc(prm[6 + k], g)
+                rest[k] = None
+        return (dx, None, *grads_w, *rest)
 
 
 def encoder_layer(x, params, nh, eps, p_attn, p_hid, p_act, training):

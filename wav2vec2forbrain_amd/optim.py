@@ -26,6 +26,7 @@ class HipAdam(torch.optim.Optimizer):
         if closure is not None:
             with torch.enable_grad():
                 loss = closure()
+        Fn.join_wgrad()    # deferred frozen-parameter gradient work is ordered before the update
         lib = _lib.load()
         stream = _lib.stream_ptr()
         for group in self.param_groups:

@@ -10,6 +10,8 @@ from typing import Literal, cast
 
 import numpy as np
 import torch
+
+from .. import functional as Fn
 import torch.distributed as dist
 
 from ..datasets.batch_types import SampleBatch
@@ -33,6 +35,9 @@ class Trainer:
             opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
             params = [p for n, p in self.model.named_parameters() if id(p) in opt_ids and n not in skip]
             self.reducer = GradBucketReducer(params)
+        # frozen parameters (not optimised): their gradient GEMMs run deferred beside the GRU backward
+        opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
+        Fn.set_deferred_wgrad([p for p in self.model.parameters() if p.requires_grad and id(p) not in opt_ids])
 
     def _log_intermediate(self, batch: int, n_batches: int, evaluator):
         print(f"Batch {batch + 1}/{n_batches} loss: {evaluator.get_latest_loss():.2f} "
@@ -51,6 +56,7 @@ class Trainer:
             outputs = self.model.forward(batch)
         loss = cast(torch.Tensor, outputs.loss)
         loss.backward()
+        Fn.join_wgrad()
         if self.reducer is not None:
             self.reducer.finish()
         if self.config.gradient_clipping is not None:
