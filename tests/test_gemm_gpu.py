@@ -300,24 +300,50 @@ def test_bf16_epilogue_pre16_aux16_colsum(M, N, K):
     assert float((cs - ref_cs).abs().max()) <= 1e-3 * float(ref.abs().sum(0).max()) + 1e-4
 
 
-@pytest.mark.parametrize("layout", ["AB", "Ab", "ab"])
-@pytest.mark.parametrize("M,N,K", [(4096, 1536, 512), (3000, 1544, 776)])
-@pytest.mark.parametrize("big", ["0", "1"])
-def test_bf16_big_tile_vs_small_tile(layout, M, N, K, big):
-    """Both bf16 tile configurations (128x128x32 4-wave default; 256x128x64 8-wave via
-    B2P_GEMM16_BIG, read once per process -> run in a subprocess) against torch fp32 on the same bf16
-    operands, with a full epilogue (bias, GELU, residual, bf16 copy, fused column sums).
+_TILE_ENV = {"small": {"B2P_GEMM16_PP": "0"}, "big": {"B2P_GEMM16_PP": "0", "B2P_GEMM16_BIG": "1"},
+             "pp": {"B2P_GEMM16_PP": "2"}}
+_TILE_CASES = [(lay, M, N, K) for lay in ("AB", "Ab", "ab") for (M, N, K) in ((4096, 1536, 512), (3000, 1544, 776))]
+
+
+@pytest.mark.parametrize("tile", ["small", "big", "pp"])
+def test_bf16_tile_configs(tile):
+    """Every bf16 tile configuration (128x128x32 4-wave; 256x128x64 8-wave; 256x256x64 8-wave
+    ping-pong), forced by environment (read once per process -> one subprocess per configuration),
+    against torch fp32 on the same bf16 operands with a full epilogue (bias, GELU, residual, bf16
+    copy, fused column sums), plus split-K and batched launches.
     (mn-contiguous operands need ld % 8 == 0, so M, N are multiples of 8.)"""
-    if big == "1":
-        import os
-        import subprocess
-        import sys
-        env = dict(os.environ, B2P_GEMM16_BIG="1")
-        code = (f"import tests.test_gemm_gpu as t; t.test_bf16_big_tile_vs_small_tile('{layout}', {M}, {N}, {K}, 'in')")
-        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=240)
-        assert r.returncode == 0, r.stderr[-2000:]
-        return
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, **_TILE_ENV[tile])
+    code = ("import tests.test_gemm_gpu as t\n"
+            "for c in t._TILE_CASES: t._check_tile_case(*c)\n"
+            "t._check_tile_splitk_batched()\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+def _check_tile_splitk_batched():
+    Fn = _fn()
+    torch.manual_seed(6)
+    bf = torch.bfloat16
+    # plain wide-K GEMM (split-K path when the grid is small) with beta accumulation
+    M, N, K = 768, 1024, 4160
+    a, w = torch.randn(K, M, device="cuda").to(bf), torch.randn(K, N, device="cuda").to(bf)
+    c0 = torch.randn(M, N, device="cuda")
+    out = c0.clone()
+    Fn.gemm(M, N, K, Fn.op(a, 0, M, False), Fn.op(w, 0, N, False), out, N, beta=1.0)
+    _close16(out, a.double().t() @ w.double() + c0.double(), 2e-6)
+    # batched (nz1 = 3) k-contiguous operands
+    Z, M, N, K = 3, 520, 776, 320
+    a, w = torch.randn(Z, M, K, device="cuda").to(bf), torch.randn(Z, N, K, device="cuda").to(bf)
+    out = torch.empty(Z, M, N, device="cuda")
+    Fn.gemm(M, N, K, Fn.op(a, 0, K, True, bs1=M * K), Fn.op(w, 0, K, True, bs1=N * K), out, N, cbs1=M * N, nz1=Z)
+    _close16(out, (a.double() @ w.double().transpose(1, 2)).float(), 2e-6)
+
+
+def _check_tile_case(layout, M, N, K):
     Fn = _fn()
     torch.manual_seed(5)
     bf = torch.bfloat16

@@ -50,14 +50,33 @@ void b2p_set_error(const char* fmt, ...);
 // ---------------------------------------------------------------------------
 // device math
 // ---------------------------------------------------------------------------
+// erf(z) for z >= 0 given e = exp(-z*z): Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), one
+// reciprocal + four FMAs, branch-free (the library erff is a ~30-instruction piecewise polynomial;
+// in the GEMM epilogues the GELU / GELU' of every FFN element is VALU work beside the MFMAs)
+__device__ __forceinline__ float b2p_erf_pos(float z, float e) {
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
+  float p = fmaf(1.061405429f, t, -1.453152027f);
+  p = fmaf(p, t, 1.421413741f);
+  p = fmaf(p, t, -0.284496736f);
+  p = fmaf(p, t, 0.254829592f);
+  return 1.0f - p * t * e;
+}
+// Phi(x) = 0.5 * (1 + erf(x / sqrt 2)), with exp(-x^2/2) returned for the GELU derivative
+__device__ __forceinline__ float b2p_phi(float x, float& e) {
+  const float z = fabsf(x) * 0.70710678118654752440f;
+  e = __expf(-z * z);
+  const float er = b2p_erf_pos(z, e);
+  return 0.5f * (1.0f + copysignf(er, x));
+}
 __device__ __forceinline__ float b2p_gelu(float x) {
-  // exact erf GELU (transformers ACT2FN["gelu"] == torch.nn.functional.gelu)
-  return 0.5f * x * (1.0f + erff(x * 0.70710678118654752440f));
+  // exact-erf GELU (transformers ACT2FN["gelu"] == torch.nn.functional.gelu), erf to 1.5e-7
+  float e;
+  return x * b2p_phi(x, e);
 }
 __device__ __forceinline__ float b2p_gelu_grad(float x) {
-  const float cdf = 0.5f * (1.0f + erff(x * 0.70710678118654752440f));
-  const float pdf = 0.39894228040143267794f * __expf(-0.5f * x * x);
-  return cdf + x * pdf;
+  float e;
+  const float cdf = b2p_phi(x, e);
+  return fmaf(x * 0.39894228040143267794f, e, cdf);   // Phi(x) + x * pdf(x), pdf = e / sqrt(2 pi)
 }
 __device__ __forceinline__ float b2p_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float b2p_silu(float x) { return x * b2p_sigmoid(x); }

@@ -161,6 +161,77 @@ __device__ __forceinline__ bf16x8 frag_t(const char* img, int col0, int kk, int 
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// Epilogue of one 64-row band of a BN-wide output tile, staged in LDS (Cs, row stride BN + 4
+// floats): every thread handles 4 consecutive columns of rows rbase, rbase + RPP, ... (16-B loads /
+// stores of C, bias, aux, residual; 8-B bf16 copies) and accumulates the final values for the fused
+// column sums. UNR = unroll of the row passes (0 = full): the epilogue body (bias, activations,
+// dropout hash, act', residual, bf16 copies) is large, and a fully unrolled 256 x 256 epilogue
+// (4 bands x 8 passes) overflowed the instruction cache (measured ~75k cycles per tile).
+#ifndef B2P_EPI_UNROLL_SMALL
+#define B2P_EPI_UNROLL_SMALL 0   // 0 = full unroll of the row passes
+#endif
+#ifndef B2P_EPI_UNROLL_PP
+#define B2P_EPI_UNROLL_PP 1      // 1 = rolled
+#endif
+template <int BN, int NT, int UNR>
+__device__ __forceinline__ void store_band(const EpiArgs& ea, const float* Cs, int tid, int z, int z1, int z2, int M,
+                                           int N, float* slab, int mband, int n0, float4& csum) {
+  constexpr int CG = BN / 4, RPP = NT / CG, CS_LD = BN + 4;
+  const int cg = tid % CG, rbase = tid / CG;
+  auto pass = [&](int i) {
+    const int rl = rbase + RPP * i;
+    const float4 v = *reinterpret_cast<const float4*>(Cs + rl * CS_LD + 4 * cg);
+    const int m = mband + rl, n = n0 + 4 * cg;
+    if (slab) {
+      if (m < M) {
+        float* dst = slab + (int64_t)m * N + n;
+        if (ea.vec4 && n + 4 <= N) *reinterpret_cast<float4*>(dst) = v;
+        else {
+          if (n < N) dst[0] = v.x;
+          if (n + 1 < N) dst[1] = v.y;
+          if (n + 2 < N) dst[2] = v.z;
+          if (n + 3 < N) dst[3] = v.w;
+        }
+      }
+    } else {
+      const float4 f = epilogue_store4(ea, z, z1, z2, m, n, v);
+      csum.x += f.x; csum.y += f.y; csum.z += f.z; csum.w += f.w;
+    }
+  };
+  if constexpr (UNR == 0) {
+#pragma unroll
+    for (int i = 0; i < 64 / RPP; ++i) pass(i);
+  } else if constexpr (UNR == 1) {
+#pragma clang loop unroll(disable)
+    for (int i = 0; i < 64 / RPP; ++i) pass(i);
+  } else {
+#pragma unroll UNR
+    for (int i = 0; i < 64 / RPP; ++i) pass(i);
+  }
+}
+
+// fused bias-gradient column sums: the RPP threads of each column group add their partial sums
+// (one BM-row tile partial; partial rows are 128-row granular, a 256-row tile zeroes its second row)
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void store_colsum(const EpiArgs& ea, float* Cs, int tid, int tm, int M, int N, int n0,
+                                             float4 csum) {
+  constexpr int CG = BN / 4, RPP = NT / CG, CS_LD = BN + 4;
+  const int cg = tid % CG, rbase = tid / CG;
+  __syncthreads();
+  *reinterpret_cast<float4*>(Cs + rbase * CS_LD + 4 * cg) = csum;
+  __syncthreads();
+  if (tid < BN && n0 + tid < N) {
+    float sacc = 0.f;
+#pragma unroll
+    for (int r = 0; r < RPP; ++r) sacc += Cs[r * CS_LD + tid];
+    const int prow = tm * (BM / 128), nprow = (M + 127) / 128;
+    ea.e.colsum_part[(int64_t)prow * N + n0 + tid] = sacc;
+#pragma unroll
+    for (int r2 = 1; r2 < BM / 128; ++r2)
+      if (prow + r2 < nprow) ea.e.colsum_part[(int64_t)(prow + r2) * N + n0 + tid] = 0.f;
+  }
+}
+
 // Tile configurations: BM x BN output tile, WGM x WGN waves of 64 x 64 each (4 x 4 MFMA tiles),
 // KT-deep k-tiles, S LDS stages (S-1 tiles in flight behind counted vmcnt waits + raw barriers).
 template <int BM_, int BN_, int KT_, int S_>
@@ -269,67 +340,223 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_
     nxt = nxt + 1 == S ? 0 : nxt + 1;
   }
 
-  // epilogue, staged through LDS one 64-row wave band at a time so that every thread then handles
-  // 4 consecutive columns (16-B loads/stores of C, bias, aux, residual; 8-B bf16 copy)
-  constexpr int CG = BN / 4;                 // column groups (4 columns each)
-  constexpr int RPP = NT / CG;               // rows per pass
+  // epilogue, staged through LDS one 64-row wave band at a time
   float* Cs = reinterpret_cast<float*>(smem);
   float* slab = ks > 1 ? d.workspace + ((int64_t)z * ks + ksl) * (int64_t)M * N : nullptr;
-  const int cg = tid % CG, rbase = tid / CG;
   float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);   // fused bias-gradient column sums (colsum_part)
-#pragma clang loop unroll(full)
+#pragma unroll
   for (int band = 0; band < CF::WGM; ++band) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
     if (wm == band) {
-#pragma clang loop unroll(full)
+#pragma unroll
       for (int i = 0; i < 4; ++i)
-#pragma clang loop unroll(full)
+#pragma unroll
         for (int j = 0; j < 4; ++j)
-#pragma clang loop unroll(full)
+#pragma unroll
           for (int r = 0; r < 4; ++r)
             Cs[(i * 16 + (lane >> 4) * 4 + r) * CS_LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
     }
     __syncthreads();
-#pragma clang loop unroll(full)
-    for (int i = 0; i < 64 / RPP; ++i) {
-      const int rl = rbase + RPP * i;
-      const float4 v = *reinterpret_cast<const float4*>(Cs + rl * CS_LD + 4 * cg);
-      const int m = m0 + band * 64 + rl, n = n0 + 4 * cg;
-      if (ks > 1) {
-        if (m < M) {
-          float* dst = slab + (int64_t)m * N + n;
-          if (ea.vec4 && n + 4 <= N) *reinterpret_cast<float4*>(dst) = v;
-          else {
-            if (n < N) dst[0] = v.x;
-            if (n + 1 < N) dst[1] = v.y;
-            if (n + 2 < N) dst[2] = v.z;
-            if (n + 3 < N) dst[3] = v.w;
-          }
-        }
+    store_band<BN, NT, B2P_EPI_UNROLL_SMALL>(ea, Cs, tid, z, z1, z2, M, N, slab, m0 + band * 64, n0, csum);
+  }
+  if (ea.e.colsum_part) store_colsum<BM, BN, NT>(ea, Cs, tid, tm, M, N, n0, csum);
+}
+
+// ------------------------------------------------------------------------------------------------
+// 256 x 256 x 64 ping-pong kernel: 8 waves in two groups of 4 (group g owns output rows
+// 128g .. 128g+127, wave wc of the group columns 64wc .. 64wc+63: a 128 x 64 sub-tile, 8 x 4 MFMA
+// tiles). Every K-tile runs in 4 phases, one output quadrant (64 x 32, K 64 = 16 MFMAs) each:
+//     ds_read this quadrant's fragments, [issue LDS-DMA of the next K-tile], lgkmcnt(0), barrier,
+//     16 MFMAs, barrier.
+// Group 1 starts one barrier later than group 0, so on every SIMD (one wave of each group) one wave
+// feeds the matrix pipe while its partner reads fragments and issues DMA. Two LDS buffers: tile
+// kt+1 is DMA'd into the idle buffer in phases 0 (A) and 1 (B) of tile kt and waited for
+// (vmcnt(0)) in phase 3 before that phase's first barrier, so every reader of tile kt+1 passes a
+// barrier after every issuer's wait. Every fragment read is retired (lgkmcnt(0)) before the
+// phase's first barrier, so the buffer a DMA overwrites has no read in flight (WAR).
+#ifdef B2P_PP_STAMPS   // diagnostic build only (tools/pp_probe.hip): per-workgroup clock stamps
+__device__ unsigned long long g_pp_stamps[8 * 8192];
+#define PP_STAMP(k)                                                                          \
+  do {                                                                                       \
+    if (tid == 0 && blockIdx.x < 8192) {                                                     \
+      g_pp_stamps[(size_t)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime();              \
+      g_pp_stamps[(size_t)blockIdx.x * 8 + 4 + (k)] = __builtin_amdgcn_s_memrealtime();      \
+    }                                                                                        \
+  } while (0)
+#else
+#define PP_STAMP(k)
+#endif
+
+constexpr int PP_NT = 512;
+constexpr int PP_KT = 64;
+constexpr int PP_ABYTES = 256 * PP_KT * 2;              // 32 KB per operand per buffer
+constexpr int PP_STAGE = 2 * PP_ABYTES;
+constexpr int PP_LDS = 2 * PP_STAGE;                    // 128 KB
+constexpr int PP_CS_LD = 256 + 4;
+
+__device__ __forceinline__ void pp_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+__device__ __forceinline__ void pp_lgkm0() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool AK, bool BK>
+__global__ void __launch_bounds__(PP_NT, 1) gemm16_pp_kernel(const b2p_gemm_desc d, const EpiArgs ea, int tiles_m,
+                                                            int tiles_n) {
+  using SA = Src<256, PP_KT, AK, false, 8>;
+  using SB = Src<256, PP_KT, BK, false, 8>;
+  __shared__ __attribute__((aligned(1024))) char smem[PP_LDS];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int g = wave >> 2, wc = wave & 3;
+  PP_STAMP(0);
+
+  const int nwg = gridDim.x;
+  const int orig = blockIdx.x;
+  const int xcd = orig & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (orig >> 3);
+  const int tiles = tiles_m * tiles_n;
+  const int zz = wgid / tiles;
+  const int t = wgid - zz * tiles;
+  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+
+  const int ks = d.ksplit > 1 ? d.ksplit : 1;
+  const int z = zz / ks, ksl = zz - z * ks;
+  const int z1 = z / d.nz2, z2 = z - z1 * d.nz2;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int M = (int)d.M, N = (int)d.N;
+  const int kchunk = ks > 1 ? (int)d.kchunk : (int)d.K;
+  const int kbeg = ksl * kchunk;
+  const int K = ((int)d.K < kbeg + kchunk) ? (int)d.K : kbeg + kchunk;
+  const int nk = K > kbeg ? (K - kbeg + PP_KT - 1) / PP_KT : 0;
+
+  SA sa;
+  SB sb;
+  sa.init(d.A, z1, z2, wave, lane, m0, M, kbeg);
+  sb.init(d.B, z1, z2, wave, lane, n0, N, kbeg);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) {
+    sa.issue(smem, wave, kbeg, K);
+    sb.issue(smem + PP_ABYTES, wave, kbeg, K);
+  }
+  wait_vm<0>();
+  pp_barrier();
+  if (g == 1) pp_barrier();   // the stagger
+  PP_STAMP(1);
+
+  bf16x8 a[4][2], b[2][2];
+  const int arow = g * 128, bcol = wc * 64;
+  auto readA = [&](const char* As, int mi) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        a[i][kk] = AK ? frag_k<PP_KT>(As, arow + mi * 64 + i * 16, kk, lane)
+                      : frag_t<256>(As, arow + mi * 64 + i * 16, kk, lane);
+  };
+  auto readB = [&](const char* Bs, int nj) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+        b[j][kk] = BK ? frag_k<PP_KT>(Bs, bcol + nj * 32 + j * 16, kk, lane)
+                      : frag_t<256>(Bs, bcol + nj * 32 + j * 16, kk, lane);
+  };
+  auto mfma = [&](int mi, int nj) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          acc[mi * 4 + i][nj * 2 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][kk], b[j][kk], acc[mi * 4 + i][nj * 2 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const char* As = smem + (kt & 1) * PP_STAGE;
+    const char* Bs = As + PP_ABYTES;
+    char* nx = smem + ((kt + 1) & 1) * PP_STAGE;
+    const bool more = kt + 1 < nk;
+    const int knext = kbeg + (kt + 1) * PP_KT;
+    // phase 0: quadrant (0, 0); DMA A of tile kt+1
+    readA(As, 0);
+    readB(Bs, 0);
+    if (more) sa.issue(nx, wave, knext, K);
+    pp_lgkm0();
+    pp_barrier();
+    mfma(0, 0);
+    pp_barrier();
+    // phase 1: quadrant (0, 1); DMA B of tile kt+1
+    readB(Bs, 1);
+    if (more) sb.issue(nx + PP_ABYTES, wave, knext, K);
+    pp_lgkm0();
+    pp_barrier();
+    mfma(0, 1);
+    pp_barrier();
+    // phase 2: quadrant (1, 1)
+    readA(As, 1);
+    pp_lgkm0();
+    pp_barrier();
+    mfma(1, 1);
+    pp_barrier();
+    // phase 3: quadrant (1, 0); tile kt+1 must have landed before this phase's first barrier
+    readB(Bs, 0);
+    wait_vm<0>();
+    pp_lgkm0();
+    pp_barrier();
+    mfma(1, 0);
+    pp_barrier();
+  }
+  if (g == 0) pp_barrier();   // equal barrier counts for both groups
+  PP_STAMP(2);
+
+  // epilogue: four 64-row bands through LDS (band = 2 * group + row half)
+  float* Cs = reinterpret_cast<float*>(smem);
+  float* slab = ks > 1 ? d.workspace + ((int64_t)z * ks + ksl) * (int64_t)M * N : nullptr;
+  float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma clang loop unroll(disable)
+  for (int band = 0; band < 4; ++band) {
+    __syncthreads();
+    if (g == (band >> 1)) {
+      if (band & 1) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              Cs[(i * 16 + (lane >> 4) * 4 + r) * PP_CS_LD + wc * 64 + j * 16 + (lane & 15)] = acc[4 + i][j][r];
       } else {
-        const float4 f = epilogue_store4(ea, z, z1, z2, m, n, v);
-        csum.x += f.x; csum.y += f.y; csum.z += f.z; csum.w += f.w;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              Cs[(i * 16 + (lane >> 4) * 4 + r) * PP_CS_LD + wc * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
       }
     }
-  }
-  if (ea.e.colsum_part) {
-    // the RPP threads of a column group add their rows: one BM-row tile partial
     __syncthreads();
-    *reinterpret_cast<float4*>(Cs + rbase * CS_LD + 4 * cg) = csum;
-    __syncthreads();
-    if (tid < BN && n0 + tid < N) {
-      float sacc = 0.f;
-#pragma unroll
-      for (int r = 0; r < RPP; ++r) sacc += Cs[r * CS_LD + tid];
-      // partial rows are 128-row granular: a BM-row tile fills its first row, zeroes the others
-      const int prow = tm * (BM / 128), nprow = (M + 127) / 128;
-      ea.e.colsum_part[(int64_t)prow * N + n0 + tid] = sacc;
-#pragma unroll
-      for (int r2 = 1; r2 < BM / 128; ++r2)
-        if (prow + r2 < nprow) ea.e.colsum_part[(int64_t)(prow + r2) * N + n0 + tid] = 0.f;
-    }
+    store_band<256, PP_NT, B2P_EPI_UNROLL_PP>(ea, Cs, tid, z, z1, z2, M, N, slab, m0 + band * 64, n0, csum);
   }
+  if (ea.e.colsum_part) store_colsum<256, 256, PP_NT>(ea, Cs, tid, tm, M, N, n0, csum);
+  PP_STAMP(3);
 }
 
 }  // namespace
@@ -365,6 +592,23 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   if (big) {
     const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 127) / 128);
     launch_cfg<CfgBig>(d, ea, st, dim3((unsigned)((int64_t)tm * tn)), tm, tn);
+    return 0;
+  }
+  // 256 x 256 ping-pong tile (B2P_GEMM16_PP: 0 off, 1 (default) for long-K launches whose grid fills
+  // most of the chip, 2 always for plain operands). One workgroup per CU cannot hide its epilogue
+  // behind another tile's K loop, so at K <= 1024 (the encoder's projections, 2-3 tiles per CU
+  // with the 128 x 128 kernel) it measured slower; at K >= 2048 its K loop (~1.0 PF) wins.
+  static int pp_mode = getenv("B2P_GEMM16_PP") ? atoi(getenv("B2P_GEMM16_PP")) : 1;
+  const int64_t tiles_pp = ((d.M + 255) / 256) * ((d.N + 255) / 256) * nz;
+  const int64_t kper = ks > 1 ? (int64_t)d.kchunk : d.K;
+  const bool pp = !d.A.conv && (pp_mode == 2 || (pp_mode == 1 && tiles_pp >= 192 && kper >= 2048));
+  if (pp) {
+    const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 255) / 256);
+    const dim3 grid((unsigned)tiles_pp), block(PP_NT);
+    const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
+    if (AK && BK) hipLaunchKernelGGL((gemm16_pp_kernel<true, true>), grid, block, 0, st, d, ea, tm, tn);
+    else if (AK) hipLaunchKernelGGL((gemm16_pp_kernel<true, false>), grid, block, 0, st, d, ea, tm, tn);
+    else hipLaunchKernelGGL((gemm16_pp_kernel<false, false>), grid, block, 0, st, d, ea, tm, tn);
     return 0;
   }
   const int tm = (int)((d.M + 127) / 128), tn = (int)((d.N + 127) / 128);
