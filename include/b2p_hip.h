@@ -115,6 +115,14 @@ typedef struct {
 
 int b2p_gemm(const b2p_gemm_desc* d, b2p_stream_t stream);
 
+/* ------------------------------------------------------------------ graph-replayed steps
+ * A training step captured once as a HIP graph (train/step_graph.py) replays with host values
+ * frozen. Dropout: every kernel adds (*dev_counter) * 0x9E3779B97F4A7C15 to its host-drawn seed
+ * when a counter is set (NULL restores eager semantics); b2p_seed_epoch_step increments it (the
+ * captured step's first node), so each replay draws new masks. */
+int b2p_set_seed_epoch(const uint64_t* dev_counter);
+int b2p_seed_epoch_step(uint64_t* dev_counter, b2p_stream_t stream);
+
 /* ------------------------------------------------------------------ elementwise / reductions */
 /* column sums over rows: out[n] (+)= sum_m X[m*ld + n]; used for bias grads. partial must hold
  * ceil(M/rows_per_block)*N floats (see b2p_colsum_workspace). */
@@ -291,6 +299,20 @@ int b2p_ctc_fwd_bwd(const float* logits, const int64_t* targets, const int32_t* 
 int b2p_adam_multi(const int64_t* table, int ntensors, int64_t max_numel, float lr, float beta1,
                    float beta2, float eps, float weight_decay, float bias_c1, float bias_c2_sqrt,
                    b2p_stream_t stream);
+/* the same update with lr read from lr_dev[0] and the step counter step_dev[0] (double) incremented
+ * and turned into the bias corrections on the device (hyper_dev: float[3] scratch): replayable in a
+ * captured step (torch.optim.Adam capturable=True semantics) */
+int b2p_adam_multi_dev(const int64_t* table, int ntensors, int64_t max_numel, const float* lr_dev, float beta1,
+                       float beta2, float eps, float weight_decay, double* step_dev, float* hyper_dev,
+                       b2p_stream_t stream);
+/* the update with the tensor records {param, grad, exp_avg, exp_avg_sq, numel} read from HOST
+ * memory by the launcher and passed in the kernel arguments (48 tensors per launch): no device
+ * table to upload, so it is also capturable. step_dev == NULL: host lr / bias corrections;
+ * otherwise the device form of b2p_adam_multi_dev, its bias corrections formed in double from the
+ * double betas exactly as the host computes them for torch.optim.Adam. */
+int b2p_adam_recs(const int64_t* recs, int ntensors, float lr, double beta1, double beta2, float eps,
+                  float weight_decay, float bias_c1, float bias_c2_sqrt, const float* lr_dev, double* step_dev,
+                  float* hyper_dev, b2p_stream_t stream);
 
 /* dropout with an extra output scale: y = x * keep(seed, i) * scale / (1-p) (macaron half-step) */
 int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t seed, float scale,

@@ -481,3 +481,39 @@ def test_encoder_layer_bf16_operands_match_fp32_path():
         assert torch.equal(Fn.weight16(w), w16a)          # torch cannot see it ...
         Fn.bump_param_epoch([w])
         assert torch.equal(Fn.weight16(w), w.to(torch.bfloat16))   # ... the epoch bump can
+
+
+def test_dropout_seed_epoch_counter():
+    """Graph-replay seed counter (b2p_set_seed_epoch): counter 0 reproduces the eager mask, every
+    b2p_seed_epoch_step gives a new mask, NULL restores eager semantics; the GEMM epilogue and the
+    stand-alone dropout kernel see the same counter."""
+    import ctypes
+    Fn = _fn()
+    lib = Fn._lib.load()
+    x = torch.ones(1 << 16, device="cuda")
+
+    def mask():
+        y = torch.empty_like(x)
+        Fn._lib.call("b2p_dropout", x.data_ptr(), y.data_ptr(), x.numel(), 0.5, 1234, Fn._st())
+        return y != 0
+
+    def gemm_mask():
+        a = torch.ones(256, 64, device="cuda", dtype=torch.bfloat16)
+        w = torch.ones(128, 64, device="cuda", dtype=torch.bfloat16)
+        out = torch.empty(256, 128, device="cuda")
+        Fn.gemm(256, 128, 64, Fn.op(a, 0, 64, True), Fn.op(w, 0, 64, True), out, 128, drop_p=0.5, seed=77)
+        return out != 0
+
+    m0, g0 = mask(), gemm_mask()
+    ctr = torch.zeros(1, dtype=torch.int64, device="cuda")
+    try:
+        Fn._lib.check(lib.b2p_set_seed_epoch(ctypes.c_void_p(ctr.data_ptr())), "set_seed_epoch")
+        assert torch.equal(mask(), m0) and torch.equal(gemm_mask(), g0)
+        Fn._lib.check(lib.b2p_seed_epoch_step(ctypes.c_void_p(ctr.data_ptr()), ctypes.c_void_p(Fn._st())), "step")
+        m1, g1 = mask(), gemm_mask()
+        assert int(ctr.item()) == 1
+        assert not torch.equal(m1, m0) and not torch.equal(g1, g0)
+        assert abs(m1.float().mean().item() - 0.5) < 0.02
+    finally:
+        Fn._lib.check(lib.b2p_set_seed_epoch(None), "set_seed_epoch")
+    assert torch.equal(mask(), m0)

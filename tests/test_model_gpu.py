@@ -155,3 +155,60 @@ def test_deferred_frozen_wgrad_matches_immediate():
     for n in a:
         d = float((a[n] - b[n]).norm())
         assert d <= 1e-5 * float(a[n].norm()) + 1e-7, n
+
+
+def test_step_graph_replay_matches_eager():
+    """A whole bf16 training step (forward, CTC, backward, side-stream frozen-weight gradients, Adam)
+    captured as a HIP graph and replayed (train/step_graph.py) gives the same losses, parameters and
+    accumulated frozen-weight gradients as the same number of eager steps (dropout off)."""
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.optim import HipAdam
+    from wav2vec2forbrain_amd.train.step_graph import StepGraph
+    cfg = CFG["plumbing_base"]
+    res = []
+    for graph in (False, True):
+        model = build_model(cfg)
+        model.train()
+        for m in model.modules():
+            if hasattr(m, "sync_metrics"):
+                m.sync_metrics = False
+        opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
+        frozen = [p for n, p in model.named_parameters() if not n.startswith("brain_encoder.")]
+        Fn.set_deferred_wgrad(frozen)
+        batch = _batch(cfg)
+
+        def step():
+            opt.zero_grad()
+            out = model(batch)
+            out.loss.backward()
+            Fn.join_wgrad()
+            opt.step()
+            return out.metrics["ctc_loss"]
+
+        with Fn.precision("bf16"):
+            if graph:
+                sg = StepGraph(step, opt, warmup=2)
+                sg.capture()
+                losses = [sg.replay().clone() for _ in range(3)]
+                torch.cuda.synchronize()
+                sg.release()
+            else:
+                losses = [step() for _ in range(5)][2:]
+        torch.cuda.synchronize()
+        res.append((torch.stack(losses).float().cpu(),
+                    {n: p.detach().clone() for n, p in model.named_parameters()},
+                    {n: p.grad.detach().clone() for n, p in model.named_parameters()
+                     if not n.startswith("brain_encoder.") and p.grad is not None},
+                    {n: float(opt.state[p]["step"]) for n, p in model.brain_encoder.named_parameters()
+                     if len(opt.state[p])}))
+        Fn.set_deferred_wgrad([])
+    (la, pa, ga, sa), (lb, pb, gb, sb) = res
+    assert torch.allclose(la, lb, rtol=1e-5, atol=0), (la, lb)
+    assert sa == sb and set(sa.values()) == {5.0}
+    for n in pa:
+        d = float((pa[n] - pb[n]).norm())
+        assert d <= 1e-5 * float(pa[n].norm()) + 1e-7, n
+    assert set(ga) == set(gb) and len(ga) > 0
+    for n in ga:
+        d = float((ga[n] - gb[n]).norm())
+        assert d <= 1e-5 * float(ga[n].norm()) + 1e-7, n

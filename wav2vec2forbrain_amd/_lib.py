@@ -102,6 +102,10 @@ _SIGS = {
     "b2p_ctc_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "b2p_ctc_fwd_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "b2p_adam_multi": (c_i32, [c_p, c_i32, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_p]),
+    "b2p_adam_multi_dev": (c_i32, [c_p, c_i32, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_p]),
+    "b2p_adam_recs": (c_i32, [c_p, c_i32, c_f32, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_p, c_p]),
+    "b2p_set_seed_epoch": (c_i32, [c_p]),
+    "b2p_seed_epoch_step": (c_i32, [c_p, c_p]),
     "b2p_dropout_scaled": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_f32, c_p]),
     "b2p_rotary": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_glu_fwd": (c_i32, [c_p, c_p, c_i64, c_i64, c_p]),

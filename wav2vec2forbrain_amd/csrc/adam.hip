@@ -12,8 +12,62 @@ constexpr int NTH = 256;
 constexpr int PER_THREAD = 4;
 
 __global__ void __launch_bounds__(NTH) adam_k(const int64_t* __restrict__ table, float lr, float b1, float b2,
-                                              float eps, float wd, float bc1, float bc2s) {
+                                              float eps, float wd, float bc1, float bc2s,
+                                              const float* __restrict__ hyper) {
+  if (hyper) {   // graph-replayable form: lr and the bias corrections live on the device
+    lr = hyper[0];
+    bc1 = hyper[1];
+    bc2s = hyper[2];
+  }
   const int64_t* rec = table + 5 * (int64_t)blockIdx.y;
+  float* __restrict__ p = reinterpret_cast<float*>(rec[0]);
+  const float* __restrict__ g = reinterpret_cast<const float*>(rec[1]);
+  float* __restrict__ m = reinterpret_cast<float*>(rec[2]);
+  float* __restrict__ v = reinterpret_cast<float*>(rec[3]);
+  const int64_t n = rec[4];
+  const float step = lr / bc1;
+  const int64_t stride = (int64_t)gridDim.x * NTH;
+  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += stride) {
+    float gi = g[i];
+    const float pi = p[i];
+    if (wd != 0.f) gi += wd * pi;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    float vi = v[i];
+    vi = b2 * vi + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    p[i] = pi - step * (mi / denom);
+  }
+}
+// one thread: the step counter of a parameter group and its bias corrections (double, as the host
+// computes them for torch.optim.Adam), for a step captured in a graph
+__global__ void adam_hyper_k(double* __restrict__ st, const float* __restrict__ lr, double b1, double b2,
+                             float* __restrict__ hyper) {
+  const double t = st[0] + 1.0;
+  st[0] = t;
+  hyper[0] = lr[0];
+  hyper[1] = (float)(1.0 - pow(b1, t));
+  hyper[2] = (float)sqrt(1.0 - pow(b2, t));
+}
+
+__global__ void epoch_step_k(uint64_t* c) { c[0] += 1; }
+
+// the same update with the tensor records passed by value in the kernel arguments (no device table:
+// nothing to upload, and a captured graph keeps the records in its kernel node)
+constexpr int ADAM_MAXR = 48;
+struct AdamRecs {
+  int64_t r[ADAM_MAXR][5];   // param, grad, exp_avg, exp_avg_sq, numel
+};
+__global__ void __launch_bounds__(NTH) adam_rec_k(const AdamRecs recs, float lr, float b1, float b2, float eps,
+                                                  float wd, float bc1, float bc2s, const float* __restrict__ hyper) {
+  if (hyper) {
+    lr = hyper[0];
+    bc1 = hyper[1];
+    bc2s = hyper[2];
+  }
+  const int64_t* rec = recs.r[blockIdx.y];
   float* __restrict__ p = reinterpret_cast<float*>(rec[0]);
   const float* __restrict__ g = reinterpret_cast<const float*>(rec[1]);
   float* __restrict__ m = reinterpret_cast<float*>(rec[2]);
@@ -37,6 +91,58 @@ __global__ void __launch_bounds__(NTH) adam_k(const int64_t* __restrict__ table,
 }
 }  // namespace
 
+extern "C" int b2p_seed_epoch_step(uint64_t* dev_counter, b2p_stream_t stream) {
+  B2P_CHECK_ARG(dev_counter != nullptr, "seed_epoch_step: NULL counter");
+  hipLaunchKernelGGL(epoch_step_k, dim3(1), dim3(1), 0, (hipStream_t)stream, dev_counter);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_adam_recs(const int64_t* recs, int ntensors, float lr, double beta1, double beta2, float eps,
+                             float weight_decay, float bias_c1, float bias_c2_sqrt, const float* lr_dev,
+                             double* step_dev, float* hyper_dev, b2p_stream_t stream) {
+  B2P_CHECK_ARG(recs != nullptr || ntensors == 0, "adam_recs: NULL records");
+  B2P_CHECK_ARG(ntensors >= 0, "adam_recs: bad tensor count");
+  const bool dev = step_dev != nullptr;
+  B2P_CHECK_ARG(!dev || (lr_dev && hyper_dev), "adam_recs: device form needs lr_dev, step_dev and hyper_dev");
+  B2P_CHECK_ARG(dev || (bias_c1 > 0.f && bias_c2_sqrt > 0.f), "adam: bias corrections must be positive");
+  hipStream_t st = (hipStream_t)stream;
+  if (dev) hipLaunchKernelGGL(adam_hyper_k, dim3(1), dim3(1), 0, st, step_dev, lr_dev, beta1, beta2, hyper_dev);
+  const float b1f = (float)beta1, b2f = (float)beta2;
+  for (int c0 = 0; c0 < ntensors; c0 += ADAM_MAXR) {
+    const int nc = ntensors - c0 < ADAM_MAXR ? ntensors - c0 : ADAM_MAXR;
+    AdamRecs a;
+    int64_t maxn = 0;
+    for (int i = 0; i < nc; ++i) {
+      for (int k = 0; k < 5; ++k) a.r[i][k] = recs[5 * (c0 + i) + k];
+      maxn = a.r[i][4] > maxn ? a.r[i][4] : maxn;
+    }
+    if (maxn <= 0) continue;
+    int64_t bx = (maxn + (int64_t)NTH * PER_THREAD - 1) / ((int64_t)NTH * PER_THREAD);
+    if (bx > 4096) bx = 4096;
+    hipLaunchKernelGGL(adam_rec_k, dim3((unsigned)bx, (unsigned)nc), dim3(NTH), 0, st, a, lr, b1f, b2f, eps,
+                       weight_decay, bias_c1, bias_c2_sqrt, dev ? (const float*)hyper_dev : nullptr);
+  }
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_adam_multi_dev(const int64_t* table, int ntensors, int64_t max_numel, const float* lr_dev,
+                                  float beta1, float beta2, float eps, float weight_decay, double* step_dev,
+                                  float* hyper_dev, b2p_stream_t stream) {
+  B2P_CHECK_ARG(table && lr_dev && step_dev && hyper_dev, "adam_dev: NULL pointer");
+  B2P_CHECK_ARG(ntensors >= 0 && ntensors < 65536, "adam: bad tensor count");
+  hipLaunchKernelGGL(adam_hyper_k, dim3(1), dim3(1), 0, (hipStream_t)stream, step_dev, lr_dev, (double)beta1,
+                     (double)beta2, hyper_dev);
+  if (ntensors == 0 || max_numel <= 0) return 0;
+  int64_t bx = (max_numel + (int64_t)NTH * PER_THREAD - 1) / ((int64_t)NTH * PER_THREAD);
+  if (bx > 4096) bx = 4096;
+  hipLaunchKernelGGL(adam_k, dim3((unsigned)bx, (unsigned)ntensors), dim3(NTH), 0, (hipStream_t)stream, table, 0.f,
+                     beta1, beta2, eps, weight_decay, 1.f, 1.f, (const float*)hyper_dev);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int b2p_adam_multi(const int64_t* table, int ntensors, int64_t max_numel, float lr, float beta1,
                               float beta2, float eps, float weight_decay, float bias_c1, float bias_c2_sqrt,
                               b2p_stream_t stream) {
@@ -47,7 +153,7 @@ extern "C" int b2p_adam_multi(const int64_t* table, int ntensors, int64_t max_nu
   int64_t bx = (max_numel + (int64_t)NTH * PER_THREAD - 1) / ((int64_t)NTH * PER_THREAD);
   if (bx > 4096) bx = 4096;
   hipLaunchKernelGGL(adam_k, dim3((unsigned)bx, (unsigned)ntensors), dim3(NTH), 0, (hipStream_t)stream, table, lr,
-                     beta1, beta2, eps, weight_decay, bias_c1, bias_c2_sqrt);
+                     beta1, beta2, eps, weight_decay, bias_c1, bias_c2_sqrt, (const float*)nullptr);
   B2P_CHECK_LAUNCH();
   return 0;
 }

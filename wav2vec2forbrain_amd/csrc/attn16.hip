@@ -90,7 +90,8 @@ __device__ __forceinline__ void block_coords(int& xb, int& h, int& b) {
 struct DropCfg {
   uint64_t seed;
   uint32_t thr;
-  float scale;   // 1 / (1 - p)
+  float scale;                // 1 / (1 - p)
+  const uint64_t* epoch;      // graph-replay seed offset (b2p_seed_eff), NULL in eager launches
 };
 template <bool DROP>
 __device__ __forceinline__ float keep_scale(const DropCfg& dc, uint64_t idx) {
@@ -103,6 +104,8 @@ __device__ __forceinline__ float keep_scale(const DropCfg& dc, uint64_t idx) {
 template <bool DROP>
 __global__ void __launch_bounds__(256) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
                                                     float* __restrict__ lse2, int T, int nh, float scale, DropCfg dc) {
+  dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
+  dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
   char* Vimg = smem + TMAX * 128;
@@ -194,6 +197,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
                                                         const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                         float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
                                                         int nh, float scale, DropCfg dc) {
+  dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Qimg = smem;
   char* dOimg = smem + TMAX * 128;
@@ -280,6 +284,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
                                                        const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                        float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
                                                        int nh, float scale, DropCfg dc) {
+  dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
   char* Vimg = smem + TMAX * 128;
@@ -355,6 +360,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
 
 DropCfg drop_cfg(float p, uint64_t seed) {
   DropCfg d;
+  d.epoch = b2p_seed_epoch();
   d.seed = seed;
   d.thr = b2p_dropout_threshold(p);
   d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;

@@ -25,6 +25,8 @@ __device__ __forceinline__ float b2p_bf16_to_f32(uint16_t b) {
 // error reporting: every C-ABI entry returns 0 on success, nonzero on failure
 // and leaves a message retrievable through b2p_last_error().
 // ---------------------------------------------------------------------------
+// device counter added to every dropout seed (NULL: none); set by b2p_set_seed_epoch (lib.cpp)
+const uint64_t* b2p_seed_epoch();
 void b2p_set_error(const char* fmt, ...);
 
 #define B2P_CHECK_ARG(cond, ...)                 \
@@ -102,6 +104,12 @@ __device__ __forceinline__ uint32_t b2p_hash(uint64_t seed, uint64_t idx) {
   return b2p_mix32(b2p_mix32((uint32_t)idx ^ k) + (uint32_t)(idx >> 32) * 0x85EBCA6Bu + k);
 }
 // keep-probability threshold: keep iff hash >= thr, thr = round(p * 2^32)
+// Graph-replayed steps: the host-drawn seed of every dropout call is offset by a device-resident
+// step counter (b2p_set_seed_epoch), so a captured step draws new masks on every replay. NULL (the
+// eager default) leaves the seed unchanged.
+__device__ __forceinline__ uint64_t b2p_seed_eff(uint64_t seed, const uint64_t* epoch) {
+  return epoch ? seed + 0x9E3779B97F4A7C15ull * (*epoch) : seed;
+}
 __device__ __forceinline__ bool b2p_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
   return b2p_hash(seed, idx) >= thr;
 }

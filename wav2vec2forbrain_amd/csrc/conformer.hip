@@ -213,9 +213,10 @@ __global__ void bn_gxhat_k(const float* __restrict__ g, const float* __restrict_
 }
 
 __global__ void dropout_scale_k(const float* __restrict__ x, float* __restrict__ y, int64_t n, uint32_t thr,
-                                float scale, uint64_t seed, int use_mask) {
+                                float scale, uint64_t seed, int use_mask, const uint64_t* __restrict__ epoch) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  seed = b2p_seed_eff(seed, epoch);
   y[i] = (!use_mask || b2p_keep(seed, (uint64_t)i, thr)) ? x[i] * scale : 0.f;
 }
 }  // namespace
@@ -355,7 +356,8 @@ extern "C" int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, 
   B2P_CHECK_ARG(p >= 0.f && p < 1.f, "dropout_scaled: p in [0,1)");
   if (n <= 0) return 0;
   hipLaunchKernelGGL(dropout_scale_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, y, n,
-                     b2p_dropout_threshold(p), p > 0.f ? scale / (1.f - p) : scale, seed, p > 0.f ? 1 : 0);
+                     b2p_dropout_threshold(p), p > 0.f ? scale / (1.f - p) : scale, seed, p > 0.f ? 1 : 0,
+                     b2p_seed_epoch());
   B2P_CHECK_LAUNCH();
   return 0;
 }

@@ -122,9 +122,10 @@ namespace {
 
 // ------------------------------------------------------------------ dropout
 __global__ void dropout_k(const float* __restrict__ x, float* __restrict__ y, int64_t n, uint32_t thr,
-                          float scale, uint64_t seed) {
+                          float scale, uint64_t seed, const uint64_t* __restrict__ epoch) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
+  seed = b2p_seed_eff(seed, epoch);
   y[i] = b2p_keep(seed, (uint64_t)i, thr) ? x[i] * scale : 0.f;
 }
 
@@ -135,7 +136,9 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
                                                 const float* __restrict__ beta, float* __restrict__ y,
                                                 float* __restrict__ mean, float* __restrict__ rstd,
                                                 int64_t rows, int cols, float eps, uint32_t thr, float dscale,
-                                                uint64_t seed, float drop_p, uint16_t* __restrict__ y16) {
+                                                uint64_t seed, float drop_p, uint16_t* __restrict__ y16,
+                                                const uint64_t* __restrict__ epoch) {
+  seed = b2p_seed_eff(seed, epoch);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -194,7 +197,9 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
                                                 const float* __restrict__ dx_accum, float* __restrict__ part,
                                                 int64_t rows, int cols, uint32_t thr, float dscale, uint64_t seed,
                                                 float drop_p, float* __restrict__ dxd, uint32_t thr2, float dscale2,
-                                                uint64_t seed2, uint16_t* __restrict__ d16) {
+                                                uint64_t seed2, uint16_t* __restrict__ d16, const uint64_t* __restrict__ epoch) {
+  seed = b2p_seed_eff(seed, epoch);
+  seed2 = b2p_seed_eff(seed2, epoch);
   __shared__ float red[4][3][LN_MAXV * 256];   // cols <= 1024
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nv = cols >> 2;
@@ -295,7 +300,9 @@ __global__ void ln_bwd_scatter(const float* __restrict__ red3, int cols, float* 
 constexpr int SM_MAXE = 8;
 __global__ void __launch_bounds__(256) softmax_fwd_k(const float* __restrict__ S, float* __restrict__ P,
                                                      float* __restrict__ Pd, int64_t rows, int n, int64_t ld,
-                                                     uint32_t thr, float dscale, uint64_t seed, float drop_p) {
+                                                     uint32_t thr, float dscale, uint64_t seed, float drop_p,
+                                                     const uint64_t* __restrict__ epoch) {
+  seed = b2p_seed_eff(seed, epoch);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -336,7 +343,9 @@ __global__ void __launch_bounds__(256) softmax_fwd_k(const float* __restrict__ S
 
 __global__ void __launch_bounds__(256) softmax_bwd_k(const float* __restrict__ P, const float* __restrict__ dPd,
                                                      float* __restrict__ dS, int64_t rows, int n, int64_t ld,
-                                                     uint32_t thr, float dscale, uint64_t seed, float drop_p) {
+                                                     uint32_t thr, float dscale, uint64_t seed, float drop_p,
+                                                     const uint64_t* __restrict__ epoch) {
+  seed = b2p_seed_eff(seed, epoch);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -511,7 +520,7 @@ extern "C" int b2p_dropout(const float* x, float* y, int64_t n, float p, uint64_
   B2P_CHECK_ARG(p >= 0.f && p < 1.f, "dropout: p must be in [0,1)");
   if (n <= 0) return 0;
   hipLaunchKernelGGL(dropout_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, x, y, n,
-                     b2p_dropout_threshold(p), p > 0.f ? 1.f / (1.f - p) : 1.f, seed);
+                     b2p_dropout_threshold(p), p > 0.f ? 1.f / (1.f - p) : 1.f, seed, b2p_seed_epoch());
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -525,7 +534,7 @@ extern "C" int b2p_layernorm_fwd16(const float* x, const float* gamma, const flo
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(ln_fwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, y,
                      mean, rstd, rows, (int)cols, eps, b2p_dropout_threshold(drop_p),
-                     drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, drop_seed, drop_p, y16);
+                     drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f, drop_seed, drop_p, y16, b2p_seed_epoch());
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -555,7 +564,7 @@ extern "C" int b2p_layernorm_bwd16(const float* dy, const float* x, const float*
   hipLaunchKernelGGL(ln_bwd_k, dim3(nblk), dim3(256), 0, st, dy, x, gamma, mean, rstd, dx, dx_accum, workspace,
                      rows, (int)cols, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
                      drop_seed, drop_p, dx_dropped, b2p_dropout_threshold(in_drop_p),
-                     in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed, d16);
+                     in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed, d16, b2p_seed_epoch());
   // partials [nblk][3][cols] -> [3][cols] with the parallel two-phase column sum, then scatter
   float* red3 = workspace + (int64_t)nblk * 3 * cols;
   float* part2 = red3 + 3 * cols;
@@ -629,7 +638,7 @@ extern "C" int b2p_softmax_fwd(const float* S, float* P, float* Pd, int64_t rows
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(softmax_fwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, S, P, Pd, rows,
                      (int)n, ld, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
-                     drop_seed, drop_p);
+                     drop_seed, drop_p, b2p_seed_epoch());
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -641,7 +650,7 @@ extern "C" int b2p_softmax_bwd(const float* P, const float* dPd, float* dS, int6
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(softmax_bwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, P, dPd, dS, rows,
                      (int)n, ld, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
-                     drop_seed, drop_p);
+                     drop_seed, drop_p, b2p_seed_epoch());
   B2P_CHECK_LAUNCH();
   return 0;
 }

@@ -27,6 +27,7 @@ struct EpiArgs {
   uint32_t drop_thr;
   float drop_scale;
   int32_t vec4;   // every C-shaped tensor allows 16-B (C16: 8-B) accesses at n % 4 == 0
+  const uint64_t* epoch;   // graph-replay dropout seed offset (b2p_seed_eff)
 };
 
 __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, int z2, int m, int n,
@@ -41,7 +42,7 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, 
   v = apply_act(v, e.act);
   if (e.drop_p > 0.0f) {
     const uint64_t idx = ((uint64_t)z * (uint64_t)a.M + (uint64_t)m) * (uint64_t)a.N + (uint64_t)n;
-    v = b2p_keep(e.drop_seed, idx, a.drop_thr) ? v * a.drop_scale : 0.0f;
+    v = b2p_keep(b2p_seed_eff(e.drop_seed, a.epoch), idx, a.drop_thr) ? v * a.drop_scale : 0.0f;
   }
   if (e.act_bwd != B2P_ACT_NONE) {
     const float x = e.aux[(int64_t)z1 * e.abs1 + (int64_t)z2 * e.abs2 + (int64_t)m * e.ldaux + n];
@@ -83,8 +84,9 @@ __device__ __forceinline__ float4 epilogue_store4(const EpiArgs& a, int z, int z
   }
   if (e.drop_p > 0.0f) {
     const uint64_t idx = ((uint64_t)z * (uint64_t)a.M + (uint64_t)m) * (uint64_t)a.N + (uint64_t)n;
+    const uint64_t sd = b2p_seed_eff(e.drop_seed, a.epoch);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = b2p_keep(e.drop_seed, idx + q, a.drop_thr) ? v[q] * a.drop_scale : 0.0f;
+    for (int q = 0; q < 4; ++q) v[q] = b2p_keep(sd, idx + q, a.drop_thr) ? v[q] * a.drop_scale : 0.0f;
   }
   if (e.act_bwd != B2P_ACT_NONE) {
     const int64_t ao = (int64_t)z1 * e.abs1 + (int64_t)z2 * e.abs2 + (int64_t)m * e.ldaux + n;
@@ -151,6 +153,7 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
   if (e.pre16) v = v && ((uintptr_t)e.pre16 & 7u) == 0;
   if (e.residual) v = v && a16(e.residual) && s4(e.ldr) && s4(e.rbs1) && s4(e.rbs2);
   ea.vec4 = v ? 1 : 0;
+  ea.epoch = b2p_seed_epoch();
   return ea;
 }
 

@@ -17,6 +17,14 @@ void b2p_set_error(const char* fmt, ...) {
 }
 
 extern "C" const char* b2p_last_error(void) { return g_err; }
+
+// device counter mixed into every dropout seed (graph replays); NULL = eager semantics
+static const uint64_t* g_seed_epoch = nullptr;
+const uint64_t* b2p_seed_epoch() { return g_seed_epoch; }
+extern "C" int b2p_set_seed_epoch(const uint64_t* dev_counter) {
+  g_seed_epoch = dev_counter;
+  return 0;
+}
 extern "C" int b2p_version(void) { return 1; }
 extern "C" int b2p_abi_sizes(int64_t* out3) {
   if (!out3) {

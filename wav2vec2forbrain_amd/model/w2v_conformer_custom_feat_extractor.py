@@ -170,7 +170,7 @@ class W2VConformerBrainEncoderModel(B2TModel):
         encoded_brain = self.brain_encoder.forward(batch)
         targets = batch.target
         assert targets is not None
-        targets = torch.where(targets < 1, torch.tensor(-100, device=targets.device), targets)
+        targets = targets.masked_fill(targets < 1, -100)
         w2v_output = self.w2v_encoder.forward(encoded_brain.logits)
         ctc_loss = (Fn.ctc_loss(w2v_output, targets, encoded_brain.logit_lens, batch.target_lens, self.blank)
                     if batch.target_lens is not None and encoded_brain.logit_lens is not None else None)

@@ -5,6 +5,7 @@ reference builds in src/experiments/experiment.py:25-28 / b2t_gru_w2v_experiment
 so LR schedulers (StepLR, LambdaLR warmup) and state_dict round-trips work unchanged."""
 from __future__ import annotations
 
+import ctypes
 import math
 
 import torch
@@ -18,7 +19,38 @@ class HipAdam(torch.optim.Optimizer):
         if amsgrad:
             raise NotImplementedError("amsgrad is not used by the reference")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
-        self._tables = {}
+        self.capturable = False
+        self._dev = []       # per param group: (lr float32[1], step float64[1], hyper float32[3]) on device
+
+    def make_capturable(self, device) -> None:
+        """Switch to the graph-replayable update (b2p_adam_multi_dev: lr and the step counter live on
+        the device, the bias corrections are formed there). Call before capturing a step; then call
+        prepare_replay() before and after_replay() after every replay."""
+        self._dev = []
+        for group in self.param_groups:
+            steps = [float(self.state[p]["step"]) for p in group["params"] if len(self.state[p])]
+            t = steps[0] if steps else 0.0
+            self._dev.append((torch.full((1,), float(group["lr"]), device=device, dtype=torch.float32),
+                              torch.full((1,), t, device=device, dtype=torch.float64),
+                              torch.zeros(3, device=device, dtype=torch.float32)))
+        self.capturable = True
+
+    def prepare_replay(self) -> None:
+        """Stream-ordered refresh of each group's device lr (LR schedulers change it on the host)."""
+        for group, (lr, _, _) in zip(self.param_groups, self._dev):
+            lr.fill_(float(group["lr"]))
+
+    def after_replay(self) -> None:
+        """Host-side step counters (state_dict) advance with every replayed update, and cached bf16
+        copies of the updated parameters are invalidated."""
+        for group in self.param_groups:
+            ps = []
+            for p in group["params"]:
+                st = self.state[p]
+                if len(st):
+                    st["step"] += 1
+                    ps.append(p)
+            Fn.bump_param_epoch(ps)
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -56,17 +88,19 @@ class HipAdam(torch.optim.Optimizer):
                     recs += [p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                              p.numel()]
                     maxn = max(maxn, p.numel())
-                key = tuple(recs)
-                table = self._tables.get(key)
-                if table is None:
-                    table = torch.tensor(recs, dtype=torch.int64).to(ps[0].device, non_blocking=False)
-                    if len(self._tables) > 64:
-                        self._tables.clear()
-                    self._tables[key] = table
-                bc1 = 1.0 - b1 ** step
-                bc2s = math.sqrt(1.0 - b2 ** step)
-                _lib.check(lib.b2p_adam_multi(table.data_ptr(), len(ps), maxn, float(group["lr"]), float(b1),
-                                              float(b2), float(group["eps"]), float(group["weight_decay"]),
-                                              float(bc1), float(bc2s), stream), "b2p_adam_multi")
+                arr = (ctypes.c_int64 * len(recs))(*recs)
+                if self.capturable:
+                    if len(buckets) != 1:
+                        raise RuntimeError("HipAdam(capturable): a param group's tensors must share one step count")
+                    lr_d, step_d, hyp_d = self._dev[self.param_groups.index(group)]
+                    _lib.check(lib.b2p_adam_recs(arr, len(ps), 0.0, float(b1), float(b2), float(group["eps"]),
+                                                 float(group["weight_decay"]), 1.0, 1.0, lr_d.data_ptr(),
+                                                 step_d.data_ptr(), hyp_d.data_ptr(), stream), "b2p_adam_recs")
+                else:
+                    bc1 = 1.0 - b1 ** step
+                    bc2s = math.sqrt(1.0 - b2 ** step)
+                    _lib.check(lib.b2p_adam_recs(arr, len(ps), float(group["lr"]), float(b1), float(b2),
+                                                 float(group["eps"]), float(group["weight_decay"]), float(bc1),
+                                                 float(bc2s), None, None, None, stream), "b2p_adam_recs")
                 Fn.bump_param_epoch(ps)   # in-place writes invisible to torch: drop bf16 weight copies
         return loss

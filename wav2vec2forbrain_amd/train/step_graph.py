@@ -1,0 +1,80 @@
+"""StepGraph: one whole training step (forward, CTC, backward, the side-stream frozen-parameter
+gradients, Adam) captured once as a HIP graph and replayed per step.
+
+The reference's step (src/train/train_loop.py:41-84) is ~560 kernel launches issued from Python;
+on MI355X the host needs about as long to issue them as the GPU needs to run them, so an eager
+step idles the GPU between launches. Replaying the captured graph issues the whole step with one
+call. What stays live across replays:
+  * dropout masks: every dropout kernel adds a device step counter (b2p_set_seed_epoch) to its
+    host-drawn seed; the counter's increment is the graph's first node, so each replay draws new
+    masks (the per-call seeds drawn at capture time only fix the call sites apart);
+  * Adam: HipAdam.make_capturable keeps lr and the step count on the device
+    (b2p_adam_multi_dev); prepare_replay() refreshes lr from the param groups (schedulers),
+    after_replay() advances the host step counters;
+  * inputs: the step reads the tensors it was captured with; load new data into them in place
+    (copy_) before a replay.
+Gradients of parameters that the optimizer does not own (the frozen wav2vec2 weights, as in the
+reference) keep accumulating in their .grad buffers across replays, exactly as in eager steps.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from .. import _lib
+from .. import functional as Fn
+
+
+class StepGraph:
+    def __init__(self, step_fn, optimizer, warmup: int = 2):
+        """step_fn() runs one step on the current stream and returns the loss tensor (no host
+        syncs inside: model.sync_metrics must be False)."""
+        self.step_fn = step_fn
+        self.opt = optimizer
+        self.warmup = warmup
+        self.graph = None
+        self.loss = None
+        self.epoch = None
+
+    def capture(self) -> None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+        lib = _lib.load()
+        self.epoch = torch.zeros(1, dtype=torch.int64, device=dev)
+        _lib.check(lib.b2p_set_seed_epoch(ctypes.c_void_p(self.epoch.data_ptr())), "b2p_set_seed_epoch")
+        self.opt.make_capturable(dev)
+        Fn.set_gemm_timing(False)
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(self.warmup):         # allocator / side-stream warm-up on the capture stream
+                self._one()
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        # the host side of the captured step runs once now without updating anything: keep the
+        # optimizer's host step counters as they were (after_replay advances them per replay)
+        steps = {p: st["step"].clone() for p, st in self.opt.state.items() if "step" in st}
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self.loss = self._one()
+        torch.cuda.synchronize()
+        for p, t in steps.items():
+            self.opt.state[p]["step"] = t
+        self.graph = g
+
+    def _one(self):
+        _lib.check(_lib.load().b2p_seed_epoch_step(ctypes.c_void_p(self.epoch.data_ptr()),
+                                                   ctypes.c_void_p(_lib.stream_ptr())), "b2p_seed_epoch_step")
+        return self.step_fn()
+
+    def replay(self) -> torch.Tensor:
+        """One training step; returns the (static) loss tensor — clone it to keep the value."""
+        self.opt.prepare_replay()
+        self.graph.replay()
+        self.opt.after_replay()
+        return self.loss
+
+    def release(self) -> None:
+        """Back to eager semantics (the seed counter is no longer mixed in)."""
+        _lib.check(_lib.load().b2p_set_seed_epoch(None), "b2p_set_seed_epoch")
+        self.graph = None
