@@ -213,6 +213,21 @@ int b2p_conv_weight_transpose_flip(const float* w, float* out, int64_t G, int64_
 
 /* weight norm over all dims but dim=2 (torch.nn.utils.parametrizations.weight_norm(dim=2),
  * transformers Wav2Vec2PositionalConvEmbedding): w[o,i,k] = g[k] * v[o,i,k] / ||v[:,:,k]|| */
+/* Grouped positional conv of wav2vec2 on bf16 MFMA (csrc/posconv16.hip; 48 channels per group,
+ * 128 taps, padding 64 + SamePad, T <= 256), replacing the implicit-conv GEMMs of
+ * Wav2Vec2PositionalConvEmbedding (modeling_wav2vec2.py, reached from
+ * src/model/w2v_custom_feat_extractor.py:152 through the encoder):
+ *   fwd:       pre = conv(e) + bias, xsum = gelu(pre) + e, e16 = bf16(e); w16 = bf16 [O][taps*Ig]
+ *              (b2p_conv_weight_permute layout)
+ *   bwd_data:  dpre = dxsum * gelu'(pre), de = conv^T(dpre) + dxsum, dpre16 = bf16(dpre),
+ *              colpart[b][c] = sum_t dpre[b,t,c]; wt16 = bf16 b2p_conv_weight_transpose_flip layout
+ *   wgrad:     dwp[o][tap*Ig + i] = sum_{b,t} dpre[b,t,o] * e[b,t+tap-64,i] (bf16 operands, fp32 sums) */
+int b2p_posconv16_fwd(const float* e, const uint16_t* w16, const float* bias, float* xsum, float* pre,
+                      uint16_t* e16, int64_t B, int64_t T, int64_t D, int64_t groups, b2p_stream_t stream);
+int b2p_posconv16_bwd_data(const float* dxsum, const float* pre, const uint16_t* wt16, float* de, uint16_t* dpre16,
+                           float* colpart, int64_t B, int64_t T, int64_t D, int64_t groups, b2p_stream_t stream);
+int b2p_posconv16_wgrad(const uint16_t* dpre16, const uint16_t* e16, float* dwp, int64_t B, int64_t T, int64_t D,
+                        int64_t groups, b2p_stream_t stream);
 int64_t b2p_weight_norm_workspace(int64_t O, int64_t I, int64_t K);
 int b2p_weight_norm_fwd(const float* g, const float* v, float* w, float* norms, int64_t O,
                         int64_t I, int64_t K, float* workspace, b2p_stream_t stream);

@@ -517,3 +517,36 @@ def test_dropout_seed_epoch_counter():
     finally:
         Fn._lib.check(lib.b2p_set_seed_epoch(None), "set_seed_epoch")
     assert torch.equal(mask(), m0)
+
+
+def test_pos_conv_ln_bf16_posconv16():
+    """wav2vec2-base positional conv (768 channels, 16 groups of 48, 128 taps) on the bf16 slab kernels
+    (csrc/posconv16.hip: forward, backward-data with the conv-bias column sums, weight gradient)
+    against the CPU oracle in fp32; odd batch (a half-empty sample pair), T below the 256 cap."""
+    Fn = _fn()
+    from oracle.b2p2t_oracle import pos_conv, layer_norm, OracleConfig
+    torch.manual_seed(15)
+    B, T, D, G, K = 3, 131, 768, 16, 128
+    cfg = OracleConfig(num_conv_pos_embeddings=K, num_conv_pos_embedding_groups=G, hidden_size=D)
+    e = torch.randn(B, T, D)
+    g = 1 + 0.1 * torch.randn(1, 1, K)
+    v = torch.randn(D, D // G, K) / math.sqrt(48 * 128)
+    cb = 0.05 * torch.randn(D)
+    lg, lb = 1 + 0.1 * torch.randn(D), 0.1 * torch.randn(D)
+    ts = [t.clone().requires_grad_(True) for t in (e, g, v, cb, lg, lb)]
+    sd = {"p.conv.parametrizations.weight.original0": ts[1], "p.conv.parametrizations.weight.original1": ts[2],
+          "p.conv.bias": ts[3]}
+    ref = layer_norm(ts[0] + pos_conv(ts[0], sd, "p.", cfg), ts[4], ts[5], 1e-5)
+    dy = torch.randn_like(ref)
+    refg = torch.autograd.grad(ref, ts, dy)
+    with Fn.precision("bf16"):
+        assert Fn._posconv16_ok(B, T, D, D, 48, K, G)
+        tg = [t.cuda().requires_grad_(True) for t in (e, g, v, cb, lg, lb)]
+        out = Fn.pos_conv_ln(*tg, G, 1e-5, 0.0, False)
+        got = torch.autograd.grad(out, tg, dy.cuda())
+
+    def rl2(a, b):
+        return float((a.detach().cpu() - b.detach()).norm() / b.detach().norm())
+    assert rl2(out, ref) < 1e-2
+    for i, (a, b) in enumerate(zip(got, refg)):
+        assert rl2(a, b) < 2e-2, (i, rl2(a, b))

@@ -1,7 +1,7 @@
 """Per-step timeline of a rocprofv3 kernel trace of bench.py: the span of the last complete step
 (between two Adam launches), busy time (union of kernel intervals over all streams), the idle gaps
 (no kernel running anywhere) and the largest gaps with the kernels around them.
-usage: python tools/timeline.py <dir with the trace .db or *kernel_trace.csv> [marker-substring]"""
+usage: python tools/timeline.py <dir with the trace .db or *kernel_trace.csv> [marker-substring] [steps back]"""
 import sys
 
 sys.path.insert(0, __file__.rsplit("/", 1)[0])
@@ -11,6 +11,7 @@ from trace_groups import dispatches  # noqa: E402
 def main():
     d = sys.argv[1]
     marker = sys.argv[2] if len(sys.argv) > 2 else "adam"
+    back = int(sys.argv[3]) if len(sys.argv) > 3 else 1   # which step, counted from the last
     ks = sorted(dispatches(d), key=lambda r: r[3])
     marks = [i for i, k in enumerate(ks) if marker in k[0]]
     # one multi-tensor Adam launch (or a few) per step: step boundaries = first marker of each run
@@ -18,7 +19,7 @@ def main():
     if len(firsts) < 3:
         print("not enough steps in the trace")
         return
-    a, b = firsts[-2] + 1, firsts[-1] + 1      # last complete step: after one Adam run up to the next
+    a, b = firsts[-1 - back] + 1, firsts[-back] + 1   # a complete step: after one Adam run up to the next
     while b < len(ks) and marker in ks[b][0]:
         b += 1
     step = ks[a:b]

@@ -888,12 +888,22 @@ class _PosConvLN(torch.autograd.Function):
         xsum = torch.empty_like(e)
         pad = K // 2
         Og = O // groups
-        A = conv_op(e, 0, D, T, T, 1, pad, Ig, T * D, True, bs1=Ig)
-        gemm(B * T, Og, K * Ig, A, op(wp, 0, K * Ig, True, bs1=Og * K * Ig), xsum, D, cbs1=Og, nz1=groups,
-             bias=cbias, biasbs1=Og, pre_out=pre, act=ACT["gelu"], residual=e, rbs1=Og, ldr=D)
+        fast = _posconv16_ok(B, T, D, O, Ig, K, groups)
+        if fast:
+            # bf16 MFMA grouped conv (csrc/posconv16.hip): slab-staged input, streamed weights
+            e16 = torch.empty(B, T, D, device=dev, dtype=BF16)
+            _lib.call("b2p_posconv16_fwd", _p(e), _p(cast16(wp)), _p(cbias), _p(xsum), _p(pre), _p(e16), B, T, D,
+                      groups, _st())
+            keep = e16
+        else:
+            A = conv_op(e, 0, D, T, T, 1, pad, Ig, T * D, True, bs1=Ig)
+            gemm(B * T, Og, K * Ig, A, op(wp, 0, K * Ig, True, bs1=Og * K * Ig), xsum, D, cbs1=Og, nz1=groups,
+                 bias=cbias, biasbs1=Og, pre_out=pre, act=ACT["gelu"], residual=e, rbs1=Og, ldr=D)
+            keep = e
         y, mean, rstd = _ln_fwd(xsum.view(B * T, D), ln_g, ln_b, eps, drop_p, seed)
-        ctx.save_for_backward(e, wg, wv, w, norms, pre, xsum, ln_g, mean, rstd)
+        ctx.save_for_backward(keep, wg, wv, w, norms, pre, xsum, ln_g, mean, rstd)
         ctx.meta = (groups, drop_p, seed, B, T, D, O, Ig, K)
+        ctx.fast = fast
         return y.view(B, T, D)
 
     @staticmethod
@@ -903,6 +913,8 @@ class _PosConvLN(torch.autograd.Function):
         dev = e.device
         dy = dy.contiguous().view(B * T, D)
         dxsum, dlg, dlb, _ = _ln_bwd(dy, xsum.view(B * T, D), ln_g, mean, rstd, True, None, drop_p, seed)
+        if ctx.fast:
+            return _posconv16_bwd(ctx, e, wg, wv, w, norms, pre, dxsum, dlg, dlb)
         dpre = _act_bwd(dxsum, pre.view(B * T, D), ACT["gelu"])
         Og = O // groups
         pad = K // 2
@@ -931,6 +943,36 @@ class _PosConvLN(torch.autograd.Function):
             gemm(B * T, Ig, K * Og, A, op(wt, 0, K * Og, True, bs1=Ig * K * Og), de, D, cbs1=Ig, nz1=groups,
                  residual=dxsum, rbs1=Ig, ldr=D)
         return de, dg, dv, dcb, dlg, dlb, None, None, None, None
+
+
+def _posconv16_ok(B, T, D, O, Ig, K, groups) -> bool:
+    return bf16_mode() and O == D and Ig == 48 and D == groups * 48 and K == 128 and 1 <= T <= 256
+
+
+def _posconv16_bwd(ctx, e16, wg, wv, w, norms, pre, dxsum, dlg, dlb):
+    groups, drop_p, seed, B, T, D, O, Ig, K = ctx.meta
+    dev = dxsum.device
+    ng = ctx.needs_input_grad
+    wt = torch.empty(groups, Ig, K * (O // groups), device=dev)
+    _lib.call("b2p_conv_weight_transpose_flip", _p(w), _p(wt), groups, O // groups, Ig, K, _st())
+    de = torch.empty(B, T, D, device=dev)
+    dpre16 = torch.empty(B, T, D, device=dev, dtype=BF16)
+    part = torch.empty(B, D, device=dev)
+    _lib.call("b2p_posconv16_bwd_data", _p(dxsum), _p(pre), _p(cast16(wt)), _p(de), _p(dpre16), _p(part), B, T, D,
+              groups, _st())
+    dcb = torch.empty(O, device=dev)
+    colsum(part, B, D, dcb)
+    dg = dv = None
+    if ng[1] or ng[2]:
+        dwp = torch.empty(O, K * Ig, device=dev)
+        _lib.call("b2p_posconv16_wgrad", _p(dpre16), _p(e16), _p(dwp), B, T, D, groups, _st())
+        dw = torch.empty_like(wv)
+        _lib.call("b2p_conv_weight_permute", _p(dwp), _p(dw), O, Ig, K, 1, _st())
+        ws = torch.empty(int(_lib.load().b2p_weight_norm_workspace(O, Ig, K)), device=dev)
+        dg = torch.empty_like(wg)
+        dv = torch.empty_like(wv)
+        _lib.call("b2p_weight_norm_bwd", _p(wg), _p(wv), _p(norms), _p(dw), _p(dg), _p(dv), O, Ig, K, _p(ws), _st())
+    return (de if ng[0] else None), dg, dv, dcb, dlg, dlb, None, None, None, None
 
 
 def pos_conv_ln(e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, training):
