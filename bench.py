@@ -137,7 +137,8 @@ def main():
     opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
     reducer = GradBucketReducer(brain_params) if world > 1 else None
     # the frozen w2v's weight gradients (computed, as the reference does) run beside the GRU backward
-    Fn.set_deferred_wgrad([p for n, p in model.named_parameters() if not n.startswith("brain_encoder.")])
+    if os.environ.get("B2P_DEFER_WGRAD", "1") != "0":
+        Fn.set_deferred_wgrad([p for n, p in model.named_parameters() if not n.startswith("brain_encoder.")])
     batch = batch_on(cfg, device)
 
     # the reference reads ctc_loss.item() inside forward (w2v_custom_feat_extractor.py:94): a host

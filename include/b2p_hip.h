@@ -170,6 +170,10 @@ int b2p_layernorm_bwd16(const float* dy, const float* x, const float* gamma, con
 /* fp32 -> bf16 (round to nearest even), the GEMM operand copy of a weight or activation
  * (master copies stay fp32; replaces the implicit .to(bfloat16) of autocast) */
 int b2p_cast_bf16(const float* x, uint16_t* y, int64_t n, b2p_stream_t stream);
+/* y[c * ldy + col0 + r] = bf16(x[r * C + c]): transposed bf16 copy of an R x C fp32 matrix (cached
+ * k-contiguous weight operands of the backward-data GEMMs) */
+int b2p_transpose_bf16(const float* x, uint16_t* y, int64_t R, int64_t C, int64_t ldy, int64_t col0,
+                       b2p_stream_t stream);
 
 /* Row softmax for attention scores (eager_attention_forward: softmax(QK^T*scale) + dropout).
  * S rows of length n (row stride ld). Writes P (pre-dropout) and Pd (dropped, scaled). */

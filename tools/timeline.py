@@ -38,8 +38,16 @@ def main():
     ksum = sum(k[4] for k in step)
     print(f"step span {span / 1e6:.3f} ms, {len(step)} kernels, kernel-time sum {ksum / 1e6:.3f} ms, "
           f"busy (union) {busy / 1e6:.3f} ms, idle {(span - busy) / 1e6:.3f} ms in {len(gaps)} gaps")
-    for g, p, n in sorted(gaps, key=lambda x: -x[0])[:12]:
+    for g, p, n in sorted(gaps, key=lambda x: -x[0])[:8]:
         print(f"  gap {g / 1e3:8.1f} us  after {str(p)[:60]}  before {n[:60]}")
+    agg = {}
+    for k in step:
+        n = k[0].replace("(anonymous namespace)::", "")
+        t, c = agg.get(n, (0, 0))
+        agg[n] = (t + k[4], c + 1)
+    print("top kernels of this step:")
+    for n, (t, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:28]:
+        print(f"  {t / 1e3:8.1f} us {c:4d}x {100 * t / ksum:5.1f}%  {n[:100]}")
 
 
 if __name__ == "__main__":

@@ -604,6 +604,36 @@ extern "C" int b2p_cast_bf16(const float* x, uint16_t* y, int64_t n, b2p_stream_
   return 0;
 }
 
+// y[c][r] = bf16(x[r][c]) for an R x C fp32 matrix written into columns col0 .. col0+R-1 of a
+// [C][ldy] bf16 matrix (several row blocks stacked side by side: the transposed [Wq; Wk; Wv]):
+// 64 x 64 tiles through LDS, reads and writes coalesced along the rows of x and y
+__global__ void __launch_bounds__(256) transpose16_k(const float* __restrict__ x, uint16_t* __restrict__ y,
+                                                     int64_t R, int64_t C, int64_t ldy, int64_t col0) {
+  __shared__ float tile[64][65];
+  const int64_t r0 = (int64_t)blockIdx.y * 64, c0 = (int64_t)blockIdx.x * 64;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t r = r0 + i, c = c0 + tx;
+    tile[i][tx] = (r < R && c < C) ? x[r * C + c] : 0.f;
+  }
+  __syncthreads();
+  for (int i = ty; i < 64; i += 4) {
+    const int64_t c = c0 + i, r = r0 + tx;
+    if (c < C && r < R) y[c * ldy + col0 + r] = b2p_bf16_bits(tile[tx][i]);
+  }
+}
+
+extern "C" int b2p_transpose_bf16(const float* x, uint16_t* y, int64_t R, int64_t C, int64_t ldy, int64_t col0,
+                                  b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && y, "transpose_bf16: NULL pointer");
+  B2P_CHECK_ARG(R >= 0 && C >= 0 && ldy >= col0 + R, "transpose_bf16: bad shape");
+  if (R == 0 || C == 0) return 0;
+  hipLaunchKernelGGL(transpose16_k, dim3((unsigned)((C + 63) / 64), (unsigned)((R + 63) / 64)), dim3(256), 0,
+                     (hipStream_t)stream, x, y, R, C, ldy, col0);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 // Unfold((k, 1), stride) of a (B, L, C) tensor, tap-major (feature tap*C + c), materialised as
 // bf16 rows of k*C: row (b, t) is the contiguous slab x[b][t*stride .. t*stride+k)[.] cast to bf16
 // (the GRU layer-0 weight-gradient GEMM operand; b2p2t_model.py:108-113,162-167).

@@ -483,6 +483,27 @@ def weight16(*ws):
     return out
 
 
+def weight16t(*ws):
+    """Transposed bf16 copy [C][sum R] of fp32 weights (R x C each, stacked along R): the
+    k-contiguous B operand of a backward-data GEMM dX = dY W (NT kernel instead of the slower
+    transposed-read NN form); cached like weight16."""
+    key = ("T",) + tuple(id(w) for w in ws)
+    st = _stamp(ws)
+    hit = _W16.get(key)
+    if hit is not None and hit[0] == st:
+        return hit[1]
+    rows = sum(w.shape[0] for w in ws)
+    C = ws[0].shape[1]
+    out = torch.empty(C, rows, device=ws[0].device, dtype=BF16)
+    off = 0
+    for w in ws:
+        _chk(w, "weight16t")
+        _lib.call("b2p_transpose_bf16", _p(w), _p(out), w.shape[0], C, rows, off, _st())
+        off += w.shape[0]
+    _W16[key] = (st, out)
+    return out
+
+
 def bias_cat(*bs):
     """fp32 concatenation of biases (None -> zeros), cached like weight16."""
     ref = next(b for b in bs if b is not None)
@@ -1228,7 +1249,8 @@ class _EncoderLayer16(torch.autograd.Function):
         dev = y1.device
         ng = ctx.needs_input_grad
         dout = dout.contiguous().view(NT, D)
-        w1_16, w2_16, wo16, wqkv16 = weight16(w1), weight16(w2), weight16(wo), weight16(wq, wk, wv)
+        # transposed bf16 weights: every backward-data GEMM runs on the k-contiguous (NT) kernel
+        w1t16, w2t16, wot16, wqkvt16 = weight16t(w1), weight16t(w2), weight16t(wo), weight16t(wq, wk, wv)
         # LN2 backward -> dy2 ; dz2 = dropout-mask(dy2) (output dropout of the FFN), bf16 copy dz2_16
         db2 = torch.empty(D, device=dev) if ng[15] else None
         dy2, dg2, dbe2, _dz2, dz2_16 = _ln_bwd16(dout, y2, g2, m2, r2, True, in_drop_p=p_hid, in_seed=seeds[3],
@@ -1247,7 +1269,7 @@ class _EncoderLayer16(torch.autograd.Function):
         # gradient) are reduced inside the epilogue from the fp32 values
         dpre16 = torch.empty(NT, F, device=dev, dtype=BF16)
         parts = colsum_parts_buf(NT, F, dev) if ng[13] else None
-        gemm(NT, F, D, op(dz2_16, 0, D, True), op(w2_16, 0, F, False), None, F, drop_p=p_act, seed=seeds[2],
+        gemm(NT, F, D, op(dz2_16, 0, D, True), op(w2t16, 0, D, True), None, F, drop_p=p_act, seed=seeds[2],
              act_bwd=ACT["gelu"], aux16=pre, C16=dpre16, colsum_part=parts)
         dw1 = None
         if ng[12]:
@@ -1261,7 +1283,7 @@ class _EncoderLayer16(torch.autograd.Function):
         db1 = colsum_from_parts(parts, torch.empty(F, device=dev)) if ng[13] else None
         # dx1 = dpre W1 + dy2
         dx1 = torch.empty(NT, D, device=dev)
-        gemm(NT, D, F, op(dpre16, 0, F, True), op(w1_16, 0, D, False), dx1, D, residual=dy2)
+        gemm(NT, D, F, op(dpre16, 0, F, True), op(w1t16, 0, F, True), dx1, D, residual=dy2)
         del dpre16
         # LN1 backward -> dy1 ; dz1 = dropout-mask(dy1) (attention output dropout)
         dbo = torch.empty(D, device=dev) if ng[9] else None
@@ -1278,12 +1300,12 @@ class _EncoderLayer16(torch.autograd.Function):
                 gemm(D, D, NT, op(dz1_16, 0, D, False), op(O16, 0, D, False), dwo, D)
         if ctx.fused:
             dO16 = torch.empty(NT, D, device=dev, dtype=BF16)
-            gemm(NT, D, D, op(dz1_16, 0, D, True), op(wo16, 0, D, False), None, D, C16=dO16)
+            gemm(NT, D, D, op(dz1_16, 0, D, True), op(wot16, 0, D, True), None, D, C16=dO16)
             dqkv, dqkv16 = _attn16_bwd(qkv, dO16, P, B, T, nh, dh, p_attn, seeds[0])
             del dO16
         else:
             dO = torch.empty(NT, D, device=dev)
-            gemm(NT, D, D, op(dz1_16, 0, D, True), op(wo16, 0, D, False), dO, D)
+            gemm(NT, D, D, op(dz1_16, 0, D, True), op(wot16, 0, D, True), dO, D)
             dqkv, dqkv16 = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seeds[0], want16=True)
             del dO
         grads_w = [None] * 6
@@ -1307,7 +1329,7 @@ class _EncoderLayer16(torch.autograd.Function):
         dx = None
         if ng[0]:
             dx = torch.empty(NT, D, device=dev)
-            gemm(NT, D, 3 * D, op(dqkv16, 0, 3 * D, True), op(wqkv16, 0, D, False), dx, D, residual=dy1)
+            gemm(NT, D, 3 * D, op(dqkv16, 0, 3 * D, True), op(wqkvt16, 0, 3 * D, True), dx, D, residual=dy1)
             dx = dx.view(B, T, D)
         rest = [dwo, dbo, dg1, dbe1, dw1, db1, dw2, db2, dg2, dbe2]
         # small gradients of frozen parameters: accumulated on the side stream too
