@@ -102,7 +102,9 @@ typedef struct {
   int32_t nz1, nz2;
   b2p_operand A, B;
   b2p_epilogue ep;
-  int32_t precision;          /* 0 = bf16 MFMA, 1 = fp32 MFMA (parity mode)                   */
+  int32_t precision;          /* 0 = bf16 MFMA, 1 = fp32 MFMA (parity mode), 2 = fp16 MFMA
+                               * (fp32 operands converted while staged; forward of the 24-layer
+                               * Conformer, whose CTC loss bf16 rounding noise biases)          */
   int32_t timing_family;      /* tag for b2p_timing_* (0 = untagged)                          */
   double flops;               /* algorithmic FLOPs of this launch (for timing)                */
   /* split-K (deterministic): ksplit > 1 slices K into kchunk-sized ranges (multiple of 32) whose

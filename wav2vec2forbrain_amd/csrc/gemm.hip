@@ -40,12 +40,21 @@ template <int KB> struct Prec<1, KB> {   // fp32 MFMA
   typedef float T;
   static constexpr int LDS_STRIDE = KB + 1;
 };
+template <int KB> struct Prec<2, KB> {   // fp16 MFMA (same rate as bf16, 3 more mantissa bits)
+  typedef _Float16 T;
+  static constexpr int LDS_STRIDE = KB + 8;
+};
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 template <int PREC, int KB>
 __device__ __forceinline__ void st4(typename Prec<PREC, KB>::T* dst, float a, float b, float c, float d) {
   if constexpr (PREC == 0) {
     bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
     *reinterpret_cast<bf16x4*>(dst) = v;
+  } else if constexpr (PREC == 2) {
+    f16x4 v = {(_Float16)a, (_Float16)b, (_Float16)c, (_Float16)d};
+    *reinterpret_cast<f16x4*>(dst) = v;
   } else {
     dst[0] = a; dst[1] = b; dst[2] = c; dst[3] = d;
   }
@@ -289,6 +298,22 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
       }
+    } else if constexpr (PREC == 2) {
+#pragma unroll
+      for (int kk = 0; kk < KB / 32; ++kk) {
+        f16x8 af[TM], bfr[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          af[i] = *reinterpret_cast<const f16x8*>(A_ + (wm * WM + i * 16 + (lane & 15)) * LS + 32 * kk + 8 * (lane >> 4));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          bfr[j] = *reinterpret_cast<const f16x8*>(B_ + (wn * WN + j * 16 + (lane & 15)) * LS + 32 * kk + 8 * (lane >> 4));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
     } else {
 #pragma unroll
       for (int ks = 0; ks < KB / 4; ++ks) {
@@ -358,6 +383,10 @@ int launch_prec(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st) {
   dim3 grid((unsigned)((d.N + BN - 1) / BN), (unsigned)((d.M + BM - 1) / BM), (unsigned)(d.nz1 * d.nz2 * ks));
   if (d.precision == 1)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKin, ACONV, BCONV, 1>), grid, dim3(NT), 0, st, d, ea);
+  else if (d.precision == 2 && (ks == 1 || d.kchunk % 64 == 0))
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 64, AK, BKin, ACONV, BCONV, 2>), grid, dim3(NT), 0, st, d, ea);
+  else if (d.precision == 2)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKin, ACONV, BCONV, 2>), grid, dim3(NT), 0, st, d, ea);
   else if (kb_choice() == 64 && (ks == 1 || d.kchunk % 64 == 0))
     hipLaunchKernelGGL((gemm_kernel<BM, BN, 64, AK, BKin, ACONV, BCONV, 0>), grid, dim3(NT), 0, st, d, ea);
   else
@@ -398,7 +427,7 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   B2P_CHECK_ARG(d.M >= 0 && d.N >= 0 && d.K >= 0, "gemm: negative size");
   B2P_CHECK_ARG(d.M < (1ll << 31) && d.N < (1ll << 31) && d.K < (1ll << 31), "gemm: size too large");
   B2P_CHECK_ARG(d.nz1 >= 1 && d.nz2 >= 1, "gemm: batch dims must be >= 1");
-  B2P_CHECK_ARG(d.precision == 0 || d.precision == 1, "gemm: precision must be 0 or 1");
+  B2P_CHECK_ARG(d.precision >= 0 && d.precision <= 2, "gemm: precision must be 0 (bf16), 1 (fp32) or 2 (fp16)");
   if (d.M == 0 || d.N == 0) return 0;
   B2P_CHECK_ARG(d.ep.C != nullptr || d.ep.C16 != nullptr, "gemm: C and C16 are NULL");
   B2P_CHECK_ARG(d.ep.C != nullptr || d.ep.beta == 0.f, "gemm: beta != 0 needs C");

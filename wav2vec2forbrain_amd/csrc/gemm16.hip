@@ -597,11 +597,12 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   // 256 x 256 ping-pong tile (B2P_GEMM16_PP: 0 off, 1 (default) for long-K launches whose grid fills
   // most of the chip, 2 always for plain operands). One workgroup per CU cannot hide its epilogue
   // behind another tile's K loop, so at K <= 1024 (the encoder's projections, 2-3 tiles per CU
-  // with the 128 x 128 kernel) it measured slower; at K >= 2048 its K loop (~1.0 PF) wins.
+  // with the 128 x 128 kernel) it measured slower; at K >= 2048 its K loop (~1.0 PF) wins, and so
+  // does a split-K launch of >= 1024-deep slices (the weight gradients, K = tokens).
   static int pp_mode = getenv("B2P_GEMM16_PP") ? atoi(getenv("B2P_GEMM16_PP")) : 1;
   const int64_t tiles_pp = ((d.M + 255) / 256) * ((d.N + 255) / 256) * nz;
   const int64_t kper = ks > 1 ? (int64_t)d.kchunk : d.K;
-  const bool pp = !d.A.conv && (pp_mode == 2 || (pp_mode == 1 && tiles_pp >= 192 && kper >= 2048));
+  const bool pp = !d.A.conv && (pp_mode == 2 || (pp_mode == 1 && ((tiles_pp >= 192 && kper >= 2048) || (ks > 1 && tiles_pp >= 160 && kper >= 1024))));
   if (pp) {
     const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 255) / 256);
     const dim3 grid((unsigned)tiles_pp), block(PP_NT);

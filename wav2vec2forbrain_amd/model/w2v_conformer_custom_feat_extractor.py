@@ -165,13 +165,17 @@ class W2VConformerBrainEncoderModel(B2TModel):
         self.w2v_encoder = Wav2Vec2ConformerWithoutFeatExtrForCTC(cfg)
         self.blank = 0
         self.sync_metrics = True
+        # bf16 mode: the Conformer's forward GEMMs on fp16 MFMA (Fn.forward_f16: removes the CTC-loss
+        # bias of bf16 logit noise over 24 layers; backward stays bf16)
+        self.forward_f16 = True
 
     def forward(self, batch: B2tSampleBatch):
         encoded_brain = self.brain_encoder.forward(batch)
         targets = batch.target
         assert targets is not None
         targets = targets.masked_fill(targets < 1, -100)
-        w2v_output = self.w2v_encoder.forward(encoded_brain.logits)
+        with Fn.forward_f16(self.forward_f16):
+            w2v_output = self.w2v_encoder.forward(encoded_brain.logits)
         ctc_loss = (Fn.ctc_loss(w2v_output, targets, encoded_brain.logit_lens, batch.target_lens, self.blank)
                     if batch.target_lens is not None and encoded_brain.logit_lens is not None else None)
         metrics = {}
