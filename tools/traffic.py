@@ -18,7 +18,7 @@ def per_kernel(db, counter):
 def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
-    isg = lambda n: "gemm16_kernel<" in n or "gemm_kernel<" in n
+    isg = lambda n: "gemm16_kernel<" in n or "gemm_kernel<" in n or "gemm16_pp_kernel<" in n
     f = [v for _, n, v in fetch if isg(n)]
     w = [v for _, n, v in write if isg(n)]
     fb = 2.0 * 1024.0 * sum(f) / max(len(f), 1)

@@ -27,12 +27,13 @@ from .. import functional as Fn
 
 
 class StepGraph:
-    def __init__(self, step_fn, optimizer, warmup: int = 2):
+    def __init__(self, step_fn, optimizer, warmup: int = 2, warm_replays: int = 2):
         """step_fn() runs one step on the current stream and returns the loss tensor (no host
         syncs inside: model.sync_metrics must be False)."""
         self.step_fn = step_fn
         self.opt = optimizer
         self.warmup = warmup
+        self.warm_replays = warm_replays
         self.graph = None
         self.loss = None
         self.epoch = None
@@ -61,6 +62,9 @@ class StepGraph:
         for p, t in steps.items():
             self.opt.state[p]["step"] = t
         self.graph = g
+        for _ in range(self.warm_replays):   # first launches of a new graph pay its upload
+            self.replay()
+        torch.cuda.synchronize()
 
     def _one(self):
         _lib.check(_lib.load().b2p_seed_epoch_step(ctypes.c_void_p(self.epoch.data_ptr()),
