@@ -109,7 +109,7 @@ def main():
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--graph", type=int, default=None,
-                    help="1/0: replay the step as a captured HIP graph (default: on for N=1, off for N>1)")
+                    help="1/0: replay the step as a captured HIP graph (default 1)")
     ap.add_argument("--config", choices=["base", "conformer"], default="base",
                     help="base = BASELINE configs[1] (headline); conformer = configs[2]")
     args = ap.parse_args()
@@ -117,9 +117,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # B2P_DIST_BACKEND=gloo (with more ranks than GPUs, ranks share devices) rehearses the N>1 path
+    # on a one-GPU box; the driver's N>1 runs use RCCL ("nccl"), one rank per GPU
+    backend = os.environ.get("B2P_DIST_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     device = f"cuda:{local}"
     torch.cuda.set_device(local)
     torch.manual_seed(1234 + rank)
@@ -135,7 +143,10 @@ def main():
     skip = unused_param_names(model)
     brain_params = [p for n, p in model.named_parameters() if n.startswith("brain_encoder.") and n not in skip]
     opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
-    reducer = GradBucketReducer(brain_params) if world > 1 else None
+    use_graph = True if args.graph is None else bool(args.graph)
+    # graph mode: backward is captured, so the bucket all-reduce runs after each replay instead of
+    # from the backward hooks
+    reducer = GradBucketReducer(brain_params, overlap=not use_graph) if world > 1 else None
     # the frozen w2v's weight gradients (computed, as the reference does) run beside the GRU backward
     if os.environ.get("B2P_DEFER_WGRAD", "1") != "0":
         Fn.set_deferred_wgrad([p for n, p in model.named_parameters() if not n.startswith("brain_encoder.")])
@@ -161,16 +172,32 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    # N=1: the whole step (forward, CTC, backward, side-stream frozen-weight gradients, Adam) is
-    # captured once as a HIP graph and replayed (train/step_graph.py): one host call per step instead
-    # of ~560 Python-issued launches. N>1 runs the eager step (RCCL bucket hooks inside backward).
-    use_graph = (world == 1) if args.graph is None else bool(args.graph)
+    # The step is captured once as a HIP graph and replayed (train/step_graph.py): one host call per
+    # step instead of ~650 Python-issued launches. N=1: forward, CTC, backward, side-stream frozen-
+    # weight gradients and Adam are all in the graph. N>1: the graph holds forward + backward; after
+    # each replay the gradient buckets are all-reduced over RCCL and Adam runs (no collective is
+    # captured). --graph 0: eager steps (RCCL bucket hooks inside backward).
     sg = None
     if use_graph:
         from wav2vec2forbrain_amd.train.step_graph import StepGraph
-        sg = StepGraph(step, opt)
+        if world == 1:
+            sg = StepGraph(step, opt)
+            run = lambda: sg.replay().clone()      # noqa: E731
+        else:
+            def fwd_bwd():
+                opt.zero_grad()
+                out = model(batch)
+                out.loss.backward()
+                Fn.join_wgrad()
+                return out.metrics["ctc_loss"]
+            sg = StepGraph(fwd_bwd, None)
+
+            def run():
+                loss = sg.replay().clone()
+                reducer.finish()
+                opt.step()
+                return loss
         sg.capture()
-        run = lambda: sg.replay().clone()      # noqa: E731
     else:
         run = step
     if world > 1:
@@ -201,7 +228,9 @@ def main():
     if rank != 0:
         dist.destroy_process_group() if world > 1 else None
         return
-    steps_per_s = args.steps / dt * 1.0          # global steps/s (every rank does one step per step)
+    # whole-job throughput: the units all ranks processed / time. A unit is one training step of one
+    # rank over its own bs-sample batch (weak scaling: N ranks process N batches per global step).
+    steps_per_s = world * args.steps / dt
     gemm_ms, gemm_n, gemm_flops = ms
     achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
     step_tflop = STEP_TFLOP[args.config] * args.bs / 32 * args.seq / 1024
@@ -213,6 +242,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(dt / args.steps * 1e3, 3),
+        "steps_per_s_per_rank": round(args.steps / dt, 4),
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
@@ -225,8 +255,8 @@ def main():
                    "per_gpu_batch": args.bs, "seq_len": args.seq, "parallelism": f"dp{world}"},
         "ctc_loss": round(losses[-1], 5),
         "step_mode": "hip-graph replay" if use_graph else "eager",
-        "samples_per_s": round(steps_per_s * args.bs * world, 2),
-        "step_mfma_frac": round(step_tflop * steps_per_s / BF16_DENSE_PEAK_TFLOPS, 4),
+        "samples_per_s": round(steps_per_s * args.bs, 2),
+        "step_mfma_frac": round(step_tflop * steps_per_s / world / BF16_DENSE_PEAK_TFLOPS, 4),
         "roofline": {"bound": "mfma", "kernel": "b2p_gemm (all GEMM launches of the step)",
                      "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": gemm_traffic(),

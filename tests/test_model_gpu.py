@@ -155,10 +155,12 @@ def test_deferred_frozen_wgrad_matches_immediate():
         assert d <= 1e-5 * float(a[n].norm()) + 1e-7, n
 
 
-def test_step_graph_replay_matches_eager():
+@pytest.mark.parametrize("adam_in_graph", [True, False])
+def test_step_graph_replay_matches_eager(adam_in_graph):
     """A whole bf16 training step (forward, CTC, backward, side-stream frozen-weight gradients, Adam)
     captured as a HIP graph and replayed (train/step_graph.py) gives the same losses, parameters and
-    accumulated frozen-weight gradients as the same number of eager steps (dropout off)."""
+    accumulated frozen-weight gradients as the same number of eager steps (dropout off). Second
+    form (the data-parallel step): forward + backward captured, Adam eager after each replay."""
     from wav2vec2forbrain_amd import functional as Fn
     from wav2vec2forbrain_amd.optim import HipAdam
     from wav2vec2forbrain_amd.train.step_graph import StepGraph
@@ -184,10 +186,27 @@ def test_step_graph_replay_matches_eager():
             return out.metrics["ctc_loss"]
 
         with Fn.precision("bf16"):
-            if graph:
+            if graph and adam_in_graph:
                 sg = StepGraph(step, opt, warmup=2, warm_replays=0)
                 sg.capture()
                 losses = [sg.replay().clone() for _ in range(3)]
+                torch.cuda.synchronize()
+                sg.release()
+            elif graph:
+                def fwd_bwd():
+                    opt.zero_grad()
+                    out = model(batch)
+                    out.loss.backward()
+                    Fn.join_wgrad()
+                    return out.metrics["ctc_loss"]
+                for _ in range(2):
+                    step()
+                sg = StepGraph(fwd_bwd, None, warmup=0, warm_replays=0)
+                sg.capture()
+                losses = []
+                for _ in range(3):
+                    losses.append(sg.replay().clone())
+                    opt.step()
                 torch.cuda.synchronize()
                 sg.release()
             else:

@@ -24,11 +24,14 @@ import torch.distributed as dist
 
 class GradBucketReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, process_group=None,
-                 average: bool = True):
+                 average: bool = True, overlap: bool = True):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.average = average
+        # overlap=False: no collective from the backward hooks, finish() exchanges every bucket (the
+        # graph-replayed step: backward is captured, the RCCL exchange runs after each replay)
+        self.overlap = overlap
         cap = int(bucket_mb * 1024 * 1024 / 4)
         self.buckets: list[list[torch.nn.Parameter]] = []
         cur, size = [], 0
@@ -75,6 +78,8 @@ class GradBucketReducer:
         self.launched[bi] = True
 
     def _hook(self, p):
+        if not self.overlap:
+            return
         bi = self.bucket_of.get(p)
         if bi is None or self.launched[bi]:
             return

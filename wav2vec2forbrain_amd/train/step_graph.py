@@ -27,9 +27,11 @@ from .. import functional as Fn
 
 
 class StepGraph:
-    def __init__(self, step_fn, optimizer, warmup: int = 2, warm_replays: int = 2):
+    def __init__(self, step_fn, optimizer=None, warmup: int = 2, warm_replays: int = 2):
         """step_fn() runs one step on the current stream and returns the loss tensor (no host
-        syncs inside: model.sync_metrics must be False)."""
+        syncs inside: model.sync_metrics must be False). Pass the optimizer when step_fn includes
+        its update (captured); without it the update runs eagerly after each replay (the data-
+        parallel step: replay, gradient all-reduce, update)."""
         self.step_fn = step_fn
         self.opt = optimizer
         self.warmup = warmup
@@ -43,7 +45,8 @@ class StepGraph:
         lib = _lib.load()
         self.epoch = torch.zeros(1, dtype=torch.int64, device=dev)
         _lib.check(lib.b2p_set_seed_epoch(ctypes.c_void_p(self.epoch.data_ptr())), "b2p_set_seed_epoch")
-        self.opt.make_capturable(dev)
+        if self.opt is not None:
+            self.opt.make_capturable(dev)
         Fn.set_gemm_timing(False)
         s = torch.cuda.Stream(device=dev)
         s.wait_stream(torch.cuda.current_stream())
@@ -54,7 +57,8 @@ class StepGraph:
         torch.cuda.synchronize()
         # the host side of the captured step runs once now without updating anything: keep the
         # optimizer's host step counters as they were (after_replay advances them per replay)
-        steps = {p: st["step"].clone() for p, st in self.opt.state.items() if "step" in st}
+        steps = ({p: st["step"].clone() for p, st in self.opt.state.items() if "step" in st}
+                 if self.opt is not None else {})
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
             self.loss = self._one()
@@ -73,9 +77,11 @@ class StepGraph:
 
     def replay(self) -> torch.Tensor:
         """One training step; returns the (static) loss tensor — clone it to keep the value."""
-        self.opt.prepare_replay()
+        if self.opt is not None:
+            self.opt.prepare_replay()
         self.graph.replay()
-        self.opt.after_replay()
+        if self.opt is not None:
+            self.opt.after_replay()
         return self.loss
 
     def release(self) -> None:
