@@ -148,6 +148,10 @@ def main():
     # from the backward hooks
     reducer = GradBucketReducer(brain_params, overlap=not use_graph) if world > 1 else None
     # the frozen w2v's weight gradients (computed, as the reference does) run beside the GRU backward
+    if os.environ.get("B2P_DIAG_NO_FROZEN_GRAD") == "1":   # diagnostic only (not the reference's work)
+        for n, p in model.named_parameters():
+            if not n.startswith("brain_encoder."):
+                p.requires_grad_(False)
     if os.environ.get("B2P_DEFER_WGRAD", "1") != "0":
         Fn.set_deferred_wgrad([p for n, p in model.named_parameters() if not n.startswith("brain_encoder.")])
     batch = batch_on(cfg, device)

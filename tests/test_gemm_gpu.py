@@ -300,15 +300,17 @@ def test_bf16_epilogue_pre16_aux16_colsum(M, N, K):
     assert float((cs - ref_cs).abs().max()) <= 1e-3 * float(ref.abs().sum(0).max()) + 1e-4
 
 
-_TILE_ENV = {"small": {"B2P_GEMM16_PP": "0"}, "big": {"B2P_GEMM16_PP": "0", "B2P_GEMM16_BIG": "1"},
+_TILE_ENV = {"small": {"B2P_GEMM16_PP": "0", "B2P_GEMM16_K64": "0"},
+             "small64": {"B2P_GEMM16_PP": "0", "B2P_GEMM16_K64": "1"},
+             "big": {"B2P_GEMM16_PP": "0", "B2P_GEMM16_BIG": "1"},
              "pp": {"B2P_GEMM16_PP": "2"}}
 _TILE_CASES = [(lay, M, N, K) for lay in ("AB", "Ab", "ab") for (M, N, K) in ((4096, 1536, 512), (3000, 1544, 776))]
 
 
-@pytest.mark.parametrize("tile", ["small", "big", "pp"])
+@pytest.mark.parametrize("tile", ["small", "small64", "big", "pp"])
 def test_bf16_tile_configs(tile):
-    """Every bf16 tile configuration (128x128x32 4-wave; 256x128x64 8-wave; 256x256x64 8-wave
-    ping-pong), forced by environment (read once per process -> one subprocess per configuration),
+    """Every bf16 tile configuration (128x128x32 3-stage and 128x128x64 2-stage 4-wave; 256x128x64
+    8-wave; 256x256x64 8-wave ping-pong), forced by environment (read once per process -> one subprocess per configuration),
     against torch fp32 on the same bf16 operands with a full epilogue (bias, GELU, residual, bf16
     copy, fused column sums), plus split-K and batched launches.
     (mn-contiguous operands need ld % 8 == 0, so M, N are multiples of 8.)"""

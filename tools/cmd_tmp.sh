@@ -1,6 +1,6 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests -m gpu -k "step_graph" > gpurun_out/t.log 2>&1 || { tail -40 gpurun_out/t.log; exit 1; }
-tail -2 gpurun_out/t.log
-B2P_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 5 --warmup 2 > gpurun_out/ddp2.log 2>&1 || { tail -30 gpurun_out/ddp2.log; exit 1; }
-grep metric gpurun_out/ddp2.log | cut -c1-250
+for e in "B2P_DIAG_SKIP_SMALL_ACC=0" "B2P_DIAG_SKIP_SMALL_ACC=1"; do
+env $e timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b.log 2>&1 || { tail -30 gpurun_out/b.log; exit 1; }
+echo $e $(tail -1 gpurun_out/b.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'])")
+done

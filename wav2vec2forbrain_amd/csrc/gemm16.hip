@@ -246,6 +246,7 @@ struct Cfg {
   static constexpr int OCC = LDS > 80 * 1024 ? 1 : 2;           // workgroups per CU
 };
 using CfgSmall = Cfg<128, 128, 32, 3>;   // 4 waves, 2 workgroups/CU (default)
+using CfgSmall64 = Cfg<128, 128, 64, 2>; // 4 waves, 2 workgroups/CU, half the barriers (small grids)
 using CfgBig = Cfg<256, 128, 64, 3>;     // 8 waves, 1 workgroup/CU (measured slower on the step's shapes:
                                          // lock-stepped waves leave the MFMA pipe idle at every barrier)
 
@@ -622,6 +623,12 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
     b2p_set_error("gemm16: split-K chunk must be a multiple of 32");
     return 1;
   }
-  launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
+  // 64-deep K tiles (half the barriers) measured -4..6 % on grids of <= 2 tiles per CU slot in
+  // isolation (N = 768 encoder shapes) and +10 % at N = 2304, but no gain inside the step (graph
+  // replay, side stream beside): B2P_GEMM16_K64 = 0 never (default), 1 always, -1 by grid size.
+  static int k64 = getenv("B2P_GEMM16_K64") ? atoi(getenv("B2P_GEMM16_K64")) : 0;
+  const bool use64 = k64 == 1 || (k64 < 0 && nwg <= 512);
+  if (use64 && (ks == 1 || d.kchunk % 64 == 0)) launch_cfg<CfgSmall64>(d, ea, st, dim3((unsigned)nwg), tm, tn);
+  else launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   return 0;
 }

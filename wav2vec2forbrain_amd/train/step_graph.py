@@ -19,6 +19,7 @@ reference) keep accumulating in their .grad buffers across replays, exactly as i
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -48,7 +49,10 @@ class StepGraph:
         if self.opt is not None:
             self.opt.make_capturable(dev)
         Fn.set_gemm_timing(False)
-        s = torch.cuda.Stream(device=dev)
+        # the captured main stream at the highest priority: the frozen-weight gradient side stream
+        # (default priority) only takes CUs the main path leaves idle
+        prio = int(os.environ.get("B2P_GRAPH_PRIORITY", "1"))
+        s = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1] if prio else 0)
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(self.warmup):         # allocator / side-stream warm-up on the capture stream
@@ -60,7 +64,7 @@ class StepGraph:
         steps = ({p: st["step"].clone() for p, st in self.opt.state.items() if "step" in st}
                  if self.opt is not None else {})
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        with torch.cuda.graph(g, stream=s):
             self.loss = self._one()
         torch.cuda.synchronize()
         for p, t in steps.items():
