@@ -186,7 +186,7 @@ def main():
         from wav2vec2forbrain_amd.train.step_graph import StepGraph
         if world == 1:
             sg = StepGraph(step, opt)
-            run = lambda: sg.replay().clone()      # noqa: E731
+            run = sg.replay
         else:
             def fwd_bwd():
                 opt.zero_grad()
@@ -197,7 +197,7 @@ def main():
             sg = StepGraph(fwd_bwd, None)
 
             def run():
-                loss = sg.replay().clone()
+                loss = sg.replay()
                 reducer.finish()
                 opt.step()
                 return loss
@@ -206,14 +206,18 @@ def main():
         run = step
     if world > 1:
         dist.barrier()
+    # every step reads its loss back to the host: an async copy into pinned memory,
+    # stream-ordered after the step, instead of the reference's blocking .item()
+    loss_host = torch.zeros(args.steps, dtype=torch.float32).pin_memory()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    losses = [run() for _ in range(args.steps)]
+    for i in range(args.steps):
+        loss_host[i].copy_(run().reshape(()), non_blocking=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    losses = [float(v) for v in losses]
+    losses = loss_host.tolist()
     # GEMM roofline: HIP events around every GEMM launch of the same number of steps, run eagerly
     # right after the timed region (a captured graph cannot carry the per-launch events); the
     # kernels and their durations are the ones the graph replays.

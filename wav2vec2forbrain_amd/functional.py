@@ -91,6 +91,7 @@ def _fp32_if(name: str):
 # accumulate into p.grad in the GEMM epilogue (beta = 1) instead of autograd's separate add.
 # join_wgrad() orders the side stream back into the main stream (train step, optimizer).
 _DIAG_SKIP_ACC = os.environ.get("B2P_DIAG_SKIP_SMALL_ACC") == "1"   # diagnostic only
+_PP_SPLIT = os.environ.get("B2P_PP_SPLIT", "0") == "1"   # measured no gain in the step (opt-in)
 
 
 class _Deferred:
@@ -352,7 +353,13 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
         bn = 64 if (N <= 64 and not b16) else 128
         blocks = -(-M // 128) * -(-N // bn) * nz1 * nz2
         ks = 1
-        if blocks < 240:
+        tpp = -(-M // 256) * -(-N // 256) * nz1 * nz2
+        kpp = min(-(-160 // tpp), K // 1024)
+        if b16 and _PP_SPLIT and tpp * kpp >= 160 and kpp >= 2:
+            # 256x256 ping-pong tiles (gemm16.hip) over >= 1024-deep K slices, ~160-200 workgroups
+            # (the frozen weight gradients, K = tokens): fewer, larger tiles than the 128 x 128 split
+            ks = kpp
+        elif blocks < 240:
             ks = min(-(-512 // blocks), K // 1024)
         if ks >= 2:
             q = 64 if b16 else 32
