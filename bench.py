@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--bs", type=int, default=32)
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--evaluator", action="store_true",
+                    help="include the train evaluator's greedy CTC decode + WER (on the device) in every step")
     ap.add_argument("--graph", type=int, default=None,
                     help="1/0: replay the step as a captured HIP graph (default 1)")
     ap.add_argument("--config", choices=["base", "conformer"], default="base",
@@ -163,6 +165,14 @@ def main():
         if hasattr(m, "sync_metrics"):
             m.sync_metrics = False
 
+    def metrics(out):
+        # the loss, plus (--evaluator) the train evaluator's greedy-decode WER computed on the device
+        # (SURVEY 8(d1) "with the evaluator"; the reference does it on the host every step)
+        if not args.evaluator:
+            return out.metrics["ctc_loss"].reshape(1)
+        wer = Fn.ctc_greedy_wer(out.logits.detach(), batch.target)[0]
+        return torch.stack([out.metrics["ctc_loss"].reshape(()), wer])
+
     def step():
         opt.zero_grad()
         out = model(batch)
@@ -171,7 +181,7 @@ def main():
         if reducer is not None:
             reducer.finish()
         opt.step()
-        return out.metrics["ctc_loss"]
+        return metrics(out)
 
     for _ in range(args.warmup):
         step()
@@ -193,7 +203,7 @@ def main():
                 out = model(batch)
                 out.loss.backward()
                 Fn.join_wgrad()
-                return out.metrics["ctc_loss"]
+                return metrics(out)
             sg = StepGraph(fwd_bwd, None)
 
             def run():
@@ -208,16 +218,17 @@ def main():
         dist.barrier()
     # every step reads its loss back to the host: an async copy into pinned memory,
     # stream-ordered after the step, instead of the reference's blocking .item()
-    loss_host = torch.zeros(args.steps, dtype=torch.float32).pin_memory()
+    loss_host = torch.zeros(args.steps, 2 if args.evaluator else 1, dtype=torch.float32).pin_memory()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(args.steps):
-        loss_host[i].copy_(run().reshape(()), non_blocking=True)
+        loss_host[i].copy_(run(), non_blocking=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
-    losses = loss_host.tolist()
+    losses = loss_host[:, 0].tolist()
+    wers = loss_host[:, 1].tolist() if args.evaluator else None
     # GEMM roofline: HIP events around every GEMM launch of the same number of steps, run eagerly
     # right after the timed region (a captured graph cannot carry the per-launch events); the
     # kernels and their durations are the ones the graph replays.
@@ -262,6 +273,7 @@ def main():
                                 "train mode, unfreeze=brain_encoder, Adam"), "global_batch": args.bs * world,
                    "per_gpu_batch": args.bs, "seq_len": args.seq, "parallelism": f"dp{world}"},
         "ctc_loss": round(losses[-1], 5),
+        "train_evaluator": ({"on_device": True, "word_error_rate": round(wers[-1], 4)} if args.evaluator else None),
         "step_mode": "hip-graph replay" if use_graph else "eager",
         "samples_per_s": round(steps_per_s * args.bs, 2),
         "step_mfma_frac": round(step_tflop * steps_per_s / world / BF16_DENSE_PEAK_TFLOPS, 4),

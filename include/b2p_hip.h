@@ -219,6 +219,15 @@ int b2p_conv_weight_transpose_flip(const float* w, float* out, int64_t G, int64_
 
 /* weight norm over all dims but dim=2 (torch.nn.utils.parametrizations.weight_norm(dim=2),
  * transformers Wav2Vec2PositionalConvEmbedding): w[o,i,k] = g[k] * v[o,i,k] / ||v[:,:,k]|| */
+/* Greedy CTC decode + word errors of a batch on the device (replaces the train
+ * evaluator's host round trip, src/train/evaluator.py:69-129): argmax per frame (first maximum),
+ * group repeats, drop `blank`, cut after the first `eos`; words split at `delim`; per sample the
+ * word-level Levenshtein distance to the target (pads dropped) and the target's word count
+ * (WER = sum errs / sum nwords). out_tokens [B][T] int32 (first out_ntok[b] valid). T <= 1024. */
+int b2p_ctc_greedy_wer(const float* logits, int64_t B, int64_t T, int64_t C, const int64_t* target, int64_t S,
+                       int blank, int eos, int delim, int32_t* out_tokens, int32_t* out_ntok, int32_t* errs,
+                       int32_t* nwords, b2p_stream_t stream);
+
 /* Grouped positional conv of wav2vec2 on bf16 MFMA (csrc/posconv16.hip; 48 channels per group,
  * 128 taps, padding 64 + SamePad, T <= 256), replacing the implicit-conv GEMMs of
  * Wav2Vec2PositionalConvEmbedding (modeling_wav2vec2.py, reached from

@@ -1,0 +1,75 @@
+"""On-device greedy CTC decode + word error rate (csrc/decode.hip) against the host
+path of the reference's train evaluator (src/train/evaluator.py:69-129): transformers'
+Wav2Vec2CTCTokenizer.batch_decode on a local copy of the wav2vec2 32-token CTC vocabulary (the
+hub tokenizer is unreachable offline; parity of the vocabulary itself is unpinned), the
+cut-after-"</s>" step, and torcheval's WordErrorRate restated (sum of word edit distances over
+sum of target words)."""
+import json
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+VOCAB = ["<pad>", "<s>", "</s>", "<unk>", "|", "E", "T", "A", "O", "N", "I", "H", "S", "R", "D", "L", "U", "M",
+         "W", "C", "F", "G", "Y", "P", "B", "V", "K", "'", "X", "J", "Q", "Z"]
+
+
+def _edit(a, b):
+    prev = list(range(len(b) + 1))
+    for i, x in enumerate(a, 1):
+        cur = [i] + [0] * len(b)
+        for j, y in enumerate(b, 1):
+            cur[j] = min(prev[j] + 1, cur[j - 1] + 1, prev[j - 1] + (x != y))
+        prev = cur
+    return prev[-1]
+
+
+def _host_reference(logits, target, tok):
+    pred = tok.batch_decode(logits.argmax(-1).cpu().numpy(), group_tokens=True)
+    pred = [p[:p.find("</s>") + 4] if p.find("</s>") != -1 else p for p in pred]
+    lab = tok.batch_decode(target.cpu().numpy(), group_tokens=False)
+    errs = [_edit(p.split(), t.split()) for p, t in zip(pred, lab)]
+    nw = [len(t.split()) for t in lab]
+    return pred, errs, nw
+
+
+def test_ctc_greedy_wer_matches_host_evaluator(tmp_path):
+    from transformers import Wav2Vec2CTCTokenizer
+    from wav2vec2forbrain_amd import functional as Fn
+    f = tmp_path / "vocab.json"
+    f.write_text(json.dumps({t: i for i, t in enumerate(VOCAB)}))
+    tok = Wav2Vec2CTCTokenizer(str(f))
+    g = torch.Generator().manual_seed(3)
+    B, T, C, S = 12, 249, 32, 90
+    # frame ids with long runs, blanks, delimiters, occasional specials; logits peaked at them
+    ids = torch.randint(4, C, (B, T), generator=g)
+    ids[torch.rand(B, T, generator=g) < 0.35] = 0
+    ids[torch.rand(B, T, generator=g) < 0.08] = 4
+    run = torch.rand(B, T, generator=g) < 0.5
+    for t in range(1, T):
+        ids[:, t] = torch.where(run[:, t], ids[:, t - 1], ids[:, t])
+    ids[0, 100] = 2            # an EOS mid-sequence: the prediction is cut after it
+    ids[1, 50:52] = 1          # <s> inside a word
+    logits = torch.randn(B, T, C, generator=g)
+    logits.scatter_(2, ids.unsqueeze(-1), 8.0)
+    target = torch.randint(5, C, (B, S), generator=g)
+    target[torch.rand(B, S, generator=g) < 0.18] = 4
+    lens = torch.randint(20, S + 1, (B,), generator=g)
+    target[torch.arange(S).unsqueeze(0) >= lens.unsqueeze(1)] = 0
+    pred_s, errs_ref, nw_ref = _host_reference(logits, target, tok)
+    wer, errs, nw, toks, ntok = Fn.ctc_greedy_wer(logits.cuda(), target.cuda())
+    assert errs.cpu().tolist() == errs_ref
+    assert nw.cpu().tolist() == nw_ref
+    assert abs(float(wer) - sum(errs_ref) / sum(nw_ref)) < 1e-6
+    for b in range(B):   # the collapsed token ids decode to the host evaluator's prediction string
+        s = tok.decode(toks[b, :int(ntok[b])].cpu().tolist(), group_tokens=False)
+        assert s == pred_s[b], (b, s, pred_s[b])
+    # a perfect prediction: zero errors
+    perfect = torch.full((1, T, C), -5.0)
+    seq = [x for x in target[3].tolist() if x != 0]
+    for t, x in enumerate(seq):
+        perfect[0, 2 * t, x] = 5.0
+        perfect[0, 2 * t + 1, 0] = 5.0
+    w1, e1, n1, _, _ = Fn.ctc_greedy_wer(perfect.cuda(), target[3:4].cuda())
+    assert int(e1[0]) == 0 and int(n1[0]) == nw_ref[3] and float(w1) == 0.0

@@ -1,4 +1,6 @@
 set -e
 mkdir -p gpurun_out
-timeout -k 10 300 python -u bench.py --no-cpu-baseline > gpurun_out/b.log 2>&1 || { tail -30 gpurun_out/b.log; exit 1; }
-tail -1 gpurun_out/b.log | cut -c1-300
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_decode_gpu.py > gpurun_out/t.log 2>&1 || { tail -40 gpurun_out/t.log; exit 1; }
+tail -2 gpurun_out/t.log
+timeout -k 10 300 python -u bench.py --no-cpu-baseline --evaluator > gpurun_out/b.log 2>&1 || { tail -30 gpurun_out/b.log; exit 1; }
+tail -1 gpurun_out/b.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['ms_per_step'], d['train_evaluator'], d['ctc_loss'])"

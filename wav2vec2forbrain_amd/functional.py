@@ -1434,6 +1434,26 @@ def ctc_loss(logits, targets, in_lens, tgt_lens, blank=0):
     return _CTC.apply(logits.contiguous(), targets, in_lens, tgt_lens, blank)
 
 
+def ctc_greedy_wer(logits, targets, blank=0, eos=2, delim=4):
+    """Device-side greedy CTC decode + word error rate of a batch (csrc/decode.hip): the train
+    evaluator's metric (reference src/train/evaluator.py:69-129) without the host round trip.
+    Defaults are the wav2vec2 CTC vocab ids (<pad>=0 blank, </s>=2, '|'=4). Returns
+    (wer 0-d tensor, errs (B,) int32, nwords (B,) int32, tokens (B,T) int32, ntok (B,) int32)."""
+    _chk(logits, "ctc_greedy_wer.logits")
+    B, T, C = logits.shape
+    targets = targets.to(torch.int64).contiguous()
+    S = targets.shape[1]
+    dev = logits.device
+    tok = torch.empty(B, T, device=dev, dtype=torch.int32)
+    ntok = torch.empty(B, device=dev, dtype=torch.int32)
+    errs = torch.empty(B, device=dev, dtype=torch.int32)
+    nw = torch.empty(B, device=dev, dtype=torch.int32)
+    _lib.call("b2p_ctc_greedy_wer", _p(logits), B, T, C, targets.data_ptr(), S, blank, eos, delim, tok.data_ptr(),
+              ntok.data_ptr(), errs.data_ptr(), nw.data_ptr(), _st())
+    wer = errs.sum().float() / nw.sum().clamp_min(1).float()
+    return wer, errs, nw, tok, ntok
+
+
 # =====================================================================================
 # Conformer (transformers Wav2Vec2ConformerEncoderLayer, rotary variant) — reference
 # src/model/w2v_conformer_custom_feat_extractor.py:62-112

@@ -1,7 +1,7 @@
-"""Host-side evaluators — a minimal mirror of reference src/train/evaluator.py:20-120 (loss
-tracking, greedy CTC decode, WER/CER). The reference uses torcheval / edit_distance (absent
-here); the edit distance is restated. Evaluation metrics are outside the accelerated hot path
-(SURVEY 8(f1))."""
+"""Evaluators — a minimal mirror of reference src/train/evaluator.py:20-120 (loss tracking, greedy
+CTC decode, WER/CER). Train/val batches on the GPU get their word errors from the device decode
+(functional.ctc_greedy_wer, csrc/decode.hip); the host path (test mode, CER, CPU
+tensors) restates the reference's torcheval / edit_distance metrics, which are absent here."""
 from __future__ import annotations
 
 from dataclasses import dataclass, field
@@ -57,6 +57,17 @@ class Evaluator:
         if isinstance(loss, torch.Tensor):
             loss = loss.item()
         self.result.losses.append(float(loss))
+        if self.decode and sample.target is not None and predictions.logits.is_cuda and self.mode != "test":
+            # word errors on the device (csrc/decode.hip): no argmax / strings round trip per step;
+            # the sums stay on the device until evaluate()
+            from .. import functional as Fn
+            ids = {t: i for i, t in enumerate(self.vocab)}
+            _, errs, nw, _, _ = Fn.ctc_greedy_wer(predictions.logits.detach().contiguous(), sample.target,
+                                                  blank=ids.get("<pad>", 0), eos=ids.get("</s>", 2),
+                                                  delim=ids.get("|", 4))
+            self.dev_errs = errs.sum() + getattr(self, "dev_errs", 0)
+            self.dev_words = nw.sum() + getattr(self, "dev_words", 0)
+            return
         if self.decode and sample.target is not None:
             pred = predictions.logits.argmax(-1).cpu().tolist()
             tgt = sample.target.cpu().tolist()
@@ -76,6 +87,8 @@ class Evaluator:
         return self.result.get_average_loss()
 
     def evaluate(self) -> EpochResult:
+        if getattr(self, "dev_words", None) is not None:
+            self.result.metrics["word_error_rate"] = float(self.dev_errs) / max(float(self.dev_words), 1.0)
         if self.decode and self.words:
             self.result.metrics["word_error_rate"] = self.word_errs / self.words
             self.result.metrics["char_error_rate"] = self.char_errs / self.chars
