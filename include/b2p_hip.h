@@ -302,12 +302,15 @@ int b2p_gru_hprev(const float* out, const float* h0, float* hp, int64_t B, int64
  * (row max + log2 sum of the log2e-scaled scores, saved for backward). Dropout keep mask =
  * b2p_keep(seed, ((b*nh + h)*T + q)*T + key), identical to b2p_softmax_fwd's. bwd writes
  * [dQ | dK | dV] into dqkv (f32, may be NULL) and/or dqkv16 (bf16, may be NULL), same layout as qkv;
- * delta_ws: B*nh*T floats of workspace (row constants sum_key P_d dP_d). */
+ * delta_ws: B*nh*T floats of workspace (row constants sum_key P_d dP_d). mask (optional, drop_p > 0):
+ * uint32 [B][nh][T][8], written by fwd as the keep bits of each row (key k = bit k%32 of word k/32)
+ * and read by bwd instead of re-hashing every (q, key) twice; NULL: bwd recomputes the hash. */
 int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
-                   int64_t dh, float scale, float drop_p, uint64_t drop_seed, b2p_stream_t stream);
+                   int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
+                   b2p_stream_t stream);
 int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws,
                    float* dqkv, void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh,
-                   float scale, float drop_p, uint64_t drop_seed, b2p_stream_t stream);
+                   float scale, float drop_p, uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream);
 
 /* ------------------------------------------------------------------ CTC
  * log_softmax + nn.CTCLoss(blank=0, reduction="mean", zero_infinity=True)

@@ -175,10 +175,15 @@ def test_gru_layer_bf16_persistent(H, B, T, h0, unfold):
 
 @pytest.mark.parametrize("B,T,nh,p", [(2, 249, 12, 0.0), (2, 249, 12, 0.1), (3, 100, 4, 0.1), (1, 17, 2, 0.0),
                                        (2, 256, 3, 0.1)])
-def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p):
+@pytest.mark.parametrize("variant", ["hash", "mask", "epoch"])
+def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
     """csrc/attn16.hip (bf16 MFMA, scores on-chip) vs the unfused fp32 attention core (GEMM ->
     softmax/dropout kernel -> GEMM) on the same bf16-rounded q/k/v and the SAME dropout mask
-    (both hash ((b*nh+h)*T+q)*T+key). Tolerance: relative L2 1e-2 on O, 2e-2 on dQ/dK/dV."""
+    (both hash ((b*nh+h)*T+q)*T+key). Tolerance: relative L2 1e-2 on O, 2e-2 on dQ/dK/dV.
+    variant: hash = backward re-hashes the mask; mask = backward reads the forward's keep bits
+    (must equal the re-hashed result bit for bit); epoch = both paths under a graph-replay seed
+    counter (the fused forward, fused backward and unfused kernels must offset the seed alike)."""
+    import ctypes
     Fn = _fn()
     torch.manual_seed(7)
     dh = 64
@@ -186,13 +191,24 @@ def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p):
     qkv = (torch.randn(B * T, 3 * D) * 0.7).to(torch.bfloat16).float().cuda()
     dO = torch.randn(B * T, D).to(torch.bfloat16).float().cuda()
     seed = 1234
-    with Fn.precision("fp32"):
-        P, Pd, O = Fn._attn_core_fwd(qkv, B, T, nh, dh, p, seed)
-        dref = Fn._attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p, seed)
-    q16 = qkv.to(torch.bfloat16)
-    O16, lse2 = Fn._attn16_fwd(q16, B, T, nh, dh, p, seed)
-    dq32, dq16 = Fn._attn16_bwd(q16, dO.to(torch.bfloat16), lse2, B, T, nh, dh, p, seed)
-    torch.cuda.synchronize()
+    ctr = torch.full((1,), 7, dtype=torch.int64, device="cuda")
+    lib = Fn._lib.load()
+    if variant == "epoch":
+        Fn._lib.check(lib.b2p_set_seed_epoch(ctypes.c_void_p(ctr.data_ptr())), "set_seed_epoch")
+    try:
+        with Fn.precision("fp32"):
+            P, Pd, O = Fn._attn_core_fwd(qkv, B, T, nh, dh, p, seed)
+            dref = Fn._attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p, seed)
+        q16 = qkv.to(torch.bfloat16)
+        O16, lse2, mask = Fn._attn16_fwd(q16, B, T, nh, dh, p, seed, want_mask=True)
+        dq32, dq16 = Fn._attn16_bwd(q16, dO.to(torch.bfloat16), lse2, B, T, nh, dh, p, seed,
+                                    mask=mask if variant == "mask" else None)
+        if variant == "mask" and p > 0:
+            h32, _ = Fn._attn16_bwd(q16, dO.to(torch.bfloat16), lse2, B, T, nh, dh, p, seed)
+            assert torch.equal(h32, dq32)
+        torch.cuda.synchronize()
+    finally:
+        Fn._lib.check(lib.b2p_set_seed_epoch(None), "set_seed_epoch")
     rel = lambda a, b: float((a.float() - b).norm() / b.norm())
     assert rel(O16, O) < 1e-2
     for i, name in enumerate(("dQ", "dK", "dV")):

@@ -16,6 +16,7 @@
 // Dropout: keep(b, h, q, key) = b2p_keep(seed, ((b*nh + h)*T + q)*T + key) — the same mask the
 // unfused softmax kernel draws, so both paths agree element for element.
 #include "common.h"
+#include <type_traits>
 #include "../../include/b2p_hip.h"
 
 namespace {
@@ -101,10 +102,11 @@ __device__ __forceinline__ float keep_scale(const DropCfg& dc, uint64_t idx) {
 
 // ------------------------------------------------------------------------------------------ forward
 // qkv16 [B*T][3*D] bf16 (q | k | v, head-major inside each); O16 [B*T][D] bf16; lse2 [B][nh][T]
-template <bool DROP>
+template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: keep bits in memory
 __global__ void __launch_bounds__(256) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
-                                                    float* __restrict__ lse2, int T, int nh, float scale, DropCfg dc) {
-  dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
+                                                    float* __restrict__ lse2, int T, int nh, float scale, DropCfg dc,
+                                                    uint32_t* __restrict__ maskw) {
+  constexpr bool DROP = DM != 0;
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
@@ -169,13 +171,22 @@ __global__ void __launch_bounds__(256) attn16_fwd_k(const uint16_t* __restrict__
   for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
+    uint32_t word = 0;   // keep bits of keys 32c .. 32c+31 (this lane's 8 of them)
 #pragma unroll
     for (int half = 0; half < 2; ++half)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int key = (2 * c + half) * 16 + 4 * g + i;
-        s[2 * c + half][i] *= inv * (key < T ? keep_scale<DROP>(dc, rowidx + key) : 0.f);
+        const float ks = key < T ? keep_scale<DROP>(dc, rowidx + key) : 0.f;
+        if (DROP) word |= (ks != 0.f ? 1u : 0u) << (half * 16 + 4 * g + i);
+        s[2 * c + half][i] *= inv * ks;
       }
+    if (DM == 2) {
+      // the mask as bits for the backward kernels ([b][h][q][8] words): OR over the 4 lanes of a query
+      word |= (uint32_t)__shfl_xor((int)word, 16, 64);
+      word |= (uint32_t)__shfl_xor((int)word, 32, 64);
+      if (qok && g == 0) maskw[(((int64_t)b * nh + h) * T + q) * 8 + c] = word;
+    }
     const bf16x8 bp = pack_acc(s[2 * c], s[2 * c + 1]);
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt)
@@ -192,17 +203,20 @@ __global__ void __launch_bounds__(256) attn16_fwd_k(const uint16_t* __restrict__
 // ------------------------------------------------------------------------------------ backward dK dV
 // dO16 [B*T][D] bf16; delta [B][nh][T] from the dQ kernel; writes dK, dV into dqkv (fp32 and/or
 // bf16) columns [D + h*64, ...) and [2D + h*64, ...).
-template <bool DROP>
+template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: keep bits in memory
 __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restrict__ qkv, const float* __restrict__ delta,
                                                         const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                         float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
-                                                        int nh, float scale, DropCfg dc) {
+                                                        int nh, float scale, DropCfg dc,
+                                                        const uint32_t* __restrict__ maskw) {
+  constexpr bool DROP = DM != 0;
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Qimg = smem;
   char* dOimg = smem + TMAX * 128;
   float* lse_s = reinterpret_cast<float*>(smem + 2 * TMAX * 128);
   float* del_s = lse_s + TMAX;
+  uint32_t* msk_s = reinterpret_cast<uint32_t*>(del_s + TMAX);   // [q][2]: this block's 64 keys' bits
   int kb, h, b;
   block_coords(kb, h, b);
   const int D = nh * DH;
@@ -216,6 +230,11 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
     const int64_t o = ((int64_t)b * nh + h) * T + qq;
     del_s[qq] = qq < T ? delta[o] : 0.f;
     lse_s[qq] = qq < T ? lse2[o] : 0.f;
+    if (DM == 2) {   // the keep bits of keys 64kb .. 64kb+63 for every query row
+      const uint2 wv = qq < T ? *reinterpret_cast<const uint2*>(maskw + o * 8 + 2 * kb) : make_uint2(0, 0);
+      msk_s[2 * qq] = wv.x;
+      msk_s[2 * qq + 1] = wv.y;
+    }
   }
   const int key = kb * 64 + w * 16 + lr;
   const bool kok = key < T;
@@ -237,6 +256,13 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
   const int nchunk = (T + 31) >> 5;
   for (int c = 0; c < nchunk; ++c) {
     f32x4 pd[2], ds[2];
+    uint32_t mw[2][4];   // keep-bit words (from the forward, staged in LDS) of this chunk's queries
+    if (DM == 2) {
+#pragma unroll
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) mw[half][i] = msk_s[2 * ((2 * c + half) * 16 + 4 * g + i) + ((key >> 5) & 1)];
+    }
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
       const int qt = 2 * c + half;
@@ -252,7 +278,9 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
         const int qq = qt * 16 + 4 * g + i;
         const bool ok = kok && qq < T;
         const float p = ok ? exp2_fast(sv[i] * c2 - lse_s[qq]) : 0.f;
-        const float ksc = ok ? keep_scale<DROP>(dc, (bh * T + qq) * (uint64_t)T + key) : 0.f;
+        const float ksc = !ok ? 0.f
+                          : (DM == 2) ? (((mw[half][i] >> (key & 31)) & 1u) ? dc.scale : 0.f)
+                                            : keep_scale<DROP>(dc, (bh * T + qq) * (uint64_t)T + key);
         pd[half][i] = p * ksc;
         ds[half][i] = p * (dp[i] * ksc - del_s[qq]);
       }
@@ -279,11 +307,13 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
 // the kernel recomputes (not as dO . O from the rounded bf16 O), so sum_key dS = 0 holds to fp32
 // rounding — otherwise the residual feeds a systematic, Q-correlated error into dK. Pass 1 keeps
 // P and dP*keep in registers, pass 2 forms dS and dQ^T += K^T dS^T.
-template <bool DROP>
+template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: keep bits in memory
 __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restrict__ qkv, float* __restrict__ delta,
                                                        const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                        float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
-                                                       int nh, float scale, DropCfg dc) {
+                                                       int nh, float scale, DropCfg dc,
+                                                       const uint32_t* __restrict__ maskw) {
+  constexpr bool DROP = DM != 0;
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
@@ -312,6 +342,12 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
   __syncthreads();
   const float c2 = scale * LOG2E;
   const uint64_t rowidx = (uint64_t)rowc * (uint64_t)T;
+  uint32_t mw[8];   // this query row's keep bits (from the forward)
+  if (DM == 2) {
+    const uint4* mp = reinterpret_cast<const uint4*>(maskw + (int64_t)rowc * 8);
+    const uint4 m0 = qok ? mp[0] : make_uint4(0, 0, 0, 0), m1 = qok ? mp[1] : make_uint4(0, 0, 0, 0);
+    mw[0] = m0.x; mw[1] = m0.y; mw[2] = m0.z; mw[3] = m0.w; mw[4] = m1.x; mw[5] = m1.y; mw[6] = m1.z; mw[7] = m1.w;
+  }
   f32x4 P[16], PD[16];
   float dl = 0.f;
 #pragma unroll
@@ -327,7 +363,9 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
       const int key = kt * 16 + 4 * g + i;
       const bool ok = qok && key < T;
       const float p = ok ? exp2_fast(sv[i] * c2 - ls) : 0.f;
-      const float pd = ok ? dp[i] * keep_scale<DROP>(dc, rowidx + key) : 0.f;
+      const float kp = (DM == 2) ? (((mw[kt >> 1] >> ((kt & 1) * 16 + 4 * g + i)) & 1u) ? dc.scale : 0.f)
+                                       : keep_scale<DROP>(dc, rowidx + key);
+      const float pd = ok ? dp[i] * kp : 0.f;
       P[kt][i] = p;
       PD[kt][i] = pd;
       dl += p * pd;
@@ -367,7 +405,7 @@ DropCfg drop_cfg(float p, uint64_t seed) {
   return d;
 }
 constexpr size_t FWD_LDS = 2 * TMAX * 128;
-constexpr size_t BWD_LDS = 2 * TMAX * 128 + 2 * TMAX * 4;
+constexpr size_t BWD_LDS = 2 * TMAX * 128 + 2 * TMAX * 4 + 2 * TMAX * 4;
 
 template <typename K>
 int set_lds(K kern, size_t bytes) {
@@ -378,38 +416,45 @@ int init_attrs() {
   static int done = -1;
   if (done >= 0) return done;
   int rc = 0;
-  rc |= set_lds(attn16_fwd_k<false>, FWD_LDS);
-  rc |= set_lds(attn16_fwd_k<true>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<false>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<true>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<false>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<true>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<0>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<1>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<2>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<0>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<1>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<2>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<0>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<1>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<2>, FWD_LDS);
   done = rc;
   return rc;
 }
 }  // namespace
 
 extern "C" int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
-                              int64_t dh, float scale, float drop_p, uint64_t drop_seed, b2p_stream_t stream) {
+                              int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
+                              b2p_stream_t stream) {
   B2P_CHECK_ARG(qkv16 && O16 && lse2, "attn16_fwd: NULL pointer");
   B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_fwd: needs head size 64 and T <= 256");
   if (B <= 0) return 0;
   if (init_attrs()) return 2;
   dim3 grid((unsigned)((T + 63) / 64), (unsigned)nh, (unsigned)B);
   const DropCfg dc = drop_cfg(drop_p, drop_seed);
-  if (drop_p > 0.f)
-    hipLaunchKernelGGL(attn16_fwd_k<true>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
-                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc);
+  if (drop_p > 0.f && mask)
+    hipLaunchKernelGGL(attn16_fwd_k<2>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
+                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, mask);
+  else if (drop_p > 0.f)
+    hipLaunchKernelGGL(attn16_fwd_k<1>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
+                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, (uint32_t*)nullptr);
   else
-    hipLaunchKernelGGL(attn16_fwd_k<false>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
-                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc);
+    hipLaunchKernelGGL(attn16_fwd_k<0>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
+                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, (uint32_t*)nullptr);
   B2P_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws, float* dqkv,
                               void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh, float scale, float drop_p,
-                              uint64_t drop_seed, b2p_stream_t stream) {
+                              uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream) {
   B2P_CHECK_ARG(qkv16 && dO16 && lse2 && delta_ws && (dqkv || dqkv16), "attn16_bwd: NULL pointer");
   B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_bwd: needs head size 64 and T <= 256");
   if (B <= 0) return 0;
@@ -419,17 +464,16 @@ extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* 
   hipStream_t st = (hipStream_t)stream;
   const uint16_t *q = (const uint16_t*)qkv16, *d = (const uint16_t*)dO16;
   uint16_t* d16 = (uint16_t*)dqkv16;
-  if (drop_p > 0.f) {
-    hipLaunchKernelGGL(attn16_bwd_dq_k<true>, grid, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
-                       (int)nh, scale, dc);
-    hipLaunchKernelGGL(attn16_bwd_dkv_k<true>, grid, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
-                       (int)nh, scale, dc);
-  } else {
-    hipLaunchKernelGGL(attn16_bwd_dq_k<false>, grid, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
-                       (int)nh, scale, dc);
-    hipLaunchKernelGGL(attn16_bwd_dkv_k<false>, grid, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
-                       (int)nh, scale, dc);
-  }
+  auto run = [&](auto dm) {
+    constexpr int DM = decltype(dm)::value;
+    hipLaunchKernelGGL(attn16_bwd_dq_k<DM>, grid, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
+                       (int)nh, scale, dc, mask);
+    hipLaunchKernelGGL(attn16_bwd_dkv_k<DM>, grid, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
+                       (int)nh, scale, dc, mask);
+  };
+  if (drop_p > 0.f && mask) run(std::integral_constant<int, 2>());
+  else if (drop_p > 0.f) run(std::integral_constant<int, 1>());
+  else run(std::integral_constant<int, 0>());
   B2P_CHECK_LAUNCH();
   return 0;
 }

@@ -1103,24 +1103,27 @@ def attn16_ok(T, dh) -> bool:
     return dh == 64 and 0 < T <= 256
 
 
-def _attn16_fwd(qkv16, B, T, nh, dh, p_attn, seed):
-    """qkv16 (B*T, 3D) bf16 -> O16 (B*T, D) bf16, lse2 (B, nh, T) f32 (fused, scores stay on-chip)."""
+def _attn16_fwd(qkv16, B, T, nh, dh, p_attn, seed, want_mask=False):
+    """qkv16 (B*T, 3D) bf16 -> O16 (B*T, D) bf16, lse2 (B, nh, T) f32 (fused, scores stay on-chip)
+    [, mask: the dropout keep bits (B, nh, T, 8) int32 for the backward, None without dropout]."""
     dev = qkv16.device
     O16 = torch.empty(B * T, nh * dh, device=dev, dtype=BF16)
     lse2 = torch.empty(B, nh, T, device=dev)
+    mask = torch.empty(B, nh, T, 8, device=dev, dtype=torch.int32) if (want_mask and p_attn > 0) else None
     _lib.call("b2p_attn16_fwd", _p(qkv16), _p(O16), _p(lse2), B, T, nh, dh, float(dh ** -0.5), float(p_attn),
-              seed, _st())
-    return O16, lse2
+              seed, None if mask is None else mask.data_ptr(), _st())
+    return (O16, lse2, mask) if want_mask else (O16, lse2)
 
 
-def _attn16_bwd(qkv16, dO16, lse2, B, T, nh, dh, p_attn, seed, want32=True):
-    """-> dqkv (B*T, 3D) f32 (or None) and its bf16 copy."""
+def _attn16_bwd(qkv16, dO16, lse2, B, T, nh, dh, p_attn, seed, want32=True, mask=None):
+    """-> dqkv (B*T, 3D) f32 (or None) and its bf16 copy (mask: the forward's keep bits, or None to
+    re-hash)."""
     dev = qkv16.device
     dqkv = torch.empty(B * T, 3 * nh * dh, device=dev) if want32 else None
     d16 = torch.empty(B * T, 3 * nh * dh, device=dev, dtype=BF16)
     delta = torch.empty(B, nh, T, device=dev)
     _lib.call("b2p_attn16_bwd", _p(qkv16), _p(dO16), _p(lse2), _p(delta), _p(dqkv), _p(d16), B, T, nh, dh,
-              float(dh ** -0.5), float(p_attn), seed, _st())
+              float(dh ** -0.5), float(p_attn), seed, None if mask is None else mask.data_ptr(), _st())
     return dqkv, d16
 
 
@@ -1247,8 +1250,8 @@ class _EncoderLayer16(torch.autograd.Function):
         if fused:
             qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16)     # bf16 only: attention operand
             gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), None, 3 * D, bias=bqkv, C16=qkv)
-            O16, P = _attn16_fwd(qkv, B, T, nh, dh, p_attn, seeds[0])   # P slot holds lse2
-            Pd = None
+            # P slot: lse2, Pd slot: the dropout keep bits for the backward
+            O16, P, Pd = _attn16_fwd(qkv, B, T, nh, dh, p_attn, seeds[0], want_mask=True)
         else:
             qkv = torch.empty(NT, 3 * D, device=dev)
             gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), qkv, 3 * D, bias=bqkv)
@@ -1346,7 +1349,7 @@ class _EncoderLayer16(torch.autograd.Function):
         if ctx.fused:
             dO16 = torch.empty(NT, D, device=dev, dtype=BF16)
             gemm(NT, D, D, op(dz1_16, 0, D, True), op(wot16, 0, D, True), None, D, C16=dO16)
-            dqkv, dqkv16 = _attn16_bwd(qkv, dO16, P, B, T, nh, dh, p_attn, seeds[0])
+            dqkv, dqkv16 = _attn16_bwd(qkv, dO16, P, B, T, nh, dh, p_attn, seeds[0], mask=Pd)
             del dO16
         else:
             dO = torch.empty(NT, D, device=dev)
