@@ -60,16 +60,18 @@ def batch_on(cfg, device):
     return b.cuda() if device != "cpu" else b
 
 
-def cpu_baseline(bs_sample=8, L=1024, bs_metric=32):
+def cpu_baseline(bs_sample=8, L=1024, bs_metric=32, kind="base"):
     """The CPU oracle (torch-CPU fp32 restatement, oracle/b2p2t_oracle.py) timed on the host on a
     bounded sample of the same workload: one warm-up + 2 timed fwd+bwd+Adam steps at bs=bs_sample,
     scaled linearly to bs_metric."""
-    from oracle.b2p2t_oracle import loss_and_grads, adam_step
+    from oracle.b2p2t_oracle import loss_and_grads, conformer_loss_and_grads, adam_step
     from tests.helpers import oracle_cfg
-    cfg = make_config(bs_sample, L)
+    cfg = make_config(bs_sample, L, kind)
     ocfg = oracle_cfg(cfg)
     ocfg.hidden_dropout = ocfg.activation_dropout = ocfg.attention_dropout = ocfg.final_dropout = 0.1
     ocfg.layerdrop = 0.1
+    if kind == "conformer":
+        ocfg.conformer_conv_dropout = 0.1
     model = build(cfg, "cpu")
     sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
     from tests.golden.configs import make_batch
@@ -80,7 +82,10 @@ def cpu_baseline(bs_sample=8, L=1024, bs_metric=32):
     state = {k: (torch.zeros_like(sd[k]), torch.zeros_like(sd[k])) for k in brain}
 
     def step(i):
-        loss, grads = loss_and_grads(sd, b, ocfg, training=True)
+        if kind == "conformer":
+            loss, grads, _bn = conformer_loss_and_grads(sd, b, ocfg, training=True)
+        else:
+            loss, grads = loss_and_grads(sd, b, ocfg, training=True)
         for k in brain:
             m, v = state[k]
             sd[k], m, v = adam_step(sd[k], grads[k], m, v, i + 1, 1e-3)
@@ -266,7 +271,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (x~N(0,1) 256-ch windows, random-init weights of the wav2vec2-base architecture)",
+        "data": "synthetic (x~N(0,1) 256-ch windows, random-init weights of the "
+                + ("wav2vec2-base" if args.config == "base" else "wav2vec2-conformer-rope-large") + " architecture)",
         "config": {"workload": ("b2p2t_gru+w2v wav2vec2-base (12L/768), GRU H256x2 bidir, train mode, "
                                 "unfreeze=brain_encoder, Adam") if args.config == "base" else
                                ("b2p2t_gru+w2v_conformer rope-large (24L/1024, k31), GRU H512x3 bidir, fc [256], "
@@ -279,24 +285,29 @@ def main():
         "step_mfma_frac": round(step_tflop * steps_per_s / world / BF16_DENSE_PEAK_TFLOPS, 4),
         "roofline": {"bound": "mfma", "kernel": "b2p_gemm (all GEMM launches of the step)",
                      "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": gemm_traffic(),
+                     "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": gemm_traffic(args.config),
                      "launches": gemm_n, "avg_launch_us": round(gemm_ms * 1e3 / max(gemm_n, 1), 2),
                      "algorithmic_flop_per_launch": round(gemm_flops / max(gemm_n, 1), 1)},
     }
     if args.config != "base":
         res["metric"] = "train steps/sec + CTC loss, b2p2t_gru+w2v_conformer bs=32 seq=1024"
-    if world == 1 and not args.no_cpu_baseline and args.config == "base":
-        res["cpu_baseline"] = cpu_baseline(L=args.seq)
+    if world == 1 and not args.no_cpu_baseline:
+        # the Conformer-large sample is 4 samples (one step is ~7x the base model's FLOPs)
+        res["cpu_baseline"] = cpu_baseline(bs_sample=8 if args.config == "base" else 4, L=args.seq,
+                                           bs_metric=args.bs, kind=args.config)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
 
 
-def gemm_traffic():
+def gemm_traffic(kind="base"):
     """HBM bytes per GEMM launch from the newest committed PMC measurement of this same bench command
-    (profiles/*_gemm_traffic.json, written by tools/round_profile.sh: FETCH_SIZE x2 + WRITE_SIZE)."""
+    (profiles/*_gemm_traffic.json for the base config, profiles/*_gemm_traffic_conformer.json for
+    --config conformer; written by tools/round_profile.sh: FETCH_SIZE x2 + WRITE_SIZE); None when the
+    config has no measurement."""
     import glob
-    fs = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic.json")), key=os.path.getmtime)
+    fs = glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic*.json"))
+    fs = sorted((f for f in fs if f.endswith("_conformer.json") == (kind == "conformer")), key=os.path.getmtime)
     if not fs:
         return None
     d = json.load(open(fs[-1]))

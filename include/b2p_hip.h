@@ -347,6 +347,12 @@ int b2p_adam_recs(const int64_t* recs, int ntensors, float lr, double beta1, dou
                   float weight_decay, float bias_c1, float bias_c2_sqrt, const float* lr_dev, double* step_dev,
                   float* hyper_dev, b2p_stream_t stream);
 
+/* dst += src (fp32) for ntensors records {dst, src, numel} read from HOST memory and passed in the
+ * kernel arguments (96 per launch; capturable): the per-step accumulation of the small gradients of
+ * frozen parameters into their .grad (src/train/train_loop.py:44,66 never zeroes them), one launch
+ * instead of one elementwise add per tensor. */
+int b2p_accum_recs(const int64_t* recs, int ntensors, b2p_stream_t stream);
+
 /* dropout with an extra output scale: y = x * keep(seed, i) * scale / (1-p) (macaron half-step) */
 int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t seed, float scale,
                        b2p_stream_t stream);

@@ -355,6 +355,40 @@ def test_adam_matches_torch():
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
 
 
+def test_accum_recs_multi_tensor():
+    """b2p_accum_recs (one launch, records by value) == per-tensor dst += src, incl. > 96 records
+    (two launches), an empty tensor and one larger than the grid stride; and the deferred small-grad
+    path of functional.flush_wgrad (p.grad None -> takes g; else accumulated) equals torch's adds."""
+    import ctypes
+    Fn = _fn()
+    torch.manual_seed(11)
+    sizes = [768, 1, 3072, 0, 5000000] + [int(n) for n in torch.randint(1, 3000, (110,))]
+    dst = [torch.randn(n, device="cuda") for n in sizes]
+    src = [torch.randn(n, device="cuda") for n in sizes]
+    ref = [d + s for d, s in zip(dst, src)]
+    recs = []
+    for d, s in zip(dst, src):
+        recs += [d.data_ptr(), s.data_ptr(), d.numel()]
+    arr = (ctypes.c_int64 * len(recs))(*recs)
+    Fn._lib.call("b2p_accum_recs", arr, len(sizes), Fn._st())
+    torch.cuda.synchronize()
+    for a, b in zip(dst, ref):
+        assert torch.equal(a, b)
+    # through the deferral queue
+    ps = [torch.nn.Parameter(torch.randn(7, 5, device="cuda")) for _ in range(4)]
+    ps[0].grad = None
+    for p in ps[1:]:
+        p.grad = torch.randn_like(p)
+    gs = [torch.randn_like(p) for p in ps]
+    want = [g.clone() if p.grad is None else p.grad + g for p, g in zip(ps, gs)]
+    for p, g in zip(ps, gs):
+        Fn._defer_acc(p, g)
+    Fn.join_wgrad()
+    torch.cuda.synchronize()
+    for p, w in zip(ps, want):
+        assert torch.equal(p.grad, w)
+
+
 def test_conformer_elementwise_kernels():
     """rotary (fwd + transpose), GLU, depthwise conv, BatchNorm+SiLU against torch fp32."""
     Fn = _fn()

@@ -89,6 +89,21 @@ __global__ void __launch_bounds__(NTH) adam_rec_k(const AdamRecs recs, float lr,
     p[i] = pi - step * (mi / denom);
   }
 }
+
+// gradient accumulation dst[i] += src[i] over many small tensors in one launch (records by value:
+// capturable, nothing uploaded). blockIdx.y = record, blockIdx.x strides its elements.
+constexpr int ACC_MAXR = 96;
+struct AccRecs {
+  int64_t r[ACC_MAXR][3];   // dst, src, numel
+};
+__global__ void __launch_bounds__(NTH) accum_rec_k(const AccRecs recs) {
+  const int64_t* rec = recs.r[blockIdx.y];
+  float* __restrict__ dst = reinterpret_cast<float*>(rec[0]);
+  const float* __restrict__ src = reinterpret_cast<const float*>(rec[1]);
+  const int64_t n = rec[2];
+  const int64_t stride = (int64_t)gridDim.x * NTH;
+  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += stride) dst[i] += src[i];
+}
 }  // namespace
 
 extern "C" int b2p_seed_epoch_step(uint64_t* dev_counter, b2p_stream_t stream) {
@@ -154,6 +169,27 @@ extern "C" int b2p_adam_multi(const int64_t* table, int ntensors, int64_t max_nu
   if (bx > 4096) bx = 4096;
   hipLaunchKernelGGL(adam_k, dim3((unsigned)bx, (unsigned)ntensors), dim3(NTH), 0, (hipStream_t)stream, table, lr,
                      beta1, beta2, eps, weight_decay, bias_c1, bias_c2_sqrt, (const float*)nullptr);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_accum_recs(const int64_t* recs, int ntensors, b2p_stream_t stream) {
+  B2P_CHECK_ARG(recs != nullptr || ntensors == 0, "accum_recs: NULL records");
+  B2P_CHECK_ARG(ntensors >= 0, "accum_recs: bad tensor count");
+  for (int c0 = 0; c0 < ntensors; c0 += ACC_MAXR) {
+    const int nc = ntensors - c0 < ACC_MAXR ? ntensors - c0 : ACC_MAXR;
+    AccRecs a;
+    int64_t maxn = 0;
+    for (int i = 0; i < nc; ++i) {
+      for (int k = 0; k < 3; ++k) a.r[i][k] = recs[3 * (c0 + i) + k];
+      B2P_CHECK_ARG(a.r[i][2] <= 0 || (a.r[i][0] && a.r[i][1]), "accum_recs: NULL tensor in a record");
+      maxn = a.r[i][2] > maxn ? a.r[i][2] : maxn;
+    }
+    if (maxn <= 0) continue;
+    int64_t bx = (maxn + (int64_t)NTH * PER_THREAD - 1) / ((int64_t)NTH * PER_THREAD);
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(accum_rec_k, dim3((unsigned)bx, (unsigned)nc), dim3(NTH), 0, (hipStream_t)stream, a);
+  }
   B2P_CHECK_LAUNCH();
   return 0;
 }

@@ -97,6 +97,7 @@ _PP_SPLIT = os.environ.get("B2P_PP_SPLIT", "0") == "1"   # measured no gain in t
 class _Deferred:
     ids: set = set()
     queue: list = []          # (fn, tensors used, key = id of the parameter it updates)
+    accs: list = []           # (parameter, small gradient) pairs accumulated in one launch
     sides: list = []          # side streams (B2P_SIDE_STREAMS, default 1: several concurrent weight-
                               # gradient streams starved the main stream, 15.1 -> 17.2-18.8 ms/step)
     lane: dict = {}           # parameter id -> side stream index (fixed: one stream per parameter)
@@ -121,10 +122,32 @@ def _acc_param(p, g) -> None:
 
 
 def _defer_acc(p, g) -> None:
-    """Accumulate a ready gradient tensor into p.grad on the side stream."""
+    """Accumulate a ready gradient tensor into p.grad on the side stream (all of a flush's small
+    accumulations go out as ONE multi-tensor launch, b2p_accum_recs)."""
     if _DIAG_SKIP_ACC:
         return
-    _Deferred.queue.append((lambda: _acc_param(p, g), (g,), id(p)))
+    _Deferred.accs.append((p, g))
+
+
+def _flush_accs(sd) -> None:
+    """The queued small-gradient accumulations on side stream sd: a parameter without .grad takes
+    the tensor itself, the rest are batched into b2p_accum_recs records {p.grad, g, numel}."""
+    recs, n = [], 0
+    with torch.cuda.stream(sd):
+        for p, g in _Deferred.accs:
+            g.record_stream(sd)
+            if p.grad is None:
+                p.grad = g
+            elif (p.grad.is_contiguous() and g.is_contiguous() and p.grad.dtype == g.dtype == torch.float32
+                  and p.grad.numel() == g.numel() and p.grad.device == g.device):
+                recs += [p.grad.data_ptr(), g.data_ptr(), g.numel()]
+                n += 1
+            else:
+                p.grad.add_(g)
+        if n:
+            arr = (ctypes.c_int64 * len(recs))(*recs)
+            _lib.call("b2p_accum_recs", arr, n, _st())
+    _Deferred.accs.clear()
 
 
 def _defer_wgemm_rows(ps, fn, *tensors) -> None:
@@ -193,7 +216,7 @@ def flush_wgrad(after=None) -> None:
     the main stream has queued so far. Each parameter's work always goes to the same side stream
     (its accumulations stay ordered); independent weight-gradient GEMMs on different streams run
     concurrently, which fills the chip without split-K partial sums and their reduce launches."""
-    if not _Deferred.queue:
+    if not _Deferred.queue and not _Deferred.accs:
         return
     main = torch.cuda.current_stream()
     if not _Deferred.sides:
@@ -215,6 +238,8 @@ def flush_wgrad(after=None) -> None:
                 fn()
             for t in ts:
                 t.record_stream(sd)
+        if _Deferred.accs:
+            _flush_accs(sides[0])
     finally:
         _state.nosplit = old
     _Deferred.queue.clear()
