@@ -65,7 +65,9 @@ typedef struct {
   int32_t conv_T_out, conv_T_in, conv_stride, conv_pad, conv_Cg;
   int32_t dtype;         /* 0 = fp32 (converted while staged into LDS), 1 = bf16: both operands
                           * bf16 selects the LDS-DMA kernel (global_load_lds, ptr/ld/bs/Cg
-                          * multiples of 8 elements, K % 8 == 0 for a k-contiguous operand)  */
+                          * multiples of 8 elements, K % 8 == 0 for a k-contiguous operand);
+                          * 2 = fp16 (precision 2 only): the same kernel on fp16 MFMA, plain
+                          * (non-conv) operands                                               */
   int64_t conv_sample_stride;
 } b2p_operand;
 
@@ -172,6 +174,12 @@ int b2p_layernorm_bwd16(const float* dy, const float* x, const float* gamma, con
 /* fp32 -> bf16 (round to nearest even), the GEMM operand copy of a weight or activation
  * (master copies stay fp32; replaces the implicit .to(bfloat16) of autocast) */
 int b2p_cast_bf16(const float* x, uint16_t* y, int64_t n, b2p_stream_t stream);
+/* y[r][c] = 16-bit(x[r][c]) for an R x C block of a row-major fp32 matrix (row stride ldx) into a
+ * 16-bit matrix of row stride ldy; fp16 = 0: bf16, 1: fp16 (both round-to-nearest-even, the
+ * conversion the fp32-operand GEMM applies while staging). Stages fp32 GEMM operands for the
+ * 16-bit LDS-DMA kernel (b2p_operand.dtype 1 / 2). */
+int b2p_cast16_2d(const float* x, int64_t R, int64_t C, int64_t ldx, uint16_t* y, int64_t ldy, int fp16,
+                  b2p_stream_t stream);
 /* y[c * ldy + col0 + r] = bf16(x[r * C + c]): transposed bf16 copy of an R x C fp32 matrix (cached
  * k-contiguous weight operands of the backward-data GEMMs) */
 int b2p_transpose_bf16(const float* x, uint16_t* y, int64_t R, int64_t C, int64_t ldy, int64_t col0,

@@ -369,3 +369,46 @@ def _check_tile_case(layout, M, N, K):
     _close(o16.float(), want, "bf16", scale=want.abs().max().item())
     cs = Fn.colsum_from_parts(parts, torch.empty(N, device="cuda"))
     assert float((cs - want.sum(0)).abs().max()) <= 1e-4 * float(want.abs().sum(0).max())
+
+
+@pytest.mark.parametrize("fwd16", [False, True])
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 2048), (7968, 1024, 1024), (1000, 600, 4100)])
+def test_auto16_staged_operands(fwd16, M, N, K):
+    """fp32-operand GEMMs above the auto-16 threshold run on staged 16-bit operand copies
+    (b2p_cast16_2d + the LDS-DMA kernel, fp16 MFMA under forward_f16): same operand rounding as the
+    fp32-operand kernel, so both agree to fp32 accumulation-order noise; and both match torch fp32
+    on the rounded operands. Layouts NT, NN, TN; an epilogue (bias + GELU + residual) on NT;
+    K = 4100 (not a multiple of 8) stays on the fp32-operand kernel."""
+    import wav2vec2forbrain_amd.functional as Fn
+    torch.manual_seed(3)
+    dt = torch.float16 if fwd16 else torch.bfloat16
+    a = torch.randn(M, K, device="cuda")
+    w = torch.randn(N, K, device="cuda") * 0.05
+    b = torch.randn(K, N, device="cuda") * 0.05
+    at = torch.randn(K, M, device="cuda")
+    bias = torch.randn(N, device="cuda")
+    res = torch.randn(M, N, device="cuda")
+    r = lambda t: t.to(dt).float()
+    cases = [
+        (lambda o: Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), o, N, bias=bias, act=Fn.ACT["gelu"],
+                           residual=res),
+         F.gelu(r(a) @ r(w).t() + bias) + res),
+        (lambda o: Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(b, 0, N, False), o, N), r(a) @ r(b)),
+        (lambda o: Fn.gemm(M, N, K, Fn.op(at, 0, M, False), Fn.op(b, 0, N, False), o, N), r(at).t() @ r(b)),
+    ]
+    old = Fn._AUTO16
+    try:
+        with Fn.precision("bf16"), Fn.forward_f16(fwd16):
+            for run, ref in cases:
+                outs = []
+                for auto in (True, False):
+                    Fn._AUTO16 = auto
+                    o = torch.empty(M, N, device="cuda")
+                    run(o)
+                    outs.append(o)
+                torch.cuda.synchronize()
+                scale = ref.abs().max().item()
+                assert (outs[0] - ref).abs().max().item() <= 2e-3 * scale
+                assert (outs[0] - outs[1]).abs().max().item() <= 1e-4 * scale
+    finally:
+        Fn._AUTO16 = old

@@ -389,6 +389,29 @@ def test_accum_recs_multi_tensor():
         assert torch.equal(p.grad, w)
 
 
+@pytest.mark.parametrize("B,T,D,K", [(2, 249, 1024, 31), (1, 65, 70, 31), (3, 130, 128, 5), (1, 3, 64, 31)])
+def test_dwconv_tiled_shapes(B, T, D, K):
+    """LDS-tiled depthwise conv (fwd, dx, dw) vs torch fp32 conv1d at the Conformer-large shape and
+    at ragged tails: T not a multiple of the 64-frame tile, channels not a multiple of 64, T < K."""
+    Fn = _fn()
+    torch.manual_seed(12)
+    x = torch.randn(B, T, D, device="cuda")
+    w = torch.randn(D, 1, K, device="cuda")
+    xc, wc = x.clone().requires_grad_(True), w.clone().requires_grad_(True)
+    yc = F.conv1d(xc.transpose(1, 2), wc, padding=(K - 1) // 2, groups=D).transpose(1, 2)
+    y = torch.empty(B, T, D, device="cuda")
+    Fn._lib.call("b2p_dwconv_fwd", x.data_ptr(), w.data_ptr(), y.data_ptr(), B, T, D, K, Fn._st())
+    gy = torch.randn_like(yc)
+    gxc, gwc = torch.autograd.grad(yc, (xc, wc), gy)
+    dx = torch.empty(B, T, D, device="cuda")
+    dw = torch.empty(D, 1, K, device="cuda")
+    ws = torch.empty(int(Fn._lib.load().b2p_dwconv_bwd_workspace(B, T, D, K)), device="cuda")
+    Fn._lib.call("b2p_dwconv_bwd", x.data_ptr(), w.data_ptr(), gy.contiguous().data_ptr(), dx.data_ptr(),
+                 dw.data_ptr(), B, T, D, K, ws.data_ptr(), Fn._st())
+    torch.cuda.synchronize()
+    assert _rel(y, yc) < 1e-5 and _rel(dx, gxc) < 1e-5 and _rel(dw, gwc) < 1e-5
+
+
 def test_conformer_elementwise_kernels():
     """rotary (fwd + transpose), GLU, depthwise conv, BatchNorm+SiLU against torch fp32."""
     Fn = _fn()

@@ -77,50 +77,88 @@ __global__ void dwconv_fwd_k(const float* __restrict__ x, const float* __restric
   y[i] = acc;
 }
 
-// dx[b,s,c] = sum_k w[c,k] dy[b, s-k+p, c]
-__global__ void dwconv_bwd_x_k(const float* __restrict__ dy, const float* __restrict__ w, float* __restrict__ dx,
-                               int64_t B, int64_t T, int64_t C, int K) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= B * T * C) return;
-  const int64_t c = i % C, s = (i / C) % T, b = i / (C * T);
+constexpr int DW_TT = 64;   // frame tile of the weight-gradient partials
+
+// LDS-tiled depthwise conv (the Conformer's k31 'same' conv, TF conf ConvolutionModule): a block
+// owns 64 channels x 64 frames of one sample; the input frames [t0 - p, t0 + 64 + p) of its channels
+// are staged once in LDS (coalesced 256-B rows), every thread keeps its channel's taps in registers
+// and a sliding window of 16 + K - 1 frames, and writes 16 outputs (coalesced over channels).
+// FLIP: the input-gradient form dx[s] = sum_k w[k] dy[s - k + p] (taps reversed).
+constexpr int DWT_T = 64, DW_KMAX = 31;
+template <bool FLIP>
+__global__ void __launch_bounds__(256) dwconv_tile_k(const float* __restrict__ x, const float* __restrict__ w,
+                                                     float* __restrict__ y, int64_t T, int64_t C, int K) {
+  __shared__ float xs[DWT_T + DW_KMAX - 1][64];
+  const int cl = threadIdx.x & 63, tg = threadIdx.x >> 6;
+  const int64_t c = (int64_t)blockIdx.x * 64 + cl;
+  const int64_t t0 = (int64_t)blockIdx.y * DWT_T;
+  const int64_t b = blockIdx.z;
   const int p = (K - 1) / 2;
-  const float* db = dy + b * T * C + c;
-  const float* wc = w + c * K;
-  float acc = 0.f;
-  for (int k = 0; k < K; ++k) {
-    const int64_t t = s - k + p;
-    if (t >= 0 && t < T) acc += wc[k] * db[t * C];
+  const bool cok = c < C;
+  const float* xb = x + b * T * C + c;
+  for (int r = tg; r < DWT_T + K - 1; r += 4) {
+    const int64_t s = t0 - p + r;
+    xs[r][cl] = (cok && s >= 0 && s < T) ? xb[s * C] : 0.f;
   }
-  dx[i] = acc;
+  float wr[DW_KMAX];
+#pragma unroll
+  for (int k = 0; k < DW_KMAX; ++k) wr[k] = (cok && k < K) ? w[c * K + (FLIP ? K - 1 - k : k)] : 0.f;
+  __syncthreads();
+  constexpr int NO = DWT_T / 4;   // outputs per thread
+  float win[NO + DW_KMAX - 1];
+#pragma unroll
+  for (int j = 0; j < NO + DW_KMAX - 1; ++j) win[j] = (j < NO + K - 1) ? xs[tg * NO + j][cl] : 0.f;
+  float* yb = y + b * T * C + c;
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k < DW_KMAX; ++k) acc += wr[k] * win[o + k];
+    const int64_t t = t0 + tg * NO + o;
+    if (cok && t < T) yb[t * C] = acc;
+  }
 }
 
-// dw partials: block = (64 channels, 64-frame tile of one sample); part[(b*ntile + tile)][k][c]
-constexpr int DW_TT = 64;
-__global__ void __launch_bounds__(256) dwconv_bwd_w_k(const float* __restrict__ x, const float* __restrict__ dy,
-                                                      float* __restrict__ part, int64_t B, int64_t T, int64_t C,
-                                                      int K, int ntile) {
-  const int cl = threadIdx.x & 63, kg = threadIdx.x >> 6;     // 4 groups of taps
+// dw partials, LDS-tiled: part[(b*ntile + tile)][k][c] = sum_{t in tile} dy[t][c] x[t + k - p][c]
+__global__ void __launch_bounds__(256) dwconv_wgrad_tile_k(const float* __restrict__ x, const float* __restrict__ dy,
+                                                           float* __restrict__ part, int64_t T, int64_t C, int K,
+                                                           int ntile) {
+  __shared__ float xs[DWT_T + DW_KMAX - 1][64];
+  __shared__ float ds[DWT_T][64];
+  const int cl = threadIdx.x & 63, kg = threadIdx.x >> 6;   // taps 8kg .. 8kg+7
   const int64_t c = (int64_t)blockIdx.x * 64 + cl;
   const int tile = blockIdx.y % ntile;
   const int64_t b = blockIdx.y / ntile;
+  const int64_t t0 = (int64_t)tile * DWT_T;
   const int p = (K - 1) / 2;
-  const int64_t t0 = (int64_t)tile * DW_TT;
-  const int64_t t1 = t0 + DW_TT < T ? t0 + DW_TT : T;
-  float acc[8];
+  const bool cok = c < C;
+  const float* xb = x + b * T * C + c;
+  const float* db = dy + b * T * C + c;
+  for (int r = kg; r < DWT_T + K - 1; r += 4) {
+    const int64_t s = t0 - p + r;
+    xs[r][cl] = (cok && s >= 0 && s < T) ? xb[s * C] : 0.f;
+  }
+  for (int r = kg; r < DWT_T; r += 4) {
+    const int64_t t = t0 + r;
+    ds[r][cl] = (cok && t < T) ? db[t * C] : 0.f;
+  }
+  __syncthreads();
+  float acc[8], win[8];
 #pragma unroll
-  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
-  if (c < C) {
-    const float* xb = x + b * T * C + c;
-    const float* db = dy + b * T * C + c;
-    for (int64_t t = t0; t < t1; ++t) {
-      const float g = db[t * C];
+  for (int q = 0; q < 8; ++q) {
+    acc[q] = 0.f;
+    win[q] = xs[kg * 8 + q][cl];
+  }
+  for (int t = 0; t < DWT_T; ++t) {
+    const float g = ds[t][cl];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int k = kg * 8 + q;
-        const int64_t s = t + k - p;
-        if (k < K && s >= 0 && s < T) acc[q] += g * xb[s * C];
-      }
-    }
+    for (int q = 0; q < 8; ++q) acc[q] += g * win[q];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) win[q] = win[q + 1];
+    const int nr = t + 1 + kg * 8 + 7;
+    win[7] = nr < DWT_T + DW_KMAX - 1 ? xs[nr][cl] : 0.f;
+  }
+  if (cok) {
     float* pp = part + (int64_t)blockIdx.y * K * C;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
@@ -255,7 +293,11 @@ extern "C" int b2p_dwconv_fwd(const float* x, const float* w, float* y, int64_t 
   B2P_CHECK_ARG(K % 2 == 1, "dwconv: kernel size must be odd ('same' padding)");
   const int64_t n = B * T * C;
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(dwconv_fwd_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, w, y, B, T, C, K);
+  if (K <= DW_KMAX)
+    hipLaunchKernelGGL(dwconv_tile_k<false>, dim3((unsigned)((C + 63) / 64), (unsigned)((T + DWT_T - 1) / DWT_T),
+                                                  (unsigned)B), dim3(256), 0, (hipStream_t)stream, x, w, y, T, C, K);
+  else
+    hipLaunchKernelGGL(dwconv_fwd_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, w, y, B, T, C, K);
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -273,14 +315,16 @@ extern "C" int b2p_dwconv_bwd(const float* x, const float* w, const float* dy, f
   hipStream_t st = (hipStream_t)stream;
   const int64_t n = B * T * C;
   if (n <= 0) return 0;
-  if (dx) hipLaunchKernelGGL(dwconv_bwd_x_k, dim3(nblk(n)), dim3(256), 0, st, dy, w, dx, B, T, C, K);
+  if (dx)
+    hipLaunchKernelGGL(dwconv_tile_k<true>, dim3((unsigned)((C + 63) / 64), (unsigned)((T + DWT_T - 1) / DWT_T),
+                                                 (unsigned)B), dim3(256), 0, st, dy, w, dx, T, C, K);
   if (dw) {
     const int ntile = (int)((T + DW_TT - 1) / DW_TT);
     float* part = workspace;
     float* kc = part + B * ntile * (int64_t)K * C;
     float* p2 = kc + (int64_t)K * C;
-    hipLaunchKernelGGL(dwconv_bwd_w_k, dim3((unsigned)((C + 63) / 64), (unsigned)(B * ntile)), dim3(256), 0, st, x,
-                       dy, part, B, T, C, K, ntile);
+    hipLaunchKernelGGL(dwconv_wgrad_tile_k, dim3((unsigned)((C + 63) / 64), (unsigned)(B * ntile)), dim3(256), 0, st,
+                       x, dy, part, T, C, K, ntile);
     if (colsum_impl(part, nullptr, 1, B * ntile, (int64_t)K * C, (int64_t)K * C, 0, 0, kc, 0, p2, st)) return 1;
     hipLaunchKernelGGL(dw_transpose_k, dim3(nblk(C * K)), dim3(256), 0, st, kc, dw, C, K);
   }

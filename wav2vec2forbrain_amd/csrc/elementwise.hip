@@ -604,6 +604,50 @@ extern "C" int b2p_cast_bf16(const float* x, uint16_t* y, int64_t n, b2p_stream_
   return 0;
 }
 
+// R x C block cast to bf16 / fp16: one thread per 4 columns of a row (16-B loads, 8-B stores when
+// both strides and pointers allow, scalar otherwise)
+template <bool H, bool VEC>
+__global__ void __launch_bounds__(256) cast16_2d_k(const float* __restrict__ x, int64_t R, int64_t C, int64_t ldx,
+                                                   uint16_t* __restrict__ y, int64_t ldy) {
+  const int64_t c4 = (C + 3) / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= R * c4) return;
+  const int64_t r = i / c4, c = (i - r * c4) * 4;
+  const float* xs = x + r * ldx + c;
+  uint16_t* ys = y + r * ldy + c;
+  auto cvt = [](float v) -> uint16_t {
+    if constexpr (H) return __builtin_bit_cast(uint16_t, (_Float16)v);
+    else return b2p_bf16_bits(v);
+  };
+  if (VEC && c + 4 <= C) {
+    const float4 v = *reinterpret_cast<const float4*>(xs);
+    *reinterpret_cast<uint2*>(ys) = make_uint2((uint32_t)cvt(v.x) | ((uint32_t)cvt(v.y) << 16),
+                                               (uint32_t)cvt(v.z) | ((uint32_t)cvt(v.w) << 16));
+  } else {
+    for (int j = 0; j < 4 && c + j < C; ++j) ys[j] = cvt(xs[j]);
+  }
+}
+
+extern "C" int b2p_cast16_2d(const float* x, int64_t R, int64_t C, int64_t ldx, uint16_t* y, int64_t ldy, int fp16,
+                             b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && y, "cast16_2d: NULL pointer");
+  B2P_CHECK_ARG(R >= 0 && C >= 0 && ldx >= C && ldy >= C, "cast16_2d: bad shape / strides");
+  if (R == 0 || C == 0) return 0;
+  const bool vec = ((uintptr_t)x & 15u) == 0 && ((uintptr_t)y & 7u) == 0 && ldx % 4 == 0 && ldy % 4 == 0;
+  const int64_t n = R * ((C + 3) / 4);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  hipStream_t st = (hipStream_t)stream;
+  if (fp16) {
+    if (vec) hipLaunchKernelGGL((cast16_2d_k<true, true>), grid, dim3(256), 0, st, x, R, C, ldx, y, ldy);
+    else hipLaunchKernelGGL((cast16_2d_k<true, false>), grid, dim3(256), 0, st, x, R, C, ldx, y, ldy);
+  } else {
+    if (vec) hipLaunchKernelGGL((cast16_2d_k<false, true>), grid, dim3(256), 0, st, x, R, C, ldx, y, ldy);
+    else hipLaunchKernelGGL((cast16_2d_k<false, false>), grid, dim3(256), 0, st, x, R, C, ldx, y, ldy);
+  }
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 // y[c][r] = bf16(x[r][c]) for an R x C fp32 matrix written into columns col0 .. col0+R-1 of a
 // [C][ldy] bf16 matrix (several row blocks stacked side by side: the transposed [Wq; Wk; Wv]):
 // 64 x 64 tiles through LDS, reads and writes coalesced along the rows of x and y

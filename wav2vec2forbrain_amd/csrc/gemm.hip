@@ -406,8 +406,8 @@ bool aligned16(const void* p) { return ((uintptr_t)p & 15u) == 0; }
 int check_operand(const b2p_operand& o, const char* name) {
   B2P_CHECK_ARG(o.ptr != nullptr, "gemm: operand %s is NULL", name);
   B2P_CHECK_ARG(aligned16(o.ptr), "gemm: operand %s not 16-byte aligned", name);
-  B2P_CHECK_ARG(o.dtype == 0 || o.dtype == 1, "gemm: operand %s dtype must be 0 (fp32) or 1 (bf16)", name);
-  const int64_t v = o.dtype == 1 ? 8 : 4;   // elements per 16-byte vector
+  B2P_CHECK_ARG(o.dtype >= 0 && o.dtype <= 2, "gemm: operand %s dtype must be 0 (fp32), 1 (bf16) or 2 (fp16)", name);
+  const int64_t v = o.dtype != 0 ? 8 : 4;   // elements per 16-byte vector
   B2P_CHECK_ARG(o.ld % v == 0 && o.bs1 % v == 0 && o.bs2 % v == 0,
                 "gemm: operand %s strides must be multiples of %lld (ld=%lld)", name, (long long)v, (long long)o.ld);
   if (o.conv) {
@@ -433,9 +433,9 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   B2P_CHECK_ARG(d.ep.C != nullptr || d.ep.beta == 0.f, "gemm: beta != 0 needs C");
   if (check_operand(d.A, "A") || check_operand(d.B, "B")) return 1;
   B2P_CHECK_ARG(d.A.dtype == d.B.dtype, "gemm: operands must share a dtype");
-  const bool bf16_ops = d.A.dtype == 1;
+  const bool bf16_ops = d.A.dtype != 0;   // 16-bit operands: the LDS-DMA kernel (gemm16.hip)
   if (bf16_ops) {
-    B2P_CHECK_ARG(d.precision == 0, "gemm: bf16 operands need precision 0");
+    B2P_CHECK_ARG(d.precision == (d.A.dtype == 1 ? 0 : 2), "gemm: bf16 operands need precision 0, fp16 precision 2");
     B2P_CHECK_ARG(!(d.A.inner_is_k || d.B.inner_is_k) || d.K % 8 == 0,
                   "gemm: bf16 k-contiguous operand needs K %% 8 == 0 (K=%lld)", (long long)d.K);
     B2P_CHECK_ARG(!d.B.conv, "gemm: bf16 path supports a conv view on A only");

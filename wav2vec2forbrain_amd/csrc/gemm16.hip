@@ -33,6 +33,7 @@ __device__ __attribute__((aligned(16))) uint32_t g_zero_page[8];   // zero-initi
 
 typedef __attribute__((address_space(3))) void lds_t;
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8g __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void glds16(const void* src, lds_t* dst) {
   __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
@@ -250,7 +251,9 @@ using CfgSmall64 = Cfg<128, 128, 64, 2>; // 4 waves, 2 workgroups/CU, half the b
 using CfgBig = Cfg<256, 128, 64, 3>;     // 8 waves, 1 workgroup/CU (measured slower on the step's shapes:
                                          // lock-stepped waves leave the MFMA pipe idle at every barrier)
 
-template <class CF, bool AK, bool BK, bool ACONV>
+// H16: the operands are fp16 (Operand.dtype 2, precision 2) and feed v_mfma_f32_16x16x32_f16; the
+// data movement is the same 16-bit copy either way
+template <class CF, bool AK, bool BK, bool ACONV, bool H16 = false>
 __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_desc d, const EpiArgs ea, int tiles_m,
                                                                 int tiles_n) {
   constexpr int BM = CF::BM, BN = CF::BN, KT = CF::KT, S = CF::S, NT = CF::NT;
@@ -335,7 +338,11 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          if constexpr (H16)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8g, af[i]),
+                                                               __builtin_bit_cast(f16x8g, bfr[j]), acc[i][j], 0, 0, 0);
+          else
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
     cur = cur + 1 == S ? 0 : cur + 1;
     nxt = nxt + 1 == S ? 0 : nxt + 1;
@@ -566,6 +573,12 @@ template <class CF>
 static void launch_cfg(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st, dim3 grid, int tm, int tn) {
   const dim3 block(CF::NT);
   const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
+  if (d.A.dtype == 2) {   // fp16 operands (precision 2): plain operand pairs only
+    if (AK && BK) hipLaunchKernelGGL((gemm16_kernel<CF, true, true, false, true>), grid, block, 0, st, d, ea, tm, tn);
+    else if (AK) hipLaunchKernelGGL((gemm16_kernel<CF, true, false, false, true>), grid, block, 0, st, d, ea, tm, tn);
+    else hipLaunchKernelGGL((gemm16_kernel<CF, false, false, false, true>), grid, block, 0, st, d, ea, tm, tn);
+    return;
+  }
   if (AK && BK) {
     if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<CF, true, true, true>), grid, block, 0, st, d, ea, tm, tn);
     else hipLaunchKernelGGL((gemm16_kernel<CF, true, true, false>), grid, block, 0, st, d, ea, tm, tn);
@@ -589,7 +602,12 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   // grid that still fills the chip
   static int big_ok = getenv("B2P_GEMM16_BIG") ? atoi(getenv("B2P_GEMM16_BIG")) : 0;
   const int64_t tiles_big = ((d.M + 255) / 256) * ((d.N + 127) / 128);
-  const bool big = big_ok && ks == 1 && nz == 1 && !d.A.conv && d.K >= 512 && tiles_big >= 192;
+  const bool h16 = d.A.dtype == 2;
+  if (h16 && d.A.conv) {
+    b2p_set_error("gemm16: fp16 operands support plain (non-conv) views only");
+    return 1;
+  }
+  const bool big = !h16 && big_ok && ks == 1 && nz == 1 && !d.A.conv && d.K >= 512 && tiles_big >= 192;
   if (big) {
     const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 127) / 128);
     launch_cfg<CfgBig>(d, ea, st, dim3((unsigned)((int64_t)tm * tn)), tm, tn);
@@ -603,7 +621,7 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   static int pp_mode = getenv("B2P_GEMM16_PP") ? atoi(getenv("B2P_GEMM16_PP")) : 1;
   const int64_t tiles_pp = ((d.M + 255) / 256) * ((d.N + 255) / 256) * nz;
   const int64_t kper = ks > 1 ? (int64_t)d.kchunk : d.K;
-  const bool pp = !d.A.conv && (pp_mode == 2 || (pp_mode == 1 && ((tiles_pp >= 192 && kper >= 2048) || (ks > 1 && tiles_pp >= 160 && kper >= 1024))));
+  const bool pp = !h16 && !d.A.conv && (pp_mode == 2 || (pp_mode == 1 && ((tiles_pp >= 192 && kper >= 2048) || (ks > 1 && tiles_pp >= 160 && kper >= 1024))));
   if (pp) {
     const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 255) / 256);
     const dim3 grid((unsigned)tiles_pp), block(PP_NT);
@@ -628,7 +646,7 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   // replay, side stream beside): B2P_GEMM16_K64 = 0 never (default), 1 always, -1 by grid size.
   static int k64 = getenv("B2P_GEMM16_K64") ? atoi(getenv("B2P_GEMM16_K64")) : 0;
   const bool use64 = k64 == 1 || (k64 < 0 && nwg <= 512);
-  if (use64 && (ks == 1 || d.kchunk % 64 == 0)) launch_cfg<CfgSmall64>(d, ea, st, dim3((unsigned)nwg), tm, tn);
+  if (use64 && !h16 && (ks == 1 || d.kchunk % 64 == 0)) launch_cfg<CfgSmall64>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   else launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   return 0;
 }

@@ -368,13 +368,22 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     e.colsum_part = _p(colsum_part)
     d.ep = e
     d.precision = 2 if (_state.fwd16 and _state.prec == 0 and A.dtype == 0) else _prec()
+    keep16 = None
+    if _AUTO16 and _state.prec == 0 and A.dtype == 0 and B.dtype == 0 and _auto16_ok(M, N, K, A, B, nz1, nz2):
+        # fp32 operands of a large plain GEMM: stage 16-bit copies (the rounding the fp32-operand
+        # kernel applies while loading LDS) and run the LDS-DMA kernel (gemm16.hip) on them
+        h = d.precision == 2
+        dev = (C if C is not None else C16).device
+        keep16 = (_cast_operand(A, M, K, h, dev), _cast_operand(B, N, K, h, dev))
+        A, B = keep16[0][1], keep16[1][1]
+        d.A, d.B = A, B
     d.timing_family = timing or _GEMM_TIMING[0]
     d.flops = 2.0 * M * N * K * nz1 * nz2
     ws = None
     plain = (bias is None and pre_out is None and act == 0 and act_bwd == 0 and drop_p == 0.0 and residual is None
              and colsum_part is None and pre16 is None)
     if plain and K >= 2048 and not _state.nosplit:
-        b16 = A.dtype == 1
+        b16 = A.dtype != 0
         bn = 64 if (N <= 64 and not b16) else 128
         blocks = -(-M // 128) * -(-N // bn) * nz1 * nz2
         ks = 1
@@ -407,6 +416,40 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
 
 # tools/gemm_census.py: when a list, every gemm() call appends its shape record
 GEMM_LOG = None
+
+# fp32-operand GEMMs at least this large (2*M*N*K) are run on staged 16-bit operand copies
+_AUTO16 = os.environ.get("B2P_GEMM_AUTO16", "1") == "1"
+_AUTO16_MIN_FLOP = float(os.environ.get("B2P_GEMM_AUTO16_MIN_GFLOP", "2")) * 1e9
+
+
+def _auto16_ok(M, N, K, A, B, nz1, nz2) -> bool:
+    """Plain single-matrix operands (no implicit conv view, gather or batch) in a layout the 16-bit
+    kernel takes, and enough work to amortise the two cast passes."""
+    if nz1 * nz2 != 1 or A.conv or B.conv or A.gather1 or B.gather1:
+        return False
+    if not A.inner_is_k and B.inner_is_k:
+        return False
+    if (A.inner_is_k or B.inner_is_k) and K % 8 != 0:
+        return False
+    return 2.0 * M * N * K >= _AUTO16_MIN_FLOP and min(M, N) >= 64 and K >= 64
+
+
+def _cast_operand(o, mn, K, fp16, dev):
+    """16-bit compact copy of the logical (mn x K) operand o (row stride rounded up to 8 elements);
+    returns (buffer, Operand)."""
+    rows, cols = (mn, K) if o.inner_is_k else (K, mn)
+    ld16 = -(-cols // 8) * 8
+    buf = torch.empty(rows, ld16, device=dev, dtype=torch.float16 if fp16 else BF16)
+    _lib.call("b2p_cast16_2d", o.ptr, rows, cols, o.ld, buf.data_ptr(), ld16, int(fp16), _st())
+    n = Operand()
+    n.ptr = buf.data_ptr()
+    n.ld = ld16
+    n.bs1 = n.bs2 = 0
+    n.gather1 = None
+    n.inner_is_k = o.inner_is_k
+    n.conv = 0
+    n.dtype = 2 if fp16 else 1
+    return buf, n
 
 
 def mm_nt(x, W, out, bias=None, act=0, pre_out=None, drop_p=0.0, seed=0, residual=None, alpha=1.0, beta=0.0,
