@@ -83,11 +83,13 @@ def test_ctc_vs_torch(seed):
 
 @pytest.mark.parametrize("unfold", [False, True])
 @pytest.mark.parametrize("h0", [False, True])
-def test_gru_layer(unfold, h0):
+@pytest.mark.parametrize("B,H", [(5, 32), (13, 512)])
+def test_gru_layer(unfold, h0, B, H):
+    """Per-step GRU kernels (csrc/gru.hip: fp32 mode, and the H = 512 Conformer encoder in every
+    mode) vs the oracle GRU; B = 13 leaves a partial 8-row batch block."""
     Fn = _fn()
     from oracle.b2p2t_oracle import gru_direction, unfold as unfold_ref
     torch.manual_seed(3)
-    B, H = 5, 32
     if unfold:
         L, C, k, s = 60, 16, 8, 4
         xsrc = torch.randn(B, L, C)

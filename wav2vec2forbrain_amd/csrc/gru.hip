@@ -38,25 +38,44 @@ __global__ void __launch_bounds__(NTH) gru_fwd_step(const float* __restrict__ gi
   const int H4 = H >> 2;
   const int G3 = 3 * H;
 
-  // stage W rows (g*H + j0 + u) and h_{t-1} rows
+  // stage W rows (g*H + j0 + u) and h_{t-1} rows; the loads of a batch of SU float4 per thread are
+  // issued back to back before their LDS stores (one memory latency per batch, not per element)
   const float* wd = whh + (int64_t)d * G3 * H;
-  for (int i = tid; i < 3 * HU * H4; i += NTH) {
-    const int r = i / H4, c = i - r * H4;
-    const int g = r / HU, u = r - g * HU;
-    reinterpret_cast<float4*>(Ws + r * HP)[c] = reinterpret_cast<const float4*>(wd + (int64_t)(g * H + j0 + u) * H)[c];
-  }
-  for (int i = tid; i < BB * H4; i += NTH) {
-    const int r = i / H4, c = i - r * H4;
-    const int b = b0 + r;
-    float4 v = make_float4(0, 0, 0, 0);
-    if (b < B) {
-      if (s == 0) {
-        if (h0) v = reinterpret_cast<const float4*>(h0 + ((int64_t)d * B + b) * H)[c];
-      } else {
-        v = reinterpret_cast<const float4*>(out + ((int64_t)b * T + tprev) * ndir * H + (int64_t)d * H)[c];
+  constexpr int SU = 8;
+  const int nW = 3 * HU * H4, nH = BB * H4;
+  for (int i0 = tid; i0 < nW + nH; i0 += NTH * SU) {
+    float4 v[SU];
+#pragma unroll
+    for (int q = 0; q < SU; ++q) {
+      const int i = i0 + q * NTH;
+      v[q] = make_float4(0, 0, 0, 0);
+      if (i < nW) {
+        const int r = i / H4, c = i - r * H4;
+        const int g = r / HU, u = r - g * HU;
+        v[q] = reinterpret_cast<const float4*>(wd + (int64_t)(g * H + j0 + u) * H)[c];
+      } else if (i < nW + nH) {
+        const int r = (i - nW) / H4, c = (i - nW) - r * H4;
+        const int b = b0 + r;
+        if (b < B) {
+          if (s == 0) {
+            if (h0) v[q] = reinterpret_cast<const float4*>(h0 + ((int64_t)d * B + b) * H)[c];
+          } else {
+            v[q] = reinterpret_cast<const float4*>(out + ((int64_t)b * T + tprev) * ndir * H + (int64_t)d * H)[c];
+          }
+        }
       }
     }
-    reinterpret_cast<float4*>(Hs + r * HP)[c] = v;
+#pragma unroll
+    for (int q = 0; q < SU; ++q) {
+      const int i = i0 + q * NTH;
+      if (i < nW) {
+        const int r = i / H4, c = i - r * H4;
+        reinterpret_cast<float4*>(Ws + r * HP)[c] = v[q];
+      } else if (i < nW + nH) {
+        const int r = (i - nW) / H4, c = (i - nW) - r * H4;
+        reinterpret_cast<float4*>(Hs + r * HP)[c] = v[q];
+      }
+    }
   }
   __syncthreads();
 
@@ -133,24 +152,50 @@ __global__ void __launch_bounds__(NTH) gru_bwd_step(const float* __restrict__ do
   if (has_next) {
     const int tn = t_of(snext, d, T);
     const float* wd = whh + (int64_t)d * G3 * H;
-    for (int i = tid; i < HU * G3; i += NTH) {
-      const int g = i / HU, uu = i - g * HU;   // 8 consecutive floats of a W row per 8 lanes
-      Wt[uu * GP + g] = wd[(int64_t)g * H + j0 + uu];
-    }
+    // W column slice: per W row g, two float4 (units j0 .. j0+7) scattered into Wt[u][g]; dgh rows
+    // as float4. Loads batched SU per thread ahead of their LDS stores (latency once per batch).
+    constexpr int SU = 8;
     const int G34 = G3 >> 2;
-    for (int i = tid; i < BB * G34; i += NTH) {
-      const int r = i / G34, c = i - r * G34;
-      const int bb = b0 + r;
-      float4 v = make_float4(0, 0, 0, 0);
-      if (bb < B) v = reinterpret_cast<const float4*>(dgh + ((int64_t)bb * T + tn) * ndir * G3 + (int64_t)d * G3)[c];
-      reinterpret_cast<float4*>(Ds + r * GP)[c] = v;
+    const int nW = 2 * G3, nD = BB * G34;
+    for (int i0 = tid; i0 < nW + nD; i0 += NTH * SU) {
+      float4 v[SU];
+#pragma unroll
+      for (int q = 0; q < SU; ++q) {
+        const int i = i0 + q * NTH;
+        v[q] = make_float4(0, 0, 0, 0);
+        if (i < nW) {
+          const int g = i >> 1, hf = i & 1;
+          v[q] = *reinterpret_cast<const float4*>(wd + (int64_t)g * H + j0 + 4 * hf);
+        } else if (i < nW + nD) {
+          const int r = (i - nW) / G34, c = (i - nW) - r * G34;
+          const int bb = b0 + r;
+          if (bb < B) v[q] = reinterpret_cast<const float4*>(dgh + ((int64_t)bb * T + tn) * ndir * G3 + (int64_t)d * G3)[c];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < SU; ++q) {
+        const int i = i0 + q * NTH;
+        if (i < nW) {
+          const int g = i >> 1, hf = i & 1;
+          Wt[(4 * hf + 0) * GP + g] = v[q].x;
+          Wt[(4 * hf + 1) * GP + g] = v[q].y;
+          Wt[(4 * hf + 2) * GP + g] = v[q].z;
+          Wt[(4 * hf + 3) * GP + g] = v[q].w;
+        } else if (i < nW + nD) {
+          const int r = (i - nW) / G34, c = (i - nW) - r * G34;
+          reinterpret_cast<float4*>(Ds + r * GP)[c] = v[q];
+        }
+      }
     }
     __syncthreads();
-    const int gq = G3 / 4;
-    const float* wr = Wt + u * GP + ks * gq;
-    const float* dr = Ds + bl * GP + ks * gq;
+    const int gq4 = G3 / 16;   // float4 per quarter of the reduction
+    const float4* wr = reinterpret_cast<const float4*>(Wt + u * GP) + ks * gq4;
+    const float4* dr = reinterpret_cast<const float4*>(Ds + bl * GP) + ks * gq4;
     float acc = 0.f;
-    for (int g = 0; g < gq; ++g) acc += wr[g] * dr[g];
+    for (int g = 0; g < gq4; ++g) {
+      const float4 a = wr[g], e = dr[g];
+      acc += a.x * e.x + a.y * e.y + a.z * e.z + a.w * e.w;
+    }
     red[ks * 64 + p] = acc;
     __syncthreads();
     if (ks != 0) return;
@@ -233,6 +278,7 @@ extern "C" int b2p_gru_bwd(const float* dout, const float* whh, const float* out
                            int64_t T, int64_t H, int ndir, b2p_stream_t stream) {
   B2P_CHECK_ARG(dout && whh && out && saved && dgi && dgh && dhbuf, "gru_bwd: NULL pointer");
   B2P_CHECK_ARG(H % 16 == 0, "gru_bwd: hidden size must be a multiple of 16");
+  B2P_CHECK_ARG(HU == 8, "gru_bwd: the W slice staging assumes 8 hidden units per block");
   B2P_CHECK_ARG(ndir == 1 || ndir == 2, "gru_bwd: ndir must be 1 or 2");
   if (B <= 0 || T <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;

@@ -108,6 +108,11 @@ class _Deferred:
 def set_deferred_wgrad(params) -> None:
     """Parameters whose gradients may be deferred (frozen: not optimised, not all-reduced)."""
     _Deferred.ids = {id(p) for p in params if p is not None}
+    # frozen parameters by storage address: their staged 16-bit GEMM operand copies are cached
+    # (keyed by the tensor version, so an in-place load still invalidates them)
+    _CAST_CACHE.clear()
+    _FROZEN_PTR.clear()
+    _FROZEN_PTR.update({p.data_ptr(): p for p in params if p is not None and p.is_cuda})
 
 
 def _defer_ok(p) -> bool:
@@ -434,13 +439,29 @@ def _auto16_ok(M, N, K, A, B, nz1, nz2) -> bool:
     return 2.0 * M * N * K >= _AUTO16_MIN_FLOP and min(M, N) >= 64 and K >= 64
 
 
+_FROZEN_PTR: dict = {}   # data_ptr -> frozen parameter (set_deferred_wgrad)
+_CAST_CACHE: dict = {}   # (ptr, rows, cols, ld, fp16) -> (version, buffer) for frozen parameters
+
+
 def _cast_operand(o, mn, K, fp16, dev):
     """16-bit compact copy of the logical (mn x K) operand o (row stride rounded up to 8 elements);
-    returns (buffer, Operand)."""
+    returns (buffer, Operand). Copies of frozen parameters are cached across calls."""
     rows, cols = (mn, K) if o.inner_is_k else (K, mn)
     ld16 = -(-cols // 8) * 8
-    buf = torch.empty(rows, ld16, device=dev, dtype=torch.float16 if fp16 else BF16)
-    _lib.call("b2p_cast16_2d", o.ptr, rows, cols, o.ld, buf.data_ptr(), ld16, int(fp16), _st())
+    prm = _FROZEN_PTR.get(o.ptr)
+    key = (o.ptr, rows, cols, o.ld, bool(fp16))
+    buf = None
+    if prm is not None and prm.numel() >= rows * o.ld - (o.ld - cols):
+        hit = _CAST_CACHE.get(key)
+        if hit is not None and hit[0] == prm._version:
+            buf = hit[1]
+    else:
+        prm = None
+    if buf is None:
+        buf = torch.empty(rows, ld16, device=dev, dtype=torch.float16 if fp16 else BF16)
+        _lib.call("b2p_cast16_2d", o.ptr, rows, cols, o.ld, buf.data_ptr(), ld16, int(fp16), _st())
+        if prm is not None:
+            _CAST_CACHE[key] = (prm._version, buf)
     n = Operand()
     n.ptr = buf.data_ptr()
     n.ld = ld16
