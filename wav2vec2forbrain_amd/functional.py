@@ -1613,6 +1613,8 @@ class _FFNBlock(torch.autograd.Function):
         ng = ctx.needs_input_grad
         dy = dy.contiguous().view(NT, D)
         dz = _dropout_scaled(dy, p_hid, s_hid, scale)
+        if bf16_mode():
+            return _FFNBlock._backward16(ctx, dy, dz, x2, h, mean, rstd, pre, f, g, w1, w2)
         dw2 = db2 = dw1 = db1 = None
         if ng[5]:
             dw2 = torch.empty_like(w2)
@@ -1633,6 +1635,50 @@ class _FFNBlock(torch.autograd.Function):
         mm_nn(dpre, w1, dh)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
         return dx.view(ctx.shape), dg, db, dw1, db1, dw2, db2, None
+
+    @staticmethod
+    def _backward16(ctx, dy, dz, x2, h, mean, rstd, pre, f, g, w1, w2):
+        """bf16-operand backward (same math): dz, f, h cast once; dpre produced in bf16 by the
+        backward-data GEMM with the FFN1 bias gradient as fused column sums; weight gradients of
+        frozen parameters deferred (accumulated into .grad by the GEMM)."""
+        act, eps, p_act, p_hid, s_act, s_hid, scale = ctx.cfg
+        NT, D = x2.shape
+        F = w1.shape[0]
+        dev = x2.device
+        ng = ctx.needs_input_grad
+        dz16 = cast16(dz)
+        db2 = db1 = None
+        if ctx.has_b[1] and ng[6]:
+            db2 = torch.empty(D, device=dev)
+            colsum(dz, NT, D, db2)
+        dw2 = _wgrad16(w2, ng[5], dz16, D, cast16(f), F, NT)
+        dpre16 = torch.empty(NT, F, device=dev, dtype=BF16)
+        parts = colsum_parts_buf(NT, F, dev) if (ctx.has_b[0] and ng[4]) else None
+        gemm(NT, F, D, op(dz16, 0, D, True), op(weight16t(w2), 0, D, True), None, F, drop_p=p_act, seed=s_act,
+             act_bwd=act, aux=pre, C16=dpre16, colsum_part=parts)
+        if parts is not None:
+            db1 = colsum_from_parts(parts, torch.empty(F, device=dev))
+        dw1 = _wgrad16(w1, ng[3], dpre16, F, cast16(h), D, NT)
+        dh = torch.empty(NT, D, device=dev)
+        gemm(NT, D, F, op(dpre16, 0, F, True), op(weight16t(w1), 0, F, True), dh, D)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        return dx.view(ctx.shape), dg, db, dw1, db1, dw2, db2, None
+
+
+def _wgrad16(w, need, dy16, M, x16, N, NT, ldy=None, ldx=None, dy_off=0):
+    """Weight gradient dW[M][N] = dy16[:, off:off+M]^T x16 (bf16 operands, K = NT tokens): deferred
+    onto the side stream and accumulated into w.grad (beta = 1) for a frozen parameter, else
+    returned. None when not needed."""
+    if not need:
+        return None
+    ldy, ldx = ldy or M, ldx or N
+    if _defer_ok(w):
+        _defer_wgemm(w, lambda o, bt, a=dy16, b=x16: gemm(M, N, NT, op(a, dy_off, ldy, False), op(b, 0, ldx, False),
+                                                          o, N, beta=bt), dy16, x16)
+        return None
+    gw = torch.empty_like(w)
+    gemm(M, N, NT, op(dy16, dy_off, ldy, False), op(x16, 0, ldx, False), gw, N)
+    return gw
 
 
 _ROT = {}
@@ -1692,6 +1738,9 @@ class _ConformerAttnBlock(torch.autograd.Function):
         hr_ = h if hr is None else hr
         dy = dy.contiguous().view(NT, D)
         dz = _dropout_scaled(dy, p_out, seeds[1], 1.0)
+        if bf16_mode():
+            return _ConformerAttnBlock._backward16(ctx, dy, dz, x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv,
+                                                   wo, cos_t, sin_t)
         dwo = dbo = None
         if ng[9]:
             dwo = torch.empty_like(wo)
@@ -1723,6 +1772,49 @@ class _ConformerAttnBlock(torch.autograd.Function):
         else:
             for i, w in enumerate((wq, wk, wv)):
                 gemm(NT, D, D, op(dqkv, i * D, 3 * D, True), op(w, 0, D, False), dh, D, beta=0.0 if i == 0 else 1.0)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        return (dx.view(B, T, D), dg, db, *grads, dwo, dbo, None, None, None)
+
+    @staticmethod
+    def _backward16(ctx, dy, dz, x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo, cos_t, sin_t):
+        """bf16-operand backward (same math): every GEMM operand cast once, Q/K (and V without
+        rotary) input gradients as one GEMM over the concatenated transposed weights, frozen
+        weight gradients deferred."""
+        nh, eps, p_attn, p_out, seeds = ctx.cfg
+        B, T, D = ctx.shape
+        NT, hd = B * T, D // nh
+        dev = x2.device
+        ng = ctx.needs_input_grad
+        dz16 = cast16(dz)
+        dbo = None
+        if ctx.has_b[3] and ng[10]:
+            dbo = torch.empty(D, device=dev)
+            colsum(dz, NT, D, dbo)
+        dwo = _wgrad16(wo, ng[9], dz16, D, cast16(O), D, NT)
+        dO = torch.empty(NT, D, device=dev)
+        gemm(NT, D, D, op(dz16, 0, D, True), op(weight16t(wo), 0, D, True), dO, D)
+        dqkv = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, hd, p_attn, seeds[0])
+        del dO
+        dqkv16 = cast16(dqkv)
+        h16 = cast16(h)
+        hr16 = h16 if hr is None else cast16(hr)
+        grads = []
+        for i, (w, src16) in enumerate(((wq, hr16), (wk, hr16), (wv, h16))):
+            gb = None
+            if ctx.has_b[i] and ng[4 + 2 * i]:
+                gb = torch.empty(D, device=dev)
+                colsum(_view_off(dqkv, i * D), NT, D, gb, ld=3 * D)
+            grads += [_wgrad16(w, ng[3 + 2 * i], dqkv16, D, src16, D, NT, ldy=3 * D, dy_off=i * D), gb]
+        del dqkv
+        dh = torch.empty(NT, D, device=dev)
+        if cos_t is not None:
+            # dh = rotary^T([dQ dK] [Wq; Wk]) + dV Wv
+            dhr = torch.empty(NT, D, device=dev)
+            gemm(NT, D, 2 * D, op(dqkv16, 0, 3 * D, True), op(weight16t(wq, wk), 0, 2 * D, True), dhr, D)
+            _lib.call("b2p_rotary", _p(dhr), _p(cos_t), _p(sin_t), _p(dh), B, T, nh, hd, D, 1, _st())
+            gemm(NT, D, D, op(dqkv16, 2 * D, 3 * D, True), op(weight16t(wv), 0, D, True), dh, D, beta=1.0)
+        else:
+            gemm(NT, D, 3 * D, op(dqkv16, 0, 3 * D, True), op(weight16t(wq, wk, wv), 0, 3 * D, True), dh, D)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
         return (dx.view(B, T, D), dg, db, *grads, dwo, dbo, None, None, None)
 
@@ -1777,12 +1869,19 @@ class _ConvModule(torch.autograd.Function):
         ng = ctx.needs_input_grad
         dy = dy.contiguous().view(NT, D)
         do = _dropout_scaled(dy, p, seed, 1.0)
-        dpw2 = None
-        if ng[7]:
-            dpw2 = torch.empty_like(w_pw2)
-            mm_tn(do, s, dpw2.view(D, D))
+        b16 = bf16_mode()   # bf16 operands: each cast once, frozen weight gradients deferred
         ds = torch.empty(NT, D, device=dev)
-        mm_nn(do, w_pw2.view(D, D), ds)
+        if b16:
+            do16 = cast16(do)
+            dpw2 = _wgrad16(w_pw2, ng[7], do16, D, cast16(s), D, NT)
+            gemm(NT, D, D, op(do16, 0, D, True), op(weight16t(w_pw2), 0, D, True), ds, D)
+            del do16
+        else:
+            dpw2 = None
+            if ng[7]:
+                dpw2 = torch.empty_like(w_pw2)
+                mm_tn(do, s, dpw2.view(D, D))
+            mm_nn(do, w_pw2.view(D, D), ds)
         dc = torch.empty(NT, D, device=dev)
         dbn_g = torch.empty(D, device=dev)
         dbn_b = torch.empty(D, device=dev)
@@ -1795,12 +1894,17 @@ class _ConvModule(torch.autograd.Function):
         _lib.call("b2p_dwconv_bwd", _p(u), _p(w_dw), _p(dc), _p(du), _p(ddw), B, T, D, K, _p(wsd), _st())
         da = torch.empty(NT, 2 * D, device=dev)
         _lib.call("b2p_glu_bwd", _p(a), _p(du), _p(da), NT, D, _st())
-        dpw1 = None
-        if ng[3]:
-            dpw1 = torch.empty_like(w_pw1)
-            mm_tn(da, h, dpw1.view(2 * D, D))
         dh = torch.empty(NT, D, device=dev)
-        mm_nn(da, w_pw1.view(2 * D, D), dh)
+        if b16:
+            da16 = cast16(da)
+            dpw1 = _wgrad16(w_pw1, ng[3], da16, 2 * D, cast16(h), D, NT)
+            gemm(NT, D, 2 * D, op(da16, 0, 2 * D, True), op(weight16t(w_pw1), 0, 2 * D, True), dh, D)
+        else:
+            dpw1 = None
+            if ng[3]:
+                dpw1 = torch.empty_like(w_pw1)
+                mm_tn(da, h, dpw1.view(2 * D, D))
+            mm_nn(da, w_pw1.view(2 * D, D), dh)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
         return dx.view(B, T, D), dg, db, dpw1, ddw, dbn_g, dbn_b, dpw2, None, None, None
 
