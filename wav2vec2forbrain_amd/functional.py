@@ -1717,9 +1717,19 @@ class _ConformerAttnBlock(torch.autograd.Function):
         qkv = torch.empty(NT, 3 * D, device=dev)
         for i, (w, bb, src) in enumerate(((wq, bq, hr), (wk, bk, hr), (wv, bv, h))):
             gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=bb)
-        P, Pd, O = _attn_core_fwd(qkv, B, T, nh, hd, p_attn, seeds[0])
+        # bf16 mode, head 64, T' <= 256: fused attention (csrc/attn16.hip, scores stay on-chip); the
+        # saved slots then hold qkv16 / lse2 / dropout keep bits / O16
+        ctx.fused = bf16_mode() and attn16_ok(T, hd)
         y = torch.empty(NT, D, device=dev)
-        gemm(NT, D, D, op(O, 0, D, True), op(wo, 0, D, True), y, D, bias=bo, drop_p=p_out, seed=seeds[1], residual=x2)
+        if ctx.fused:
+            qkv = cast16(qkv)
+            O, P, Pd = _attn16_fwd(qkv, B, T, nh, hd, p_attn, seeds[0], want_mask=True)
+            gemm(NT, D, D, op(O, 0, D, True), op(weight16(wo), 0, D, True), y, D, bias=bo, drop_p=p_out,
+                 seed=seeds[1], residual=x2)
+        else:
+            P, Pd, O = _attn_core_fwd(qkv, B, T, nh, hd, p_attn, seeds[0])
+            gemm(NT, D, D, op(O, 0, D, True), op(wo, 0, D, True), y, D, bias=bo, drop_p=p_out, seed=seeds[1],
+                 residual=x2)
         ctx.save_for_backward(x2, h, hr if cos_t is not None else None, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo,
                               cos_t, sin_t)
         ctx.cfg = cfg
@@ -1738,7 +1748,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
         hr_ = h if hr is None else hr
         dy = dy.contiguous().view(NT, D)
         dz = _dropout_scaled(dy, p_out, seeds[1], 1.0)
-        if bf16_mode():
+        if bf16_mode() or ctx.fused:
             return _ConformerAttnBlock._backward16(ctx, dy, dz, x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv,
                                                    wo, cos_t, sin_t)
         dwo = dbo = None
@@ -1790,12 +1800,19 @@ class _ConformerAttnBlock(torch.autograd.Function):
         if ctx.has_b[3] and ng[10]:
             dbo = torch.empty(D, device=dev)
             colsum(dz, NT, D, dbo)
-        dwo = _wgrad16(wo, ng[9], dz16, D, cast16(O), D, NT)
-        dO = torch.empty(NT, D, device=dev)
-        gemm(NT, D, D, op(dz16, 0, D, True), op(weight16t(wo), 0, D, True), dO, D)
-        dqkv = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, hd, p_attn, seeds[0])
-        del dO
-        dqkv16 = cast16(dqkv)
+        dwo = _wgrad16(wo, ng[9], dz16, D, O if ctx.fused else cast16(O), D, NT)
+        if ctx.fused:
+            # qkv / P / Pd / O hold qkv16, lse2, the dropout keep bits and O16 (forward)
+            dO16 = torch.empty(NT, D, device=dev, dtype=BF16)
+            gemm(NT, D, D, op(dz16, 0, D, True), op(weight16t(wo), 0, D, True), None, D, C16=dO16)
+            dqkv, dqkv16 = _attn16_bwd(qkv, dO16, P, B, T, nh, hd, p_attn, seeds[0], mask=Pd)
+            del dO16
+        else:
+            dO = torch.empty(NT, D, device=dev)
+            gemm(NT, D, D, op(dz16, 0, D, True), op(weight16t(wo), 0, D, True), dO, D)
+            dqkv = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, hd, p_attn, seeds[0])
+            del dO
+            dqkv16 = cast16(dqkv)
         h16 = cast16(h)
         hr16 = h16 if hr is None else cast16(hr)
         grads = []
