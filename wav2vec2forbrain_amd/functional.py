@@ -1714,15 +1714,18 @@ class _ConformerAttnBlock(torch.autograd.Function):
             _lib.call("b2p_rotary", _p(h), _p(cos_t), _p(sin_t), _p(hr), B, T, nh, hd, D, 0, _st())
         else:
             hr = h
-        qkv = torch.empty(NT, 3 * D, device=dev)
-        for i, (w, bb, src) in enumerate(((wq, bq, hr), (wk, bk, hr), (wv, bv, h))):
-            gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=bb)
         # bf16 mode, head 64, T' <= 256: fused attention (csrc/attn16.hip, scores stay on-chip); the
-        # saved slots then hold qkv16 / lse2 / dropout keep bits / O16
+        # QKV GEMMs then write only the bf16 operand, and the saved slots hold qkv16 / lse2 / dropout
+        # keep bits / O16
         ctx.fused = bf16_mode() and attn16_ok(T, hd)
+        qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16 if ctx.fused else torch.float32)
+        for i, (w, bb, src) in enumerate(((wq, bq, hr), (wk, bk, hr), (wv, bv, h))):
+            if ctx.fused:
+                gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), None, 3 * D, c_off=i * D, bias=bb, C16=qkv)
+            else:
+                gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=bb)
         y = torch.empty(NT, D, device=dev)
         if ctx.fused:
-            qkv = cast16(qkv)
             O, P, Pd = _attn16_fwd(qkv, B, T, nh, hd, p_attn, seeds[0], want_mask=True)
             gemm(NT, D, D, op(O, 0, D, True), op(weight16(wo), 0, D, True), y, D, bias=bo, drop_p=p_out,
                  seed=seeds[1], residual=x2)
