@@ -39,13 +39,15 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, 
   if (e.beta != 0.0f) v += e.beta * e.C[coff];
   if (e.bias) v += e.bias[(e.bias_gather ? e.bias_gather[z1] : (int64_t)z1) * e.biasbs1 + n];
   if (e.pre_out) e.pre_out[coff] = v;
+  if (e.pre16) e.pre16[coff] = b2p_bf16_bits(v);
   v = apply_act(v, e.act);
   if (e.drop_p > 0.0f) {
     const uint64_t idx = ((uint64_t)z * (uint64_t)a.M + (uint64_t)m) * (uint64_t)a.N + (uint64_t)n;
     v = b2p_keep(b2p_seed_eff(e.drop_seed, a.epoch), idx, a.drop_thr) ? v * a.drop_scale : 0.0f;
   }
   if (e.act_bwd != B2P_ACT_NONE) {
-    const float x = e.aux[(int64_t)z1 * e.abs1 + (int64_t)z2 * e.abs2 + (int64_t)m * e.ldaux + n];
+    const int64_t ao = (int64_t)z1 * e.abs1 + (int64_t)z2 * e.abs2 + (int64_t)m * e.ldaux + n;
+    const float x = e.aux16 ? b2p_bf16_to_f32(e.aux16[ao]) : e.aux[ao];
     v *= act_grad(x, e.act_bwd);
   }
   if (e.residual) v += e.residual[(int64_t)z1 * e.rbs1 + (int64_t)z2 * e.rbs2 + (int64_t)m * e.ldr + n];
