@@ -108,8 +108,8 @@ def cpu_baseline(bs_sample=8, L=1024, bs_metric=32, kind="base"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--bs", type=int, default=32)
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
