@@ -60,13 +60,49 @@ def batch_on(cfg, device):
     return b.cuda() if device != "cpu" else b
 
 
-def cpu_baseline(bs_sample=8, L=1024, bs_metric=32, kind="base"):
-    """The CPU oracle (torch-CPU fp32 restatement, oracle/b2p2t_oracle.py) timed on the host on a
-    bounded sample of the same workload: one warm-up + 2 timed fwd+bwd+Adam steps at bs=bs_sample,
-    scaled linearly to bs_metric."""
+def host_cpu_info():
+    """(threads to use, physical cores on the host, CPU model). Threads = the host's physical cores,
+    capped by what this process may actually run on (affinity mask, cgroup CPU quota, and
+    OMP_NUM_THREADS, which the GPU box sets to its 16-CPU share)."""
+    phys, model = set(), "unknown"
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name":
+                model = v
+            elif k in ("physical id", "core id"):
+                cur[k] = v
+            elif not k and cur:
+                phys.add((cur.get("physical id"), cur.get("core id")))
+                cur = {}
+        if cur:
+            phys.add((cur.get("physical id"), cur.get("core id")))
+    except OSError:
+        pass
+    n_phys = len(phys) or (os.cpu_count() or 1)
+    caps = [n_phys, len(os.sched_getaffinity(0))]
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            caps.append(max(1, int(int(q) / int(per))))
+    except (OSError, ValueError):
+        pass
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        caps.append(int(os.environ["OMP_NUM_THREADS"]))
+    return min(caps), n_phys, model
+
+
+def cpu_baseline(bs=32, L=1024, kind="base", steps=5):
+    """The CPU oracle (torch-CPU fp32 restatement, oracle/b2p2t_oracle.py) timed on the host cores:
+    SURVEY 8(d5) — same workload (train mode, the same dropouts, fwd + bwd + Adam over the brain
+    encoder) at the bench's batch size, 1 warm-up step, median of `steps` timed steps."""
     from oracle.b2p2t_oracle import loss_and_grads, conformer_loss_and_grads, adam_step
     from tests.helpers import oracle_cfg
-    cfg = make_config(bs_sample, L, kind)
+    threads, n_phys, model_name = host_cpu_info()
+    torch.set_num_threads(threads)
+    cfg = make_config(bs, L, kind)
     ocfg = oracle_cfg(cfg)
     ocfg.hidden_dropout = ocfg.activation_dropout = ocfg.attention_dropout = ocfg.final_dropout = 0.1
     ocfg.layerdrop = 0.1
@@ -93,16 +129,64 @@ def cpu_baseline(bs_sample=8, L=1024, bs_metric=32, kind="base"):
         return float(loss)
 
     step(0)
-    t0 = time.perf_counter()
-    n = 2
-    for i in range(n):
+    times = []
+    for i in range(steps):
+        t0 = time.perf_counter()
         step(i + 1)
-    dt = (time.perf_counter() - t0) / n
-    per_metric_step = dt * bs_metric / bs_sample
-    return {"value": round(1.0 / per_metric_step, 5), "unit": "steps/s", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"oracle fwd+bwd+Adam, bs={bs_sample} L={L} train mode, mean of {n} steps after 1 warm-up "
-                      f"({dt:.2f} s/step), scaled x{bs_metric // bs_sample} to bs={bs_metric}"}
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    return {"value": round(1.0 / med, 5), "unit": "steps/s", "cores": threads, "kind": "port",
+            "host_physical_cores": n_phys, "cpu_model": model_name,
+            "sample": f"oracle fwd+bwd+Adam (fp32, torch-CPU, {threads} threads), bs={bs} L={L} train mode, "
+                      f"median of {steps} steps after 1 warm-up: {med:.2f} s/step "
+                      f"(all: {', '.join(f'{t:.2f}' for t in times)})"}
+
+
+def parity_check(cfg, device, kind="base", steps=2):
+    """north_star parity: per-step CTC loss of the HIP bf16 step vs the fp32 CPU oracle on identical
+    weights and inputs, deterministic mode (dropout 0, LayerDrop 0; the reference's Philox masks
+    cannot be reproduced), `steps` consecutive steps with Adam (lr 1e-3) over the brain encoder, so
+    step 2 also checks the optimizer update. Tolerance 1e-3 rel (BASELINE.json north_star)."""
+    from oracle.b2p2t_oracle import loss_and_grads, conformer_loss_and_grads, adam_step
+    from tests.helpers import oracle_cfg
+    from wav2vec2forbrain_amd.optim import HipAdam
+    model = build(cfg, device, train_dropouts=False)
+    model.train()
+    sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
+    batch = batch_on(cfg, device)
+    hip = []
+    for _ in range(steps):
+        opt.zero_grad()
+        out = model(batch)
+        out.loss.backward()
+        opt.step()
+        hip.append(float(out.metrics["ctc_loss"]))
+    torch.cuda.synchronize()
+    del model, opt
+    threads, _, _ = host_cpu_info()
+    torch.set_num_threads(threads)
+    ocfg = oracle_cfg(cfg)
+    from tests.golden.configs import make_batch
+    x, day, il, tgt, tl = make_batch(cfg)
+    b = dict(x=x, day_idxs=day, input_lens=il, target=tgt, target_lens=tl)
+    brain = [k for k in sd if k.startswith("brain_encoder.") and sd[k].is_floating_point() and "gaussian" not in k]
+    state = {k: (torch.zeros_like(sd[k]), torch.zeros_like(sd[k])) for k in brain}
+    ref = []
+    for i in range(steps):
+        if kind == "conformer":
+            loss, grads, _bn = conformer_loss_and_grads(sd, b, ocfg, training=True)
+        else:
+            loss, grads = loss_and_grads(sd, b, ocfg, training=True)
+        ref.append(float(loss))
+        for k in brain:
+            m, v = state[k]
+            sd[k], m, v = adam_step(sd[k], grads[k], m, v, i + 1, 1e-3)
+            state[k] = (m, v)
+    rel = [abs(h - r) / abs(r) for h, r in zip(hip, ref)]
+    return {"mode": "deterministic (dropout 0, LayerDrop 0), bf16 HIP step vs fp32 CPU oracle, same weights/inputs",
+            "steps": steps, "hip_ctc_loss": [round(v, 6) for v in hip], "oracle_ctc_loss": [round(v, 6) for v in ref],
+            "max_rel_err": float(f"{max(rel):.3e}"), "tolerance": 1e-3, "pass": max(rel) <= 1e-3}
 
 
 def main():
@@ -113,6 +197,7 @@ def main():
     ap.add_argument("--bs", type=int, default=32)
     ap.add_argument("--seq", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--evaluator", action="store_true",
                     help="include the train evaluator's greedy CTC decode + WER (on the device) in every step")
     ap.add_argument("--graph", type=int, default=None,
@@ -120,6 +205,9 @@ def main():
     ap.add_argument("--config", choices=["base", "conformer"], default="base",
                     help="base = BASELINE configs[1] (headline); conformer = configs[2]")
     args = ap.parse_args()
+    # the committed tree carries sources only: build the library before the first HIP call
+    from wav2vec2forbrain_amd import build_lib
+    build_lib.ensure_built()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -291,10 +379,24 @@ def main():
     }
     if args.config != "base":
         res["metric"] = "train steps/sec + CTC loss, b2p2t_gru+w2v_conformer bs=32 seq=1024"
+    def log(msg):
+        print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+    log(f"timed {args.steps} steps: {dt / args.steps * 1e3:.3f} ms/step")
+    if world == 1 and not args.no_parity:
+        log("parity: deterministic HIP steps vs CPU oracle")
+        res["parity"] = parity_check(cfg, device, args.config, steps=2 if args.config == "base" else 1)
     if world == 1 and not args.no_cpu_baseline:
-        # the Conformer-large sample is 4 samples (one step is ~7x the base model's FLOPs)
-        res["cpu_baseline"] = cpu_baseline(bs_sample=8 if args.config == "base" else 4, L=args.seq,
-                                           bs_metric=args.bs, kind=args.config)
+        log("cpu_baseline: oracle steps on the host cores")
+        if args.config == "base":
+            res["cpu_baseline"] = cpu_baseline(bs=args.bs, L=args.seq, kind="base", steps=5)
+        else:
+            # Conformer-large: one fp32 CPU step at bs=32 is ~100 s, so the bounded sample is bs=4
+            # (5 timed steps), scaled to the bench batch (the CPU step is linear in batch size)
+            cb = cpu_baseline(bs=4, L=args.seq, kind="conformer", steps=5)
+            cb["value"] = round(cb["value"] * 4 / args.bs, 6)
+            cb["sample"] += f"; scaled x{args.bs / 4:g} to bs={args.bs}"
+            res["cpu_baseline"] = cb
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()

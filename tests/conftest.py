@@ -9,6 +9,10 @@ if ROOT not in sys.path:
 
 
 def pytest_configure(config):
+    # a fresh checkout carries sources only: build the HIP library (hipcc child processes, no GPU
+    # touched) before anything calls torch.cuda; _lib.load() itself never builds
+    from wav2vec2forbrain_amd import build_lib
+    build_lib.ensure_built()
     config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP device); run with -m gpu")
     config.addinivalue_line("markers", "slow: long-running CPU oracle case")
 

@@ -35,7 +35,7 @@ def _compile(src: str, hmt: float, verbose: bool) -> str:
         return obj
     cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
     if verbose:
-        print(" ".join(cmd), flush=True)
+        print(f"build_lib: hipcc {os.path.basename(src)}", flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -43,10 +43,32 @@ def _compile(src: str, hmt: float, verbose: bool) -> str:
 
 
 def build(verbose: bool = False, jobs: int | None = None) -> str:
+    """Compiles what is stale and links the library. Serialised across processes by a file lock
+    (N bench ranks or a pytest run may call it at once on the same tree)."""
+    import fcntl
+    import time
     os.makedirs(BUILD, exist_ok=True)
+    with open(os.path.join(BUILD, ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        t0 = time.perf_counter()
+        path = _build_locked(verbose, jobs)
+        if verbose:
+            print(f"build_lib: {path} ready in {time.perf_counter() - t0:.1f} s", flush=True)
+        return path
+
+
+def ensure_built() -> str:
+    """The hook every GPU entry point (tests/conftest.py, bench.py, __graft_entry__.smoke) runs before
+    its first HIP call: the committed tree carries sources only (the .so is git-ignored), so a fresh
+    checkout builds here. Compilation runs in hipcc child processes; nothing here touches the GPU."""
+    return build(verbose=True)
+
+
+def _build_locked(verbose: bool, jobs: int | None) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     hmt = _headers_mtime()
-    jobs = jobs or min(8, os.cpu_count() or 4)
+    # the GPU box reports the whole machine's CPUs; its share is 16
+    jobs = jobs or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, hmt, verbose), srcs))
     newest = max(os.path.getmtime(o) for o in objs)
