@@ -409,7 +409,7 @@ def gemm_traffic(kind="base"):
     config has no measurement."""
     import glob
     fs = glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic*.json"))
-    fs = sorted((f for f in fs if f.endswith("_conformer.json") == (kind == "conformer")), key=os.path.getmtime)
+    fs = sorted((f for f in fs if f.endswith("_conformer.json") == (kind == "conformer")), key=os.path.basename)
     if not fs:
         return None
     d = json.load(open(fs[-1]))

@@ -25,6 +25,16 @@ CONFIGS = [
     dict(name="conformer_large_b2", seed=45, B=2, L=288, in_lens=[288, 256], tgt_range=(10, 25), hidden_size=1024,
          layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512, gru_layers=3, bidirectional=True,
          fc_hidden=[256], learnable_h0=False, full_grad_max=4096, infeasible=False, conformer=True, dw_kernel=31),
+    # the bench workloads themselves (BASELINE configs[1] and configs[2]) at bs=32, 1024-bin windows:
+    # loss, per-parameter gradient norms and sampled gradient entries (inputs are regenerated from the
+    # seed, not stored: x alone would be 33 MB)
+    dict(name="base_bs32", seed=42, B=32, L=1024, in_lens=[1024] * 32, tgt_range=(60, 120), hidden_size=768,
+         layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2, bidirectional=True,
+         fc_hidden=[], learnable_h0=False, full_grad_max=0, infeasible=False, big=True),
+    dict(name="conformer_large_bs32", seed=42, B=32, L=1024, in_lens=[1024] * 32, tgt_range=(60, 120),
+         hidden_size=1024, layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512, gru_layers=3,
+         bidirectional=True, fc_hidden=[256], learnable_h0=False, full_grad_max=0, infeasible=False, conformer=True,
+         dw_kernel=31, big=True),
 ]
 
 
