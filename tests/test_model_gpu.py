@@ -32,9 +32,13 @@ def _run(name, mode):
     return model, out
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2"])
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2",
+                                  "base_bs32", "conformer_large_bs32"])
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
 def test_step_matches_reference_golden(name, mode):
+    """One deterministic training step (forward, CTC, backward) vs the reference's own modules run on
+    the same weights and inputs (tests/golden/make_golden.py). base_bs32 / conformer_large_bs32 are
+    the bench workloads themselves (BASELINE configs[1] / configs[2], bs=32, 1024-bin windows)."""
     fx = load_fixture(name)
     model, out = _run(name, mode)
     ref = float(fx["loss"])
