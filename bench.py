@@ -235,6 +235,10 @@ def main():
     cfg = make_config(args.bs, args.seq, args.config)
     model = build(cfg, device)
     model.train()
+    if os.environ.get("B2P_DIAG_LAYERDROP"):   # diagnostic only: override the encoder's LayerDrop
+        enc = model.w2v_encoder
+        enc = enc.wav2vec2_conformer.encoder if hasattr(enc, "wav2vec2_conformer") else enc.wav2vec2.encoder
+        enc.config.layerdrop = float(os.environ["B2P_DIAG_LAYERDROP"])
     skip = unused_param_names(model)
     brain_params = [p for n, p in model.named_parameters() if n.startswith("brain_encoder.") and n not in skip]
     opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
@@ -266,8 +270,12 @@ def main():
         wer = Fn.ctc_greedy_wer(out.logits.detach(), batch.target)[0]
         return torch.stack([out.metrics["ctc_loss"].reshape(()), wer])
 
+    def zero_grad():
+        # N>1: the trainable gradients live in the reducer's bucket buffers (bound as p.grad views)
+        reducer.zero_grad() if reducer is not None else opt.zero_grad()
+
     def step():
-        opt.zero_grad()
+        zero_grad()
         out = model(batch)
         out.loss.backward()
         Fn.join_wgrad()
@@ -292,7 +300,7 @@ def main():
             run = sg.replay
         else:
             def fwd_bwd():
-                opt.zero_grad()
+                zero_grad()
                 out = model(batch)
                 out.loss.backward()
                 Fn.join_wgrad()

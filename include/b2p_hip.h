@@ -235,6 +235,15 @@ int b2p_conv_weight_transpose_flip(const float* w, float* out, int64_t G, int64_
 int b2p_ctc_greedy_wer(const float* logits, int64_t B, int64_t T, int64_t C, const int64_t* target, int64_t S,
                        int blank, int eos, int delim, int32_t* out_tokens, int32_t* out_ntok, int32_t* errs,
                        int32_t* nwords, b2p_stream_t stream);
+/* Character errors of the same greedy decode (reference EvaluatorWithW2vLMDecoder
+ * .calculate_char_error_rate, src/train/evaluator.py:212-214,231-242): prediction and target
+ * rendered to characters as Wav2Vec2CTCTokenizer.batch_decode does (token id -> tok_chars[id*8 ..
+ * +tok_len[id]), delim -> ' ', stripped, prediction cut after the first eos), per-sample
+ * Levenshtein distance char_errs[b] and target length nchars[b] (CER = sum errs / sum nchars).
+ * char_errs[b] = -1 if a rendered string exceeds 2048 characters. */
+int b2p_ctc_greedy_cer(const float* logits, int64_t B, int64_t T, int64_t C, const int64_t* target, int64_t S,
+                       int blank, int eos, int delim, const uint8_t* tok_chars, const int32_t* tok_len,
+                       int32_t* char_errs, int32_t* nchars, b2p_stream_t stream);
 
 /* Grouped positional conv of wav2vec2 on bf16 MFMA (csrc/posconv16.hip; 48 channels per group,
  * 128 taps, padding 64 + SamePad, T <= 256), replacing the implicit-conv GEMMs of
@@ -397,6 +406,45 @@ int b2p_batchnorm_eval(const float* x, const float* gamma, const float* beta,
 int b2p_batchnorm_bwd(const float* dy, const float* pre, const float* x, const float* mean,
                       const float* rstd, const float* gamma, float* dx, float* dgamma, float* dbeta,
                       int64_t M, int64_t C, int act, float* workspace, b2p_stream_t stream);
+
+/* BatchNorm in stages, for synchronised statistics across data-parallel ranks (SyncBN; SURVEY
+ * 8(e3)(iii)): the caller all-reduces the per-channel sums between the stages.
+ *   stats    : out[c] = sum_m x[m][c] (center NULL) or sum_m (x[m][c] - center[c])^2
+ *   finalize : mean = sum / count (phase 0, in place on sum -> mean); phase 1: rstd from the summed
+ *              squared deviations and the running-stat update (count = global row count)
+ *   apply    : y = act(pre), pre = (x - mean) * rstd * gamma + beta
+ *   bwd_sums : g = dy * act'(pre) (into g, M*C), sum_g[c], sum_gx[c] = sum g * xhat
+ *   bwd_dx   : dx = gamma * rstd * (g - sum_g / count - xhat * sum_gx / count)
+ * workspace: b2p_batchnorm_workspace(M, C) floats. */
+int b2p_batchnorm_stats(const float* x, const float* center, float* out, int64_t M, int64_t C,
+                        float* workspace, b2p_stream_t stream);
+int b2p_batchnorm_finalize(float* sum_or_mean, const float* sqdev, float* rstd, float* running_mean,
+                           float* running_var, int64_t C, int64_t count, float eps, float momentum,
+                           int phase, b2p_stream_t stream);
+int b2p_batchnorm_apply(const float* x, const float* mean, const float* rstd, const float* gamma,
+                        const float* beta, float* y, float* pre, int64_t M, int64_t C, int act,
+                        b2p_stream_t stream);
+int b2p_batchnorm_bwd_sums(const float* dy, const float* pre, const float* x, const float* mean,
+                           const float* rstd, float* g, float* sum_g, float* sum_gx, int64_t M,
+                           int64_t C, int act, float* workspace, b2p_stream_t stream);
+int b2p_batchnorm_bwd_dx(const float* g, const float* x, const float* mean, const float* rstd,
+                         const float* gamma, const float* sum_g, const float* sum_gx, float* dx,
+                         int64_t M, int64_t C, int64_t count, b2p_stream_t stream);
+
+/* ------------------------------------------------------------------ LayerDrop in a captured step
+ * (csrc/layerdrop.hip). The reference skips an encoder layer when torch.rand([]) < layerdrop (TF
+ * w2v Wav2Vec2Encoder.forward, TF conf Wav2Vec2ConformerEncoder.forward), a host decision a
+ * captured graph cannot redraw. In a graph every layer runs and the decision is drawn on the device,
+ * keep = hash(seed + step counter) >= p, so each replay redraws it:
+ *   select: out = keep ? keep_val : skip_val (and out16 from keep16/skip16 or a cast, if out16)
+ *   route : d_keep = keep ? dout : 0, d_skip = keep ? 0 : dout
+ *   keep  : the same draw on the host (epoch = the step counter's value, has_epoch 0 = eager). */
+int b2p_layerdrop_keep(float p, uint64_t seed, uint64_t epoch, int has_epoch, int32_t* keep);
+int b2p_layerdrop_select(const float* skip_val, const float* keep_val, float* out,
+                         const uint16_t* skip16, const uint16_t* keep16, uint16_t* out16, int64_t n,
+                         float p, uint64_t seed, b2p_stream_t stream);
+int b2p_layerdrop_route(const float* dout, float* d_keep, float* d_skip, int64_t n, float p,
+                        uint64_t seed, b2p_stream_t stream);
 
 #ifdef __cplusplus
 }

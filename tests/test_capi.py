@@ -57,3 +57,18 @@ def test_argument_validation_without_device():
     with pytest.raises(RuntimeError):
         _lib.call("b2p_dropout", None, None, 10, 0.5, 1, None)
     assert lib.b2p_ctc_workspace(2, 10, 3, 32) == 2 * (10 * 32 + 2 * 10 * 7)
+
+
+def test_layerdrop_draw_host_side():
+    """LayerDrop device draw (csrc/layerdrop.hip) evaluated on the host: keep rate 1 - p over seeds,
+    p = 0 always keeps, and the step counter changes the draw of a fixed seed."""
+    from wav2vec2forbrain_amd import functional as Fn
+    seeds = range(1, 4001)
+    for p in (0.1, 0.5):
+        rate = sum(Fn.layerdrop_keep(p, s * 0x9E3779B1) for s in seeds) / len(seeds)
+        assert abs(rate - (1 - p)) < 0.03, (p, rate)
+    assert all(Fn.layerdrop_keep(0.0, s) for s in range(100))
+    draws = {Fn.layerdrop_keep(0.5, 12345, e) for e in range(64)}
+    assert draws == {True, False}
+    with pytest.raises(RuntimeError):
+        Fn.layerdrop_keep(1.0, 1)

@@ -1,7 +1,9 @@
 """World-size-2 data-parallel gradient exchange on CPU (gloo): train/ddp.GradBucketReducer averages
 every trainable gradient over the ranks, in both its modes — buckets all-reduced from the backward
 hooks (eager step) and all buckets exchanged after backward (the graph-replayed step) — with
-parameters that got no gradient on a rank contributing zeros."""
+parameters that got no gradient on a rank contributing zeros, the collectives issued in the same
+(index) order on every rank although one rank's backward never reaches a parameter, and gradients
+accumulated either into bucket views (zero_grad) or into fresh tensors (copied in)."""
 import os
 import socket
 
@@ -22,14 +24,20 @@ def _free_port():
 def _model():
     torch.manual_seed(0)
     m = torch.nn.Sequential(torch.nn.Linear(16, 32), torch.nn.GELU(), torch.nn.Linear(32, 8))
-    m.extra = torch.nn.Linear(8, 8)      # used on rank 0 only
-    return m
+    extra = torch.nn.Linear(8, 8)      # a separate module, used on rank 0 only (registered last, so
+    return m, extra                    # its parameters land in bucket 0, the first one launched)
 
 
-def _loss(m, rank, x):
+def _params(mm):
+    m, extra = mm
+    return list(m.parameters()) + list(extra.parameters())
+
+
+def _loss(mm, rank, x):
+    m, extra = mm
     y = m(x)
     if rank == 0:
-        y = m.extra(y)
+        y = extra(y)
     return (y ** 2).mean()
 
 
@@ -45,22 +53,29 @@ def _worker(rank, world, port, overlap, q):
     try:
         from wav2vec2forbrain_amd.train.ddp import GradBucketReducer
         m = _model()
-        params = list(m.parameters())
+        params = _params(m)
         red = GradBucketReducer(params, bucket_mb=0.001, overlap=overlap)   # several small buckets
-        for _ in range(2):                                                   # reusable across steps
-            for p in params:
-                p.grad = None
+        for it in range(3):                                                  # reusable across steps
+            if it == 0:
+                for p in params:          # fresh gradient tensors: copied into the buckets
+                    p.grad = None
+            else:
+                red.zero_grad()           # gradients accumulate straight into the bucket views
+            red.launch_log.clear()
             _loss(m, rank, _data(rank)).backward()
             red.finish()
+            if it > 0:
+                assert all(p.grad.data_ptr() == red.views[p].data_ptr() for p in params)
+        order = list(red.launch_log)
         # expected: mean over ranks of each rank's own gradient (zeros where a rank had none)
         exp = []
         for r in range(world):
             mr = _model()
             _loss(mr, r, _data(r)).backward()
-            exp.append([p.grad if p.grad is not None else torch.zeros_like(p) for p in mr.parameters()])
+            exp.append([p.grad if p.grad is not None else torch.zeros_like(p) for p in _params(mr)])
         ok = all(torch.allclose(p.grad, sum(e[i] for e in exp) / world, rtol=1e-5, atol=1e-7)
                  for i, p in enumerate(params))
-        q.put((rank, ok, len(red.buckets)))
+        q.put((rank, ok, len(red.buckets), order))
     finally:
         dist.destroy_process_group()
 
@@ -76,5 +91,7 @@ def test_grad_bucket_reducer_world2_gloo(overlap):
     res = [q.get(timeout=120) for _ in procs]
     for p in procs:
         p.join(timeout=60)
-    assert all(ok for _, ok, _ in res), res
-    assert all(nb > 1 for _, _, nb in res)
+    assert all(ok for _, ok, _, _ in res), res
+    assert all(nb > 1 for _, _, nb, _ in res)
+    # identical collective order on both ranks: bucket index order
+    assert all(order == list(range(nb)) for _, _, nb, order in res), res

@@ -73,3 +73,43 @@ def test_ctc_greedy_wer_matches_host_evaluator(tmp_path):
         perfect[0, 2 * t + 1, 0] = 5.0
     w1, e1, n1, _, _ = Fn.ctc_greedy_wer(perfect.cuda(), target[3:4].cuda())
     assert int(e1[0]) == 0 and int(n1[0]) == nw_ref[3] and float(w1) == 0.0
+
+
+def test_ctc_greedy_cer_matches_host_evaluator(tmp_path):
+    """Device character error rate (csrc/decode.hip ctc_greedy_cer) vs the reference evaluator's
+    calculate_char_error_rate (src/train/evaluator.py:231-242: character Levenshtein of the
+    tokenizer-decoded strings, cut after "</s>", summed over the batch / summed target lengths),
+    including special tokens rendered as several characters, leading/trailing delimiters and
+    repeated delimiters."""
+    from transformers import Wav2Vec2CTCTokenizer
+    from wav2vec2forbrain_amd import functional as Fn
+    f = tmp_path / "vocab.json"
+    f.write_text(json.dumps({t: i for i, t in enumerate(VOCAB)}))
+    tok = Wav2Vec2CTCTokenizer(str(f))
+    g = torch.Generator().manual_seed(5)
+    B, T, C, S = 16, 249, 32, 100
+    ids = torch.randint(4, C, (B, T), generator=g)
+    ids[torch.rand(B, T, generator=g) < 0.35] = 0
+    ids[torch.rand(B, T, generator=g) < 0.12] = 4
+    ids[torch.rand(B, T, generator=g) < 0.02] = 3           # <unk>: 5 characters
+    run = torch.rand(B, T, generator=g) < 0.5
+    for t in range(1, T):
+        ids[:, t] = torch.where(run[:, t], ids[:, t - 1], ids[:, t])
+    ids[0, 120] = 2                                          # EOS: cut after it
+    ids[1, 30:33] = 1                                        # <s>
+    ids[2, :6] = torch.tensor([4, 0, 4, 4, 7, 0])            # leading delimiters
+    ids[3, -5:] = torch.tensor([9, 4, 0, 4, 4])              # trailing delimiters
+    logits = torch.randn(B, T, C, generator=g)
+    logits.scatter_(2, ids.unsqueeze(-1), 8.0)
+    target = torch.randint(5, C, (B, S), generator=g)
+    target[torch.rand(B, S, generator=g) < 0.18] = 4
+    lens = torch.randint(20, S + 1, (B,), generator=g)
+    target[torch.arange(S).unsqueeze(0) >= lens.unsqueeze(1)] = 0
+    pred_s, _, _ = _host_reference(logits, target, tok)
+    lab = tok.batch_decode(target.numpy(), group_tokens=False)
+    errs_ref = [_edit(list(t), list(p)) for p, t in zip(pred_s, lab)]
+    n_ref = [len(t) for t in lab]
+    cer, errs, nch = Fn.ctc_greedy_cer(logits.cuda(), target.cuda(), VOCAB)
+    assert errs.cpu().tolist() == errs_ref
+    assert nch.cpu().tolist() == n_ref
+    assert abs(float(cer) - sum(errs_ref) / sum(n_ref)) < 1e-6

@@ -1,0 +1,120 @@
+"""LayerDrop inside a captured training step (csrc/layerdrop.hip, functional.layerdrop_layer).
+
+The reference redraws LayerDrop every step on the host (TF w2v Wav2Vec2Encoder.forward /
+TF conf Wav2Vec2ConformerEncoder.forward: skip a layer when torch.rand([]) < layerdrop). A captured
+step cannot redraw a host decision, so in a graph the draw is made on the device from the step
+counter. These tests replay one captured step several times and check every replay against an eager
+step that skips exactly the layers the device draw skipped in that replay: same loss, same
+gradients, same Conformer BatchNorm running statistics (restored for skipped layers)."""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import CFG, build_model, batch_dict
+
+pytestmark = pytest.mark.gpu
+
+P_LD = 0.5
+REPLAYS = 8
+
+
+def _batch(cfg):
+    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    b = batch_dict(cfg)
+    return make_b2t_batch(b["x"], b["target"], b["day_idxs"], b["input_lens"], b["target_lens"]).cuda()
+
+
+def _encoder(model):
+    w = model.w2v_encoder
+    return w.wav2vec2_conformer.encoder if hasattr(w, "wav2vec2_conformer") else w.wav2vec2.encoder
+
+
+def _model(name):
+    model = build_model(CFG[name])
+    model.train()
+    model.sync_metrics = False
+    _encoder(model).config.layerdrop = P_LD
+    return model
+
+
+class _ForcedRand:
+    """torch.rand([]) replacement for the eager reference: yields 0 (skip) / 0.99 (keep) per layer."""
+
+    def __init__(self, pattern):
+        self.vals = [0.99 if k else 0.0 for k in pattern]
+        self.orig = torch.rand
+
+    def __call__(self, *a, **kw):
+        if len(a) == 1 and list(a[0]) == [] and not kw:
+            return torch.tensor(self.vals.pop(0))
+        return self.orig(*a, **kw)
+
+
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_conf"])
+def test_captured_layerdrop_redraws_per_replay(name):
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.train.step_graph import StepGraph
+    cfg = CFG[name]
+    nl = cfg["layers"]
+    Fn.SEEDS.reseed(1234)
+
+    # ---- captured step, replayed
+    model = _model(name)
+    batch = _batch(cfg)
+
+    def step():
+        for p in model.parameters():
+            p.grad = None
+        out = model(batch)
+        out.loss.backward()
+        return out.metrics["ctc_loss"]
+
+    Fn.LAYERDROP_LOG = []
+    with Fn.precision("bf16"):
+        sg = StepGraph(step, None, warmup=0, warm_replays=0)
+        sg.capture()
+        seeds = list(Fn.LAYERDROP_LOG)
+        Fn.LAYERDROP_LOG = None
+        assert len(seeds) == nl
+        losses, patterns = [], []
+        for _ in range(REPLAYS):
+            losses.append(float(sg.replay()))
+            ep = int(sg.epoch.item())
+            patterns.append(tuple(Fn.layerdrop_keep(P_LD, s, ep) for s in seeds))
+        grads_g = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+        bufs_g = {n: b.detach().clone() for n, b in model.named_buffers() if b.is_floating_point()}
+        sg.release()
+    torch.cuda.synchronize()
+    # the draw changes between replays (with p = 0.5 over REPLAYS replays)
+    assert len(set(patterns)) > 1, patterns
+
+    # ---- eager steps that skip the same layers
+    ref = _model(name)
+    for m in ref.modules():
+        if hasattr(m, "sync_metrics"):
+            m.sync_metrics = True
+    losses_e = []
+    with Fn.precision("bf16"):
+        for pat in patterns:
+            for p in ref.parameters():
+                p.grad = None
+            forced = _ForcedRand(pat)
+            torch.rand = forced
+            try:
+                out = ref(batch)
+            finally:
+                torch.rand = forced.orig
+            out.loss.backward()
+            losses_e.append(out.metrics["ctc_loss"])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(losses, losses_e, rtol=1e-5, atol=0)
+    grads_e = {n: p.grad for n, p in ref.named_parameters() if p.grad is not None}
+    for n, g in grads_g.items():
+        e = grads_e.get(n)
+        if e is None:   # a layer the last eager step skipped: the captured step wrote exact zeros
+            assert float(g.abs().max()) == 0.0, n
+            continue
+        assert float((g - e).norm()) <= 1e-5 * float(e.norm()) + 1e-7, n
+    for n, b in bufs_g.items():   # BatchNorm running statistics: updated only by kept layers
+        e = dict(ref.named_buffers())[n]
+        assert float((b - e).norm()) <= 1e-5 * float(e.norm()) + 1e-7, n

@@ -1,6 +1,8 @@
 """Pins the CPU oracle (oracle/b2p2t_oracle.py) against golden vectors produced by the reference's
 own modules (tests/golden/make_golden.py), plus the build's module tree against the reference
 state_dict (key names and shapes). CPU only."""
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -17,8 +19,13 @@ def test_state_dict_keys_match_reference(name):
     assert ours == list(fx["param_names"])
 
 
+# the Conformer-large bs=32 oracle step is ~2 min of CPU: opt-in (B2P_SLOW_ORACLE=1) so the default
+# CPU suite stays short; that fixture is always checked against the HIP step (tests/test_model_gpu.py)
+_SLOW = pytest.mark.skipif(os.environ.get("B2P_SLOW_ORACLE") != "1", reason="set B2P_SLOW_ORACLE=1")
+
+
 @pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2",
-                                  "base_bs32", "conformer_large_bs32"])
+                                  "base_bs32", pytest.param("conformer_large_bs32", marks=_SLOW)])
 def test_oracle_matches_reference_golden(name):
     cfg = CFG[name]
     fx = load_fixture(name)

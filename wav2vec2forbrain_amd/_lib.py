@@ -109,6 +109,7 @@ _SIGS = {
     "b2p_adam_recs": (c_i32, [c_p, c_i32, c_f32, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_p, c_p]),
     "b2p_set_seed_epoch": (c_i32, [c_p]),
     "b2p_ctc_greedy_wer": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "b2p_ctc_greedy_cer": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "b2p_transpose_bf16": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_posconv16_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_posconv16_bwd_data": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
@@ -126,6 +127,14 @@ _SIGS = {
                                   c_p, c_p]),
     "b2p_batchnorm_eval": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_i32, c_p, c_p]),
     "b2p_batchnorm_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p]),
+    "b2p_batchnorm_stats": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_p, c_p]),
+    "b2p_batchnorm_finalize": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_i32, c_p]),
+    "b2p_batchnorm_apply": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p]),
+    "b2p_batchnorm_bwd_sums": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p]),
+    "b2p_batchnorm_bwd_dx": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p]),
+    "b2p_layerdrop_keep": (c_i32, [c_f32, c_u64, c_u64, c_i32, ctypes.POINTER(c_i32)]),
+    "b2p_layerdrop_select": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_f32, c_u64, c_p]),
+    "b2p_layerdrop_route": (c_i32, [c_p, c_p, c_p, c_i64, c_f32, c_u64, c_p]),
 }
 
 # timing families (b2p_timing_*)

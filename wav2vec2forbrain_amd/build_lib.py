@@ -34,11 +34,17 @@ def _compile(src: str, hmt: float, verbose: bool) -> str:
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hmt):
         return obj
     cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
+    audit = os.environ.get("B2P_BUILD_AUDIT") == "1"
+    if audit:   # per-kernel resource usage (VGPRs, LDS, scratch) saved beside the object
+        cmd.append("-Rpass-analysis=kernel-resource-usage")
     if verbose:
         print(f"build_lib: hipcc {os.path.basename(src)}", flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
+    if audit:
+        with open(obj + ".audit", "w") as f:
+            f.write(r.stdout + r.stderr)
     return obj
 
 
@@ -89,16 +95,13 @@ if __name__ == "__main__":
     print(build(verbose="-v" in sys.argv))
 
 
-def audit_scratch(src: str = "gemm.hip") -> dict:
-    """Compiles one source with -Rpass-analysis=kernel-resource-usage and returns
-    {kernel: scratch_bytes_per_lane}. A nonzero value means registers spilled or a private array
-    went to scratch (e.g. accumulators indexed dynamically) — a silent 4x slowdown seen once."""
+def parse_scratch(text: str) -> dict:
+    """{kernel: scratch_bytes_per_lane} from hipcc -Rpass-analysis=kernel-resource-usage output. A
+    nonzero value means registers spilled or a private array went to scratch (e.g. accumulators
+    indexed dynamically) — a silent 4x slowdown seen once."""
     import re
-    path = os.path.join(CSRC, src)
-    r = subprocess.run([HIPCC, *FLAGS, "-c", path, "-o", os.devnull, "-Rpass-analysis=kernel-resource-usage"],
-                       capture_output=True, text=True)
     out, cur = {}, None
-    for line in (r.stdout + r.stderr).splitlines():
+    for line in text.splitlines():
         m = re.search(r"Function Name: (\S+)", line)
         if m:
             cur = m.group(1)
@@ -106,3 +109,11 @@ def audit_scratch(src: str = "gemm.hip") -> dict:
         if m and cur:
             out[cur] = int(m.group(1))
     return out
+
+
+def audit_scratch(src: str = "gemm.hip") -> dict:
+    """Compiles one source with the resource-usage remarks and returns parse_scratch of them."""
+    path = os.path.join(CSRC, src)
+    r = subprocess.run([HIPCC, *FLAGS, "-c", path, "-o", os.devnull, "-Rpass-analysis=kernel-resource-usage"],
+                       capture_output=True, text=True)
+    return parse_scratch(r.stdout + r.stderr)

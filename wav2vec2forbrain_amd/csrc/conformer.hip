@@ -394,6 +394,69 @@ extern "C" int b2p_batchnorm_bwd(const float* dy, const float* pre, const float*
   return 0;
 }
 
+// ---- staged BatchNorm (SyncBN: the caller all-reduces the per-channel sums between stages)
+extern "C" int b2p_batchnorm_stats(const float* x, const float* center, float* out, int64_t M, int64_t C,
+                                   float* workspace, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && out && workspace, "batchnorm_stats: NULL");
+  if (M <= 0 || C <= 0) return 0;
+  return colsum_impl(x, center, 1, M, C, C, 0, center ? 3 : 0, out, 0, workspace + 4 * C, (hipStream_t)stream);
+}
+
+extern "C" int b2p_batchnorm_finalize(float* sum_or_mean, const float* sqdev, float* rstd, float* running_mean,
+                                      float* running_var, int64_t C, int64_t count, float eps, float momentum,
+                                      int phase, b2p_stream_t stream) {
+  B2P_CHECK_ARG(sum_or_mean && count > 0, "batchnorm_finalize: bad arguments");
+  hipStream_t st = (hipStream_t)stream;
+  if (C <= 0) return 0;
+  if (phase == 0) {
+    hipLaunchKernelGGL(scale_k, dim3(nblk(C)), dim3(256), 0, st, sum_or_mean, C, 1.f / (float)count);
+  } else {
+    B2P_CHECK_ARG(sqdev && rstd, "batchnorm_finalize: phase 1 needs sqdev and rstd");
+    hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sqdev,
+                       (const float*)sum_or_mean, rstd, running_mean, running_var, C, count, eps, momentum);
+  }
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_batchnorm_apply(const float* x, const float* mean, const float* rstd, const float* gamma,
+                                   const float* beta, float* y, float* pre, int64_t M, int64_t C, int act,
+                                   b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && mean && rstd && gamma && beta && y, "batchnorm_apply: NULL");
+  if (M * C <= 0) return 0;
+  hipLaunchKernelGGL(bn_apply_k, dim3(nblk(M * C)), dim3(256), 0, (hipStream_t)stream, x, mean, rstd, gamma, beta, y,
+                     pre, M, C, act);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_batchnorm_bwd_sums(const float* dy, const float* pre, const float* x, const float* mean,
+                                      const float* rstd, float* g, float* sum_g, float* sum_gx, int64_t M, int64_t C,
+                                      int act, float* workspace, b2p_stream_t stream) {
+  B2P_CHECK_ARG(dy && pre && x && mean && rstd && g && sum_g && sum_gx && workspace, "batchnorm_bwd_sums: NULL");
+  hipStream_t st = (hipStream_t)stream;
+  if (M <= 0) return 0;
+  float* t = workspace;                  // M*C: g * xhat
+  float* part = workspace + M * C + 4 * C;
+  hipLaunchKernelGGL(bn_grad_pre_k, dim3(nblk(M * C)), dim3(256), 0, st, dy, pre, g, M * C, act);
+  if (colsum_impl(g, nullptr, 1, M, C, C, 0, 0, sum_g, 0, part, st)) return 1;
+  hipLaunchKernelGGL(bn_gxhat_k, dim3(nblk(M * C)), dim3(256), 0, st, g, x, mean, rstd, t, M, C);
+  if (colsum_impl(t, nullptr, 1, M, C, C, 0, 0, sum_gx, 0, part, st)) return 1;
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_batchnorm_bwd_dx(const float* g, const float* x, const float* mean, const float* rstd,
+                                    const float* gamma, const float* sum_g, const float* sum_gx, float* dx, int64_t M,
+                                    int64_t C, int64_t count, b2p_stream_t stream) {
+  B2P_CHECK_ARG(g && x && mean && rstd && gamma && sum_g && sum_gx && dx && count > 0, "batchnorm_bwd_dx: bad args");
+  if (M * C <= 0) return 0;
+  hipLaunchKernelGGL(bn_bwd_dx_k, dim3(nblk(M * C)), dim3(256), 0, (hipStream_t)stream, g, x, mean, rstd, gamma,
+                     sum_g, sum_gx, dx, M, C, count);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t seed, float scale,
                                   b2p_stream_t stream) {
   B2P_CHECK_ARG(x && y, "dropout_scaled: NULL");

@@ -592,6 +592,13 @@ def _stamp(ws):
     return tuple((id(w), w.data_ptr(), tuple(w.shape), w._version, _PARAM_EPOCH.get(id(w), 0)) for w in ws)
 
 
+def _cache_ok(ws) -> bool:
+    """Inside a graph capture only frozen parameters (set_deferred_wgrad) may come from or go to the
+    weight-copy cache: the copy of a trained weight must be a node of the graph, so that every replay
+    reads the weight the previous replay's (captured or eager) optimizer step wrote."""
+    return not capturing() or all(id(w) in _Deferred.ids for w in ws)
+
+
 def cast16(x, out=None):
     out = torch.empty(x.shape, device=x.device, dtype=BF16) if out is None else out
     _lib.call("b2p_cast_bf16", _p(x), _p(out), x.numel(), _st())
@@ -603,7 +610,8 @@ def weight16(*ws):
     until any source tensor changes (version counter or optimiser epoch)."""
     key = tuple(id(w) for w in ws)
     st = _stamp(ws)
-    hit = _W16.get(key)
+    cache = _cache_ok(ws)
+    hit = _W16.get(key) if cache else None
     if hit is not None and hit[0] == st:
         return hit[1]
     rows = sum(w.shape[0] for w in ws)
@@ -613,7 +621,8 @@ def weight16(*ws):
         _chk(w, "weight16")
         _lib.call("b2p_cast_bf16", _p(w), _p(out, off), w.numel(), _st())
         off += w.numel()
-    _W16[key] = (st, out)
+    if cache:
+        _W16[key] = (st, out)
     return out
 
 
@@ -623,7 +632,8 @@ def weight16t(*ws):
     transposed-read NN form); cached like weight16."""
     key = ("T",) + tuple(id(w) for w in ws)
     st = _stamp(ws)
-    hit = _W16.get(key)
+    cache = _cache_ok(ws)
+    hit = _W16.get(key) if cache else None
     if hit is not None and hit[0] == st:
         return hit[1]
     rows = sum(w.shape[0] for w in ws)
@@ -634,7 +644,8 @@ def weight16t(*ws):
         _chk(w, "weight16t")
         _lib.call("b2p_transpose_bf16", _p(w), _p(out), w.shape[0], C, rows, off, _st())
         off += w.shape[0]
-    _W16[key] = (st, out)
+    if cache:
+        _W16[key] = (st, out)
     return out
 
 
@@ -644,7 +655,8 @@ def bias_cat(*bs):
     real = tuple(b for b in bs if b is not None)
     key = ("bias",) + tuple(id(b) if b is not None else None for b in bs)
     st = _stamp(real)
-    hit = _W16.get(key)
+    cache = _cache_ok(real)
+    hit = _W16.get(key) if cache else None
     if hit is not None and hit[0] == st:
         return hit[1]
     out = torch.zeros(sum(ref.numel() for _ in bs), device=ref.device)
@@ -652,7 +664,8 @@ def bias_cat(*bs):
     for i, b in enumerate(bs):
         if b is not None:
             out[i * n:(i + 1) * n].copy_(b)
-    _W16[key] = (st, out)
+    if cache:
+        _W16[key] = (st, out)
     return out
 
 
@@ -1021,6 +1034,75 @@ def dropout(x, p, training):
     if not training or p <= 0.0:
         return x
     return _Dropout.apply(x, float(p), SEEDS.next())
+
+
+# ------------------------------------------------------------------ LayerDrop in a captured step
+def _b16_of(x):
+    t = getattr(x, "_b16", None)
+    return t[1] if t is not None and t[0] == x._version else None
+
+
+class _LayerDropSelect(torch.autograd.Function):
+    """out = keep ? y : x with keep drawn on the device (csrc/layerdrop.hip); the backward routes
+    dout to the layer (keep) or around it (skip)."""
+
+    @staticmethod
+    def forward(ctx, x, y, p, seed):
+        x = x.contiguous()
+        y = y.contiguous()
+        _chk(x, "layerdrop.x")
+        _chk(y, "layerdrop.y")
+        out = torch.empty_like(y)
+        out16 = torch.empty(y.shape, device=y.device, dtype=BF16) if bf16_mode() else None
+        x16, y16 = (_b16_of(x), _b16_of(y)) if out16 is not None else (None, None)
+        _lib.call("b2p_layerdrop_select", _p(x), _p(y), _p(out), _p(x16), _p(y16), _p(out16), y.numel(), float(p),
+                  seed, _st())
+        ctx.p, ctx.seed = p, seed
+        if out16 is not None:
+            attach16(out, out16)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        dout = dout.contiguous()
+        d_keep = torch.empty_like(dout)
+        d_skip = torch.empty_like(dout)
+        _lib.call("b2p_layerdrop_route", _p(dout), _p(d_keep), _p(d_skip), dout.numel(), float(ctx.p), ctx.seed, _st())
+        return d_skip, d_keep, None, None
+
+
+LAYERDROP_LOG = None   # tests: when a list, layerdrop_layer appends each layer's draw seed
+# diagnostic only (B2P_GRAPH_LAYERDROP=0): a captured step keeps the host draw made at capture time
+GRAPH_LAYERDROP = os.environ.get("B2P_GRAPH_LAYERDROP", "1") != "0"
+
+
+def capturing() -> bool:
+    """True while a step is being captured as a HIP graph: LayerDrop then draws on the device."""
+    return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
+
+
+def layerdrop_layer(layer, x, p):
+    """One encoder layer under LayerDrop inside a captured step (see csrc/layerdrop.hip): the layer
+    always runs, its output or its input is selected by the device draw of this replay, and float
+    buffers it updates in place (Conformer BatchNorm running statistics) are restored when it is
+    skipped. Eager steps keep the reference's host draw and skip the layer outright."""
+    seed = SEEDS.next()
+    if LAYERDROP_LOG is not None:
+        LAYERDROP_LOG.append(seed)
+    bufs = [b for b in layer.buffers() if b.is_floating_point() and b.numel() % 4 == 0]
+    olds = [b.clone() for b in bufs]
+    y = layer(x)
+    for b, o in zip(bufs, olds):
+        _lib.call("b2p_layerdrop_select", _p(o), _p(b), _p(b), None, None, None, b.numel(), float(p), seed, _st())
+    return _LayerDropSelect.apply(x, y, float(p), seed)
+
+
+def layerdrop_keep(p, seed, epoch=None) -> bool:
+    """Host evaluation of the device draw (tests): epoch = the step counter's value in that replay."""
+    k = ctypes.c_int32(0)
+    _lib.check(_lib.load().b2p_layerdrop_keep(float(p), seed, 0 if epoch is None else int(epoch),
+                                              0 if epoch is None else 1, ctypes.byref(k)), "b2p_layerdrop_keep")
+    return bool(k.value)
 
 
 # =====================================================================================
@@ -1546,6 +1628,46 @@ def ctc_greedy_wer(logits, targets, blank=0, eos=2, delim=4):
     return wer, errs, nw, tok, ntok
 
 
+_TOKCHARS: dict = {}
+
+
+def token_char_table(vocab, device):
+    """(tok_chars uint8 [C][8], tok_len int32 [C]) device tables of a CTC vocabulary (list of token
+    strings, index = id) for ctc_greedy_cer; cached per vocabulary."""
+    key = (tuple(vocab), str(device))
+    if key not in _TOKCHARS:
+        chars = torch.zeros(len(vocab), 8, dtype=torch.uint8)
+        lens = torch.zeros(len(vocab), dtype=torch.int32)
+        for i, t in enumerate(vocab):
+            b = t.encode("utf-8")
+            if len(b) > 8:
+                raise ValueError(f"token {t!r} longer than 8 bytes")
+            chars[i, :len(b)] = torch.tensor(list(b), dtype=torch.uint8)
+            lens[i] = len(b)
+        _TOKCHARS[key] = (chars.to(device), lens.to(device))
+    return _TOKCHARS[key]
+
+
+def ctc_greedy_cer(logits, targets, vocab, blank=0, eos=2, delim=4):
+    """Device-side character error rate of the greedy decode (csrc/decode.hip; reference
+    EvaluatorWithW2vLMDecoder.calculate_char_error_rate, src/train/evaluator.py:212-214,231-242).
+    Returns (cer 0-d tensor, char_errs (B,) int32, nchars (B,) int32)."""
+    _chk(logits, "ctc_greedy_cer.logits")
+    B, T, C = logits.shape
+    targets = targets.to(torch.int64).contiguous()
+    S = targets.shape[1]
+    dev = logits.device
+    chars, lens = token_char_table(vocab, dev)
+    if chars.shape[0] < C:
+        raise ValueError(f"vocabulary has {chars.shape[0]} tokens, logits have {C} classes")
+    errs = torch.empty(B, device=dev, dtype=torch.int32)
+    nch = torch.empty(B, device=dev, dtype=torch.int32)
+    _lib.call("b2p_ctc_greedy_cer", _p(logits), B, T, C, targets.data_ptr(), S, blank, eos, delim, chars.data_ptr(),
+              lens.data_ptr(), errs.data_ptr(), nch.data_ptr(), _st())
+    cer = errs.sum().float() / nch.sum().clamp_min(1).float()
+    return cer, errs, nch
+
+
 # =====================================================================================
 # Conformer (transformers Wav2Vec2ConformerEncoderLayer, rotary variant) — reference
 # src/model/w2v_conformer_custom_feat_extractor.py:62-112
@@ -1689,8 +1811,11 @@ def rotary_tables(T, D, base, device):
     emb = cat(t*inv_freq, t*inv_freq) -> (cos, sin) of shape (T, D). Cached per (T, D, base)."""
     key = (T, D, base, str(device))
     if key not in _ROT:
-        inv_freq = 1.0 / (base ** (torch.arange(0, D, 2, dtype=torch.int64).float() / D))
-        t = torch.arange(T).type_as(inv_freq)
+        # first use inside a graph capture (no host-to-device copy allowed): build the table on the
+        # device, as the reference's own module does (TF conf builds it on hidden_states.device)
+        on = torch.device(device) if capturing() else torch.device("cpu")
+        inv_freq = 1.0 / (base ** (torch.arange(0, D, 2, dtype=torch.int64, device=on).float() / D))
+        t = torch.arange(T, device=on).type_as(inv_freq)
         freqs = torch.einsum("i,j->ij", t, inv_freq)
         emb = torch.cat((freqs, freqs), dim=-1)
         _ROT[key] = (emb.cos().contiguous().to(device), emb.sin().contiguous().to(device))

@@ -115,8 +115,12 @@ class Wav2Vec2ConformerEncoder(nn.Module):
     def forward(self, hidden_states):
         c = self.config
         hidden_states = Fn.dropout(hidden_states, c.hidden_dropout, self.training)
+        graph_ld = self.training and c.layerdrop > 0 and Fn.capturing() and Fn.GRAPH_LAYERDROP
         for layer in self.layers:
             dropout_probability = torch.rand([])
+            if graph_ld:   # captured step: device-drawn LayerDrop (Fn.layerdrop_layer)
+                hidden_states = Fn.layerdrop_layer(layer, hidden_states, c.layerdrop)
+                continue
             skip = self.training and bool(dropout_probability < c.layerdrop)
             if not skip:
                 hidden_states = layer(hidden_states)

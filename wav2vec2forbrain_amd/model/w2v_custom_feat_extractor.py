@@ -104,9 +104,14 @@ class Wav2Vec2Encoder(nn.Module):
         # hidden = dropout(LN(x + gelu(posconv(x))))  (TF Wav2Vec2Encoder.forward)
         hidden_states = Fn.pos_conv_ln(hidden_states, g, v, cb, self.layer_norm.weight, self.layer_norm.bias,
                                        self.pos_conv_embed.groups, c.layer_norm_eps, c.hidden_dropout, self.training)
+        graph_ld = self.training and c.layerdrop > 0 and Fn.capturing() and Fn.GRAPH_LAYERDROP
         for layer in self.layers:
-            # LayerDrop: one CPU torch.rand([]) draw per layer, as the reference's encoder does
+            # LayerDrop: one CPU torch.rand([]) draw per layer, as the reference's encoder does; inside
+            # a captured step the draw moves to the device (redrawn on every replay)
             dropout_probability = torch.rand([])
+            if graph_ld:
+                hidden_states = Fn.layerdrop_layer(layer, hidden_states, c.layerdrop)
+                continue
             skip_the_layer = self.training and bool(dropout_probability < c.layerdrop)
             if not skip_the_layer:
                 hidden_states = layer(hidden_states)

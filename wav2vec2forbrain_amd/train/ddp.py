@@ -2,17 +2,25 @@
 torch.distributed over RCCL (backend "nccl" on ROCm) / gloo on CPU.
 
 GradBucketReducer packs the trainable gradients into fixed buckets in reverse registration order
-(lm_head -> encoder layers -> fc -> GRU -> front end, i.e. the order backward produces them) and
-issues an async all-reduce per bucket from the post-accumulate-grad hook as soon as the bucket is
-complete, so the exchange overlaps the rest of the backward. Buckets are static: a parameter that
-got no gradient on this rank (LayerDrop-skipped layer) contributes zeros, never a "find unused
-parameters" pass. Parameters that the path never uses (reference inpLayer*, hidden_start unless
-learnable, conformer pos_conv_embed) are excluded by the caller.
+(lm_head -> encoder layers -> fc -> GRU -> front end, i.e. the order backward produces them). The
+gradients live IN the buckets: zero_grad() binds every p.grad to its slice of a flat bucket buffer,
+so autograd accumulates straight into the buffer that is all-reduced (no copy in, no copy out).
+Buckets are launched strictly in index order on every rank (bucket i only after buckets < i), as
+from the post-accumulate-grad hook as soon as they are complete, so the exchange overlaps the rest
+of the backward and the collectives match across ranks even when a rank's backward skips a
+parameter (LayerDrop): such a parameter contributes the zeros of its bucket slice. Parameters the
+path never uses (reference inpLayer*, hidden_start unless learnable, conformer pos_conv_embed) are
+excluded by the caller.
 
 Bucket size: the xGMI fabric of an MI355X node is point-to-point (7 links x ~153 GB/s per GPU);
 RCCL spreads one large all-reduce over all links with multiple channels, so fewer, larger buckets
-(default 64 MB) amortise the per-collective latency while still leaving >= 2 buckets to overlap
-for the 64 MB frozen-w2v gradient set.
+(default 64 MB) amortise the per-collective latency while still leaving several buckets to overlap
+for the full-fine-tune gradient sets (424 MB base, 2.47 GB Conformer-large).
+
+Graph-replayed steps (bench.py N>1, overlap=False): backward is captured and finish() exchanges the
+buckets after the replay. Under unfreeze=brain_encoder (BASELINE configs 1-4) every trainable
+gradient is produced at the very end of backward (GRU, front end), so there is no backward left to
+overlap with; the exchange is the 64 MB brain-encoder set, ~0.1 ms on 7 links.
 """
 from __future__ import annotations
 
@@ -24,14 +32,18 @@ import torch.distributed as dist
 
 class GradBucketReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, process_group=None,
-                 average: bool = True, overlap: bool = True):
+                 average: bool = True, overlap: bool = True, grad_views: bool = True):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
         self.average = average
+        # RCCL averages inside the collective; gloo has no AVG: sum, then one scale
+        self.avg_op = (average and dist.is_initialized()
+                       and dist.get_backend(process_group) == "nccl")
         # overlap=False: no collective from the backward hooks, finish() exchanges every bucket (the
         # graph-replayed step: backward is captured, the RCCL exchange runs after each replay)
         self.overlap = overlap
+        self.grad_views = grad_views
         cap = int(bucket_mb * 1024 * 1024 / 4)
         self.buckets: list[list[torch.nn.Parameter]] = []
         cur, size = [], 0
@@ -44,68 +56,80 @@ class GradBucketReducer:
         if cur:
             self.buckets.append(cur)
         self.bucket_of = {}
-        self.offsets = {}
+        self.views = {}
         self.flat = []
         for bi, b in enumerate(self.buckets):
+            n = sum(p.numel() for p in b)
+            flat = torch.zeros(n, device=b[0].device, dtype=torch.float32)
             off = 0
             for p in b:
                 self.bucket_of[p] = bi
-                self.offsets[p] = off
+                self.views[p] = flat[off:off + p.numel()].view_as(p)
                 off += p.numel()
-            dev = b[0].device
-            self.flat.append(torch.empty(off, device=dev, dtype=torch.float32))
-        self._handles = []
+            self.flat.append(flat)
+        self.launch_log: list[int] = []     # bucket indices in the order their collectives were issued
         self._reset()
         if self.world > 1:
             for p in self.params:
                 p.register_post_accumulate_grad_hook(self._hook)
+        if grad_views:
+            self.zero_grad()
 
     def _reset(self):
         self.pending = [len(b) for b in self.buckets]
-        self.launched = [False] * len(self.buckets)
+        self.next_launch = 0
         self.works = [None] * len(self.buckets)
 
+    def zero_grad(self) -> None:
+        """Zeroes the buckets and binds every p.grad to its bucket slice (use instead of the
+        optimizer's zero_grad for these parameters: set_to_none would unbind the views)."""
+        for f in self.flat:
+            f.zero_()
+        if self.grad_views:
+            for p in self.params:
+                if p.grad is None or p.grad.data_ptr() != self.views[p].data_ptr():
+                    p.grad = self.views[p]
+
     def _launch(self, bi: int):
-        flat = self.flat[bi]
         for p in self.buckets[bi]:
-            o = self.offsets[p]
-            seg = flat[o:o + p.numel()]
+            v = self.views[p]
             if p.grad is None:
-                seg.zero_()
-            else:
-                seg.copy_(p.grad.reshape(-1))
-        self.works[bi] = dist.all_reduce(flat, group=self.pg, async_op=True)
-        self.launched[bi] = True
+                v.zero_()
+            elif p.grad.data_ptr() != v.data_ptr():
+                v.copy_(p.grad)
+        op = dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM
+        self.works[bi] = dist.all_reduce(self.flat[bi], op=op, group=self.pg, async_op=True)
+        self.launch_log.append(bi)
+
+    def _launch_ready(self):
+        while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
+            self._launch(self.next_launch)
+            self.next_launch += 1
 
     def _hook(self, p):
         if not self.overlap:
             return
         bi = self.bucket_of.get(p)
-        if bi is None or self.launched[bi]:
+        if bi is None or bi < self.next_launch:
             return
         self.pending[bi] -= 1
-        if self.pending[bi] == 0:
-            self._launch(bi)
+        self._launch_ready()
 
     def finish(self):
-        """Call after loss.backward(): launches incomplete buckets, waits, writes averaged grads."""
+        """Call after loss.backward(): launches the remaining buckets (in order), waits, and leaves
+        the averaged gradient in every p.grad (its bucket slice)."""
         if self.world <= 1:
             return
-        for bi in range(len(self.buckets)):
-            if not self.launched[bi]:
-                self._launch(bi)
+        while self.next_launch < len(self.buckets):
+            self._launch(self.next_launch)
+            self.next_launch += 1
         for bi, w in enumerate(self.works):
             w.wait()
-            flat = self.flat[bi]
-            if self.average:
-                flat.div_(self.world)
+            if self.average and not self.avg_op:
+                self.flat[bi].div_(self.world)
             for p in self.buckets[bi]:
-                o = self.offsets[p]
-                g = flat[o:o + p.numel()].view_as(p)
-                if p.grad is None:
-                    p.grad = g.clone()
-                else:
-                    p.grad.copy_(g)
+                if p.grad is None or p.grad.data_ptr() != self.views[p].data_ptr():
+                    p.grad = self.views[p]
         self._reset()
 
 
@@ -116,7 +140,6 @@ def unused_param_names(model: torch.nn.Module) -> set[str]:
         if ".inpLayer" in n or n.startswith("inpLayer"):
             out.add(n)
         if n.endswith("hidden_start"):
-            enc = model
             learn = False
             try:
                 learn = model.brain_encoder.neural_decoder.encoder.config.encoder_learnable_inital_state

@@ -30,14 +30,21 @@ class Trainer:
         self.optimizer = experiment.create_optimizer()
         self.scheduler = experiment.get_scheduler(self.optimizer)
         self.reducer = None
+        self.frozen_reducer = None
+        opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
+        frozen = [p for p in self.model.parameters() if p.requires_grad and id(p) not in opt_ids]
         if dist.is_initialized() and dist.get_world_size() > 1:
             skip = unused_param_names(self.model)
-            opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
             params = [p for n, p in self.model.named_parameters() if id(p) in opt_ids and n not in skip]
             self.reducer = GradBucketReducer(params)
+            if self.config.gradient_clipping is not None:
+                # clip_grad_norm_ runs over model.parameters() (reference :72-75), frozen gradients
+                # included; averaging those too keeps every rank's clip coefficient equal to the
+                # single-process global-batch one (they accumulate across steps identically on all
+                # ranks once averaged, so averaging the running sum each step is exact)
+                self.frozen_reducer = GradBucketReducer(frozen, overlap=False, grad_views=False)
         # frozen parameters (not optimised): their gradient GEMMs run deferred beside the GRU backward
-        opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
-        Fn.set_deferred_wgrad([p for p in self.model.parameters() if p.requires_grad and id(p) not in opt_ids])
+        Fn.set_deferred_wgrad(frozen)
 
     def _log_intermediate(self, batch: int, n_batches: int, evaluator):
         print(f"Batch {batch + 1}/{n_batches} loss: {evaluator.get_latest_loss():.2f} "
@@ -46,7 +53,10 @@ class Trainer:
     def train_step(self, batch: SampleBatch):
         """One step of the reference loop body (:42-79): zero_grad, (no-op noise), forward,
         backward, [DP all-reduce], optional clip, optimizer step."""
-        self.optimizer.zero_grad()
+        if self.reducer is not None:
+            self.reducer.zero_grad()    # trainable gradients live in the all-reduce buckets
+        else:
+            self.optimizer.zero_grad()
         if self.config.whiteNoiseSD > 0:       # reference :46-52: computed and discarded
             _ = torch.randn(batch.input.shape, device=batch.input.device) * self.config.whiteNoiseSD
         if self.config.constantOffsetSD > 0:   # reference :54-62: computed and discarded
@@ -59,6 +69,8 @@ class Trainer:
         Fn.join_wgrad()
         if self.reducer is not None:
             self.reducer.finish()
+        if self.frozen_reducer is not None:
+            self.frozen_reducer.finish()
         if self.config.gradient_clipping is not None:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.gradient_clipping)
         self.optimizer.step()
@@ -129,6 +141,9 @@ class Trainer:
             self.model.load_state_dict(torch.load(best_path, weights_only=True))
             os.remove(best_path)
             os.rmdir(os.path.dirname(best_path))
+        if getattr(self.config, "train_on_val_once", False):   # reference :211-213
+            print("Training one epoch on val set")
+            self._train_epoch(self.dataloader_val)
         test_losses = self._evaluate_epoch("test")
         print(f"\nTest loss: {test_losses.get_average_loss()}")
         return self.model, (history, test_losses)
