@@ -1,0 +1,119 @@
+"""Data-parallel identity on the real model: two ranks (gloo, both on
+the one GPU of the box), each stepping half of a global batch through the HIP training step with
+train.ddp.GradBucketReducer, produce the single-process global-batch loss (mean of the rank means)
+and gradients (bucket average). For the Conformer this holds because BatchNorm statistics are
+synchronised over the ranks (functional.sync_batchnorm); its running statistics match too.
+Deterministic mode (dropout / LayerDrop 0), exact-fp32 MFMA, so only the reduction order differs."""
+import os
+import socket
+
+import pytest
+import torch
+
+from tests.helpers import CFG, build_model, batch_dict
+
+pytestmark = pytest.mark.gpu
+
+WORLD = 2
+
+
+def _cfg(name):
+    c = dict(CFG[name])
+    c.update(name=name, B=4, in_lens=[c["L"], c["L"] - 16, c["L"] - 24, c["L"]])
+    return c
+
+
+def _batch(cfg, rows):
+    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    b = batch_dict(cfg)
+    sl = slice(rows[0], rows[1])
+    tl = b["target_lens"][sl]
+    S = int(b["target_lens"].max())
+    return make_b2t_batch(b["x"][sl], b["target"][sl, :S], b["day_idxs"][sl], b["input_lens"][sl], tl).cuda()
+
+
+def _step(model, batch, reducer=None):
+    from wav2vec2forbrain_amd import functional as Fn
+    if reducer is not None:
+        reducer.zero_grad()
+    with Fn.precision("fp32"):
+        out = model(batch)
+        out.loss.backward()
+        Fn.join_wgrad()
+    if reducer is not None:
+        reducer.finish()
+    torch.cuda.synchronize()
+    return float(out.metrics["ctc_loss"])
+
+
+def _trainable(model):
+    from wav2vec2forbrain_amd.train.ddp import unused_param_names
+    skip = unused_param_names(model)
+    return [(n, p) for n, p in model.named_parameters() if n.startswith("brain_encoder.") and n not in skip]
+
+
+def _worker(rank, name, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from wav2vec2forbrain_amd.train.ddp import GradBucketReducer
+        cfg = _cfg(name)
+        model = build_model(cfg)
+        model.train()
+        for p in model.w2v_encoder.parameters():   # unfreeze=brain_encoder: w2v weights frozen
+            p.requires_grad_(False)
+        red = GradBucketReducer([p for _, p in _trainable(model)], bucket_mb=0.05)
+        per = cfg["B"] // WORLD
+        loss = _step(model, _batch(cfg, (rank * per, (rank + 1) * per)), red)
+        loss_t = torch.tensor([loss])
+        dist.all_reduce(loss_t)
+        torch.save({"loss": float(loss_t) / WORLD,
+                    "grads": {n: p.grad.detach().cpu() for n, p in _trainable(model)},
+                    "bufs": {n: b.detach().cpu() for n, b in model.named_buffers() if b.is_floating_point()}},
+                   os.path.join(out_dir, f"rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_conf"])
+def test_dp_step_equals_global_batch_step(name, tmp_path):
+    import torch.multiprocessing as mp
+    cfg = _cfg(name)
+    ref = build_model(cfg)
+    ref.train()
+    for p in ref.w2v_encoder.parameters():
+        p.requires_grad_(False)
+    loss = _step(ref, _batch(cfg, (0, cfg["B"])))
+    grads = {n: p.grad.detach().cpu() for n, p in _trainable(ref)}
+    bufs = {n: b.detach().cpu() for n, b in ref.named_buffers() if b.is_floating_point()}
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, name, port, str(tmp_path))) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(WORLD)]
+    for r in res:
+        assert abs(r["loss"] - loss) <= 2e-5 * abs(loss), (r["loss"], loss)
+        gmax = max(float(g.norm()) for g in grads.values())
+        for n, g in grads.items():
+            d = float((r["grads"][n] - g).norm())
+            assert d <= 1e-4 * float(g.norm()) + 1e-6 * gmax, (n, d, float(g.norm()))
+        for n, b in bufs.items():   # Conformer BatchNorm running stats: global-batch statistics (SyncBN)
+            d = float((r["bufs"][n] - b).norm())
+            assert d <= 1e-4 * float(b.norm()) + 1e-6, (n, d)
+    # the ranks hold identical gradients after the exchange
+    for n in grads:
+        assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n

@@ -1,0 +1,1 @@
+"""Experiment layer (reference src/experiments): run.py builds one of these by name."""

@@ -35,6 +35,7 @@ class _State:
     prec = 0
     fwd16 = False   # forward_f16(): fp32-operand GEMMs of a forward pass on fp16 MFMA
     nosplit = False  # no split-K (deferred weight gradients issued on concurrent side streams)
+    sync_bn = None   # process group for synchronised BatchNorm statistics (sync_batchnorm())
 
 
 _state = _State()
@@ -1964,6 +1965,52 @@ class _ConformerAttnBlock(torch.autograd.Function):
         return (dx.view(B, T, D), dg, db, *grads, dwo, dbo, None, None, None)
 
 
+# ------------------------------------------------------------------ synchronised BatchNorm
+def _bn_fwd_sync(c, gamma, beta, run_mean, run_var, y, pre, mean, rstd, M, C, eps, momentum, act, ws, group):
+    """Training BatchNorm over the rows of every data-parallel rank: the
+    per-channel sum and the sum of squared deviations from the global mean are all-reduced
+    (2 x C floats per conv module); running statistics use the global count, like torch SyncBN."""
+    import torch.distributed as dist
+    count = M * dist.get_world_size(group)
+    _lib.call("b2p_batchnorm_stats", _p(c), None, _p(mean), M, C, _p(ws), _st())
+    dist.all_reduce(mean, group=group)
+    _lib.call("b2p_batchnorm_finalize", _p(mean), None, None, None, None, C, count, float(eps), float(momentum), 0,
+              _st())
+    sq = torch.empty(C, device=c.device)
+    _lib.call("b2p_batchnorm_stats", _p(c), _p(mean), _p(sq), M, C, _p(ws), _st())
+    dist.all_reduce(sq, group=group)
+    _lib.call("b2p_batchnorm_finalize", _p(mean), _p(sq), _p(rstd), _p(run_mean), _p(run_var), C, count, float(eps),
+              float(momentum), 1, _st())
+    _lib.call("b2p_batchnorm_apply", _p(c), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(y), _p(pre), M, C, act,
+              _st())
+
+
+def _bn_bwd_sync(dy, pre, c, mean, rstd, gamma, dx, dgamma, dbeta, M, C, act, ws, group):
+    """Backward of _bn_fwd_sync: the per-channel sums of g and g * xhat are all-reduced for the input
+    gradient (one 2C all-reduce); dgamma / dbeta stay this rank's sums (the gradient all-reduce
+    averages them like every other parameter)."""
+    import torch.distributed as dist
+    count = M * dist.get_world_size(group)
+    g = torch.empty(M, C, device=c.device)
+    _lib.call("b2p_batchnorm_bwd_sums", _p(dy), _p(pre), _p(c), _p(mean), _p(rstd), _p(g), _p(dbeta), _p(dgamma), M,
+              C, act, _p(ws), _st())
+    sums = torch.cat([dbeta, dgamma])
+    dist.all_reduce(sums, group=group)
+    _lib.call("b2p_batchnorm_bwd_dx", _p(g), _p(c), _p(mean), _p(rstd), _p(gamma), _p(sums), _p(sums, C), _p(dx), M, C,
+              count, _st())
+
+
+@contextlib.contextmanager
+def sync_batchnorm(group):
+    """Training-mode BatchNorm inside uses statistics synchronised over `group` (None: local)."""
+    old = _state.sync_bn
+    _state.sync_bn = group
+    try:
+        yield
+    finally:
+        _state.sync_bn = old
+
+
 class _ConvModule(torch.autograd.Function):
     """y = x + dropout(pw2(act(BN(dwconv(GLU(pw1(LN x)))))))   (TF conf Wav2Vec2ConformerConvolutionModule)"""
 
@@ -1985,12 +2032,17 @@ class _ConvModule(torch.autograd.Function):
         _lib.call("b2p_dwconv_fwd", _p(u), _p(w_dw), _p(c), B, T, D, K, _st())
         s = torch.empty(NT, D, device=dev)
         ws = torch.empty(int(_lib.load().b2p_batchnorm_workspace(NT, D)), device=dev)
+        sync = None
         if training:
             pre = torch.empty(NT, D, device=dev)
             bm = torch.empty(D, device=dev)
             br = torch.empty(D, device=dev)
-            _lib.call("b2p_batchnorm_fwd", _p(c), _p(bn_g), _p(bn_b), _p(bn_rm), _p(bn_rv), _p(s), _p(pre), _p(bm),
-                      _p(br), NT, D, float(bn_eps), float(momentum), act, _p(ws), _st())
+            sync = _state.sync_bn
+            if sync is not None:
+                _bn_fwd_sync(c, bn_g, bn_b, bn_rm, bn_rv, s, pre, bm, br, NT, D, bn_eps, momentum, act, ws, sync)
+            else:
+                _lib.call("b2p_batchnorm_fwd", _p(c), _p(bn_g), _p(bn_b), _p(bn_rm), _p(bn_rv), _p(s), _p(pre),
+                          _p(bm), _p(br), NT, D, float(bn_eps), float(momentum), act, _p(ws), _st())
         else:
             pre = bm = br = None
             _lib.call("b2p_batchnorm_eval", _p(c), _p(bn_g), _p(bn_b), _p(bn_rm), _p(bn_rv), _p(s), NT, D,
@@ -2000,6 +2052,7 @@ class _ConvModule(torch.autograd.Function):
         ctx.save_for_backward(x2, h, mean, rstd, a, u, c, pre, bm, br, s, g, w_pw1, w_dw, bn_g, w_pw2)
         ctx.cfg = cfg
         ctx.shape = (B, T, D, K)
+        ctx.sync = sync
         return y.view(B, T, D)
 
     @staticmethod
@@ -2031,8 +2084,11 @@ class _ConvModule(torch.autograd.Function):
         dbn_g = torch.empty(D, device=dev)
         dbn_b = torch.empty(D, device=dev)
         ws = torch.empty(int(_lib.load().b2p_batchnorm_workspace(NT, D)), device=dev)
-        _lib.call("b2p_batchnorm_bwd", _p(ds), _p(pre), _p(c), _p(bm), _p(br), _p(bn_g), _p(dc), _p(dbn_g), _p(dbn_b),
-                  NT, D, act, _p(ws), _st())
+        if ctx.sync is not None:
+            _bn_bwd_sync(ds, pre, c, bm, br, bn_g, dc, dbn_g, dbn_b, NT, D, act, ws, ctx.sync)
+        else:
+            _lib.call("b2p_batchnorm_bwd", _p(ds), _p(pre), _p(c), _p(bm), _p(br), _p(bn_g), _p(dc), _p(dbn_g),
+                      _p(dbn_b), NT, D, act, _p(ws), _st())
         du = torch.empty(NT, D, device=dev)
         ddw = torch.empty_like(w_dw) if ng[4] else None
         wsd = torch.empty(int(_lib.load().b2p_dwconv_bwd_workspace(B, T, D, K)), device=dev)

@@ -172,13 +172,21 @@ class W2VConformerBrainEncoderModel(B2TModel):
         # bf16 mode: the Conformer's forward GEMMs on fp16 MFMA (Fn.forward_f16: removes the CTC-loss
         # bias of bf16 logit noise over 24 layers; backward stays bf16)
         self.forward_f16 = True
+        # data-parallel runs: BatchNorm statistics over the global batch (SyncBN), so a DP step equals
+        # the single-process step on the same global batch; False = per-rank stats
+        self.sync_batchnorm = True
+        self.process_group = None
 
     def forward(self, batch: B2tSampleBatch):
         encoded_brain = self.brain_encoder.forward(batch)
         targets = batch.target
         assert targets is not None
         targets = targets.masked_fill(targets < 1, -100)
-        with Fn.forward_f16(self.forward_f16):
+        import torch.distributed as dist
+        sync = (self.training and self.sync_batchnorm and dist.is_available() and dist.is_initialized()
+                and dist.get_world_size(self.process_group) > 1)
+        with Fn.forward_f16(self.forward_f16), Fn.sync_batchnorm(
+                (self.process_group or dist.group.WORLD) if sync else None):
             w2v_output = self.w2v_encoder.forward(encoded_brain.logits)
         ctc_loss = (Fn.ctc_loss(w2v_output, targets, encoded_brain.logit_lens, batch.target_lens, self.blank)
                     if batch.target_lens is not None and encoded_brain.logit_lens is not None else None)

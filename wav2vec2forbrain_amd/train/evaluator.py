@@ -1,17 +1,30 @@
-"""Evaluators — a minimal mirror of reference src/train/evaluator.py:20-120 (loss tracking, greedy
-CTC decode, WER/CER). Train/val batches on the GPU get their word errors from the device decode
-(functional.ctc_greedy_wer, csrc/decode.hip); the host path (test mode, CER, CPU
-tensors) restates the reference's torcheval / edit_distance metrics, which are absent here."""
+"""Evaluators — mirror reference src/train/evaluator.py:20-242 (per-batch loss, greedy CTC decode,
+word and character error rates into a SingleEpochHistory).
+
+The reference decodes every batch on the host (logits.argmax(-1).cpu() -> tokenizer.batch_decode ->
+torcheval WordErrorRate / edit_distance CER). Here a batch whose logits are on the GPU gets its
+word and character errors from the device decode kernels (csrc/decode.hip: functional.
+ctc_greedy_wer / ctc_greedy_cer) and only the scalars cross to the host, in one
+transfer with the loss. Strings are still built on the host where the reference keeps them (test
+mode, track_non_test_predictions), from the same greedy decode.
+
+LM decoding (pyctcdecode + KenLM through Wav2Vec2ProcessorWithLM, src/train/evaluator.py:148-210)
+needs hub/KenLM assets that are not available offline; lm_decode_test_predictions raises.
+"""
 from __future__ import annotations
 
-from dataclasses import dataclass, field
+from abc import ABC, abstractmethod
+from math import nan
+from typing import Literal
 
 import torch
 
 from ..model.b2tmodel import ModelOutput
+from .history import DecodedPredictionBatch, MetricEntry, SingleEpochHistory
 
 
 def edit_distance(a, b) -> int:
+    """Levenshtein distance (unit costs) between two sequences (host path)."""
     prev = list(range(len(b) + 1))
     for i, x in enumerate(a, 1):
         cur = [i] + [0] * len(b)
@@ -21,78 +34,140 @@ def edit_distance(a, b) -> int:
     return prev[-1]
 
 
-def greedy_ctc_decode(ids, vocab, blank=0, word_delimiter="|"):
-    """argmax ids -> group repeats -> drop blank/pad -> string (tokenizer.batch_decode(group_tokens=True))."""
-    out, last = [], None
-    for i in ids:
-        if i != last and i != blank:
-            tok = vocab[i] if i < len(vocab) else ""
-            if not (tok.startswith("<") and tok.endswith(">")):
-                out.append(" " if tok == word_delimiter else tok)
-        last = i
-    return "".join(out).strip()
+def cut_after_eos_token(s: str, eos: str = "</s>") -> str:
+    i = s.find(eos)
+    return s if i == -1 else s[:i + len(eos)]
 
 
-@dataclass
-class EpochResult:
-    losses: list = field(default_factory=list)
-    metrics: dict = field(default_factory=dict)
-
-    def get_average_loss(self):
-        return sum(self.losses) / max(len(self.losses), 1)
+def word_error_rate(preds: list[str], targets: list[str]) -> float:
+    """torcheval WordErrorRate over a batch: summed word edit distances / summed target words."""
+    errs = sum(edit_distance(p.split(), t.split()) for p, t in zip(preds, targets))
+    n = sum(len(t.split()) for t in targets)
+    return errs / n if n else nan
 
 
-class Evaluator:
-    def __init__(self, mode: str, vocab=None, decode: bool = False):
+def char_error_rate(preds: list[str], targets: list[str]) -> float:
+    """Reference calculate_char_error_rate: summed character edit distances / summed target lengths."""
+    errs = sum(edit_distance(t, p) for p, t in zip(preds, targets))
+    n = sum(len(t) for t in targets)
+    return errs / n if n else nan
+
+
+def _ids(tokenizer):
+    v = tokenizer.get_vocab()
+    return v.get(tokenizer.pad_token, 0), v.get(tokenizer.eos_token, 2), v.get(tokenizer.word_delimiter_token, 4)
+
+
+class Evaluator(ABC):
+    def __init__(self, mode: Literal["train", "val", "test"], track_non_test_predictions: bool = False):
+        self.running_loss = 0.0
+        self.n_losses = 0
+        self.latest_loss = nan
         self.mode = mode
-        self.vocab = vocab
-        self.decode = decode and vocab is not None
-        self.result = EpochResult()
-        self.word_errs = self.words = self.char_errs = self.chars = 0
+        self.track_non_test_predictions = track_non_test_predictions
 
     def track_batch(self, predictions: ModelOutput, sample):
-        loss = predictions.metrics.get("ctc_loss")
-        if loss is None and predictions.loss is not None:
-            loss = predictions.loss.item()
-        if isinstance(loss, torch.Tensor):
-            loss = loss.item()
-        self.result.losses.append(float(loss))
-        if self.decode and sample.target is not None and predictions.logits.is_cuda and self.mode != "test":
-            # word errors on the device (csrc/decode.hip): no argmax / strings round trip per step;
-            # the sums stay on the device until evaluate()
-            from .. import functional as Fn
-            ids = {t: i for i, t in enumerate(self.vocab)}
-            _, errs, nw, _, _ = Fn.ctc_greedy_wer(predictions.logits.detach().contiguous(), sample.target,
-                                                  blank=ids.get("<pad>", 0), eos=ids.get("</s>", 2),
-                                                  delim=ids.get("|", 4))
-            self.dev_errs = errs.sum() + getattr(self, "dev_errs", 0)
-            self.dev_words = nw.sum() + getattr(self, "dev_words", 0)
-            return
-        if self.decode and sample.target is not None:
-            pred = predictions.logits.argmax(-1).cpu().tolist()
-            tgt = sample.target.cpu().tolist()
-            for p, t in zip(pred, tgt):
-                ps = greedy_ctc_decode(p, self.vocab)
-                ts = greedy_ctc_decode([x for x in t if x > 0], self.vocab) if False else \
-                    "".join(" " if self.vocab[x] == "|" else self.vocab[x] for x in t if x > 0).strip()
-                self.word_errs += edit_distance(ps.split(), ts.split())
-                self.words += max(len(ts.split()), 1)
-                self.char_errs += edit_distance(ps, ts)
-                self.chars += max(len(ts), 1)
-
-    def get_latest_loss(self):
-        return self.result.losses[-1]
+        assert predictions.loss is not None
+        loss = self._track_batch(predictions, sample)
+        self.running_loss += loss
+        self.n_losses += 1
+        self.latest_loss = loss
 
     def get_running_loss(self):
-        return self.result.get_average_loss()
+        return self.running_loss / self.n_losses
 
-    def evaluate(self) -> EpochResult:
-        if getattr(self, "dev_words", None) is not None:
-            self.result.metrics["word_error_rate"] = float(self.dev_errs) / max(float(self.dev_words), 1.0)
-        if self.decode and self.words:
-            self.result.metrics["word_error_rate"] = self.word_errs / self.words
-            self.result.metrics["char_error_rate"] = self.char_errs / self.chars
-        return self.result
+    def get_latest_loss(self):
+        return self.latest_loss
+
+    @abstractmethod
+    def _track_batch(self, predictions: ModelOutput, sample) -> float:
+        """Records the batch; returns its loss as a float."""
+
+    @abstractmethod
+    def evaluate(self) -> SingleEpochHistory:
+        raise NotImplementedError()
 
     def clean_up(self):
         pass
+
+
+class DefaultEvaluator(Evaluator):
+    """Greedy decode + word error rate per batch (reference :57-120)."""
+
+    with_cer = False
+
+    def __init__(self, tokenizer, mode: Literal["train", "val", "test"], track_non_test_predictions: bool = False):
+        super().__init__(mode, track_non_test_predictions)
+        self.history = SingleEpochHistory()
+        self.tokenizer = tokenizer
+
+    def keep_strings(self) -> bool:
+        return self.mode == "test" or self.track_non_test_predictions
+
+    def decode_predictions(self, predictions: ModelOutput, sample) -> DecodedPredictionBatch:
+        ids = predictions.logits.argmax(dim=-1).cpu().numpy()
+        pred = self.tokenizer.batch_decode(ids, group_tokens=True)
+        labels = (self.tokenizer.batch_decode(sample.target.cpu().numpy(), group_tokens=False)
+                  if sample.target is not None else None)
+        return DecodedPredictionBatch(pred, labels)
+
+    def _device_metrics(self, predictions: ModelOutput, sample) -> list[torch.Tensor]:
+        from .. import functional as Fn
+        from ..datasets.tokenizer import vocab_of
+        blank, eos, delim = _ids(self.tokenizer)
+        logits = predictions.logits.detach().contiguous()
+        wer, _, nw, _, _ = Fn.ctc_greedy_wer(logits, sample.target, blank=blank, eos=eos, delim=delim)
+        out = [torch.where(nw.sum() > 0, wer, torch.full_like(wer, nan))]
+        if self.with_cer:
+            cer, _, nch = Fn.ctc_greedy_cer(logits, sample.target, vocab_of(self.tokenizer), blank=blank, eos=eos,
+                                            delim=delim)
+            out.append(torch.where(nch.sum() > 0, cer, torch.full_like(cer, nan)))
+        return out
+
+    def _track_batch(self, predictions: ModelOutput, sample) -> float:
+        loss_t = predictions.loss.detach().reshape(())
+        decoded = None
+        extra = {}
+        if sample.target is not None and predictions.logits.is_cuda and not self.keep_strings():
+            vals = torch.stack([loss_t.float()] + [v.float().to(loss_t.device) for v in
+                                                   self._device_metrics(predictions, sample)]).tolist()
+            loss = vals[0]
+            extra["word_error_rate"] = vals[1]
+            if self.with_cer:
+                extra["char_error_rate"] = vals[2]
+        else:
+            loss = float(loss_t)
+            pred, labels = self.decode_predictions(predictions, sample)
+            pred = [cut_after_eos_token(s) for s in pred]
+            if labels is not None:
+                extra["word_error_rate"] = word_error_rate(pred, labels)
+                if self.with_cer:
+                    extra["char_error_rate"] = char_error_rate(pred, labels)
+            decoded = DecodedPredictionBatch(pred, labels) if self.keep_strings() else None
+        metrics = {k: (float(v) if isinstance(v, torch.Tensor) else v) for k, v in predictions.metrics.items()}
+        metrics.update(extra)
+        predictions.metrics.update(extra)
+        self.history.add_batch_metric(MetricEntry(metrics, loss), decoded)
+        return loss
+
+    def evaluate(self) -> SingleEpochHistory:
+        return self.history
+
+
+class EvaluatorWithW2vLMDecoder(DefaultEvaluator):
+    """DefaultEvaluator + character error rate (reference :127-242)."""
+
+    with_cer = True
+
+    def __init__(self, tokenizer, mode: Literal["train", "val", "test"], cache_dir: str = "",
+                 processor_checkpoint: str = "", track_non_test_predictions: bool = False,
+                 lm_decode_test_predictions: bool = False, lm_decode_beam_width=None, lm_decode_beam_prune_logp=None,
+                 lm_decode_token_min_logp=None, lm_decode_alpha=None, lm_decode_beta=None,
+                 lm_decode_score_boundary=None):
+        super().__init__(tokenizer, mode, track_non_test_predictions)
+        if lm_decode_test_predictions and mode == "test":
+            raise NotImplementedError(
+                f"LM decoding needs Wav2Vec2ProcessorWithLM.from_pretrained({processor_checkpoint!r}) and its KenLM "
+                "model, which are not available offline")
+        self.lm_decode_beam_width = lm_decode_beam_width
+        self.lm_decode_alpha, self.lm_decode_beta = lm_decode_alpha, lm_decode_beta

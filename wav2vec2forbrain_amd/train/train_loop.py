@@ -16,7 +16,7 @@ import torch.distributed as dist
 
 from ..datasets.batch_types import SampleBatch
 from .ddp import GradBucketReducer, unused_param_names
-from .evaluator import EpochResult
+from .history import EpochLosses, SingleEpochHistory, TrainHistory
 
 
 class Trainer:
@@ -103,13 +103,16 @@ class Trainer:
         return results
 
     def train(self):
-        history = []
+        history: list[EpochLosses] = (list(self.experiment.checkpoint_history.epochs)
+                                      if self.experiment.checkpoint_history is not None else [])
         best = float("inf" if self.config.minimize_best_model_metric else "-inf")
-        best_path = os.path.join(self.experiment.cache_dir, "model_checkpoints", str(uuid.uuid4()), "best_model.pt")
+        best_path = os.path.join(self.experiment.yaml_config.cache_dir, "model_checkpoints", str(uuid.uuid4()),
+                                 "best_model.pt")
         os.makedirs(os.path.dirname(best_path), exist_ok=True)
 
-        def metric(r: EpochResult):
-            return r.get_average_loss() if self.config.best_model_metric == "loss" else r.metrics[self.config.best_model_metric]
+        def metric(h: SingleEpochHistory):
+            avg = h.get_average()
+            return avg.loss if self.config.best_model_metric == "loss" else avg.metrics[self.config.best_model_metric]
 
         saved = False
         for epoch in range(self.config.epochs):
@@ -117,33 +120,36 @@ class Trainer:
             train_losses = self._train_epoch(self.dataloader_train)
             val_losses = self._evaluate_epoch("val")
             self.scheduler.step()
-            print(f"\nFinished Epoch {epoch + 1}/{self.config.epochs} train loss: {train_losses.get_average_loss()} "
-                  f"val loss: {val_losses.get_average_loss()}")
-            history.append((train_losses, val_losses))
+            print(f"\n\n{'=' * 20}\nFinished Epoch {epoch + 1}/{self.config.epochs} "
+                  f"train {self.config.loss_function}-loss: {train_losses.get_average().loss} "
+                  f"val {self.config.loss_function}-loss: {val_losses.get_average().loss}")
+            history.append(EpochLosses(train_losses, val_losses))
             if self.config.return_best_model:
                 cur = metric(val_losses)
-                better = cur < best if self.config.minimize_best_model_metric else cur > best
-                if better:
+                if (cur < best) if self.config.minimize_best_model_metric else (cur > best):
                     best = cur
                     torch.save(self.model.state_dict(), best_path)
                     saved = True
-            if self.config.early_stopping_patience is not None and len(history) >= self.config.early_stopping_patience:
-                hist = [metric(v) for _, v in history][-self.config.early_stopping_patience:]
-                if self.config.minimize_best_model_metric:
-                    hist[0] -= self.config.early_stopping_delta
-                else:
-                    hist[0] += self.config.early_stopping_delta
-                bi = np.argmin(hist) if self.config.minimize_best_model_metric else np.argmax(hist)
+                    print(f"\n\nSaving model checkpoint at {best_path}\n")
+            patience = self.config.early_stopping_patience
+            if patience is not None and len(history) >= patience:
+                recent = [metric(e.val_losses) for e in history][-patience:]
+                # the oldest of the window, shifted by the delta, is the baseline to beat
+                recent[0] += -self.config.early_stopping_delta if self.config.minimize_best_model_metric \
+                    else self.config.early_stopping_delta
+                bi = np.argmin(recent) if self.config.minimize_best_model_metric else np.argmax(recent)
                 if bi == 0:
-                    print(f"\nEarly stopping after {epoch} epochs")
+                    print(f"\nEarly stopping after {epoch} epochs ({patience} epochs without improvement in "
+                          f"validation {self.config.best_model_metric} metrics)")
                     break
         if self.config.return_best_model and saved:
             self.model.load_state_dict(torch.load(best_path, weights_only=True))
             os.remove(best_path)
             os.rmdir(os.path.dirname(best_path))
+            print("Loaded model with best validation loss of this experiment from disk")
         if getattr(self.config, "train_on_val_once", False):   # reference :211-213
             print("Training one epoch on val set")
             self._train_epoch(self.dataloader_val)
         test_losses = self._evaluate_epoch("test")
-        print(f"\nTest loss: {test_losses.get_average_loss()}")
-        return self.model, (history, test_losses)
+        print(f"\nTest loss ({self.config.loss_function}): {test_losses.get_average().loss}")
+        return self.model, TrainHistory(history, test_losses)
