@@ -311,6 +311,24 @@ int b2p_gru_bwd16(const float* doL, const float* whh, const float* hL, const flo
 int b2p_gru_hprev(const float* out, const float* h0, float* hp, int64_t B, int64_t T, int64_t H,
                   int ndir, b2p_stream_t stream);
 
+/* ------------------------------------------------------------------ multi-CU persistent GRU (bf16)
+ * csrc/grumc.hip: the whole recurrence of an nn.GRU layer in one launch for hidden sizes one CU
+ * cannot hold (256, 384, 512; the Conformer experiment's H = 512 encoder, reference
+ * src/model/brain_feature_extractor.py:39-47). H/64 workgroups per (direction, 16 batch rows), each
+ * keeping its units' W_hh rows in registers, exchange the state every step through L2 as tagged
+ * granules. Same tensors and layouts as b2p_gru_fwd / b2p_gru_bwd (standard (B, T, ...) layouts);
+ * bf16 MFMA operands, fp32 accumulation and state. workspace: b2p_gru_mc_workspace(B, H, ndir)
+ * bytes, 16-byte aligned, zeroed by the call itself (the first int is a timeout flag: nonzero after
+ * the call means a member never arrived). Needs (H/64) * ndir * ceil(B/16) co-resident CUs. */
+int b2p_gru_mc_supported(int64_t H);
+int64_t b2p_gru_mc_workspace(int64_t B, int64_t H, int ndir);
+int b2p_gru_fwd_mc(const float* gi, const float* whh, const float* bhh, const float* h0, float* out,
+                   float* saved, void* workspace, int64_t B, int64_t T, int64_t H, int ndir,
+                   b2p_stream_t stream);
+int b2p_gru_bwd_mc(const float* dout, const float* whh, const float* out, const float* saved,
+                   const float* h0, float* dgi, float* dgh, float* dh0, void* workspace, int64_t B,
+                   int64_t T, int64_t H, int ndir, b2p_stream_t stream);
+
 /* ------------------------------------------------------------------ fused attention (bf16 mode)
  * softmax(Q K^T * scale) -> dropout(p) -> @ V per (batch, head), no mask (HF Wav2Vec2Attention,
  * TF w2v:438-463,529-545; the Conformer's rotary self-attention core, TF conf:458-470);

@@ -133,11 +133,15 @@ def test_gru_layer(unfold, h0, B, H):
 
 
 @pytest.mark.parametrize("H,B,T,h0,unfold", [(32, 3, 17, True, False), (64, 5, 23, True, False), (128, 20, 40, False, False),
-                                               (256, 33, 57, True, False), (256, 32, 249, False, True)])
+                                               (256, 33, 57, True, False), (256, 32, 249, False, True),
+                                               (384, 20, 40, True, False), (512, 33, 57, True, False),
+                                               (512, 32, 249, False, True)])
 def test_gru_layer_bf16_persistent(H, B, T, h0, unfold):
-    """bf16 mode: the persistent MFMA recurrence (csrc/gru16.hip) vs the fp32 oracle GRU
-    (nn.GRU semantics). bf16 MFMA operands (W_hh, h) -> relative L2 tolerance 2e-2 on outputs and
-    every gradient; B not a multiple of the 16-row workgroup tile; both directions; optional h0."""
+    """bf16 mode: the persistent MFMA recurrences — one CU per (direction, 16 rows) for H <= 256
+    (csrc/gru16.hip), H/64 CUs exchanging the state through L2 for H = 384 / 512 (csrc/grumc.hip,
+    the Conformer encoder's H = 512) — vs the fp32 oracle GRU (nn.GRU semantics). bf16 MFMA operands
+    (W_hh, h) -> relative L2 tolerance 2e-2 on outputs and every gradient; B not a multiple of the
+    16-row tile; both directions; optional h0."""
     Fn = _fn()
     from oracle.b2p2t_oracle import gru_direction, unfold as unfold_ref
     torch.manual_seed(11)
@@ -625,3 +629,63 @@ def test_pos_conv_ln_bf16_posconv16():
     assert rl2(out, ref) < 1e-2
     for i, (a, b) in enumerate(zip(got, refg)):
         assert rl2(a, b) < 2e-2, (i, rl2(a, b))
+
+
+def test_gru_mc_direct_and_graph_replay():
+    """csrc/grumc.hip through the C ABI: the multi-CU forward / backward equal the per-step fp32
+    kernels (csrc/gru.hip) within bf16 operand rounding, the timeout flag stays 0, and replaying a
+    captured graph of both launches (the workspace memset is a graph node, so stale tags of the
+    previous replay never match) reproduces the eager results bit for bit."""
+    Fn = _fn()
+    from wav2vec2forbrain_amd import _lib
+    torch.manual_seed(5)
+    B, T, H, nd = 33, 41, 512, 2
+    dev = "cuda"
+    gi = torch.randn(B, T, nd * 3 * H, device=dev)
+    whh = torch.randn(nd, 3 * H, H, device=dev) / math.sqrt(H)
+    bhh = torch.randn(nd, 3 * H, device=dev) * 0.1
+    h0 = torch.randn(nd, B, H, device=dev)
+    dout = torch.randn(B, T, nd * H, device=dev)
+
+    def run(mc):
+        out = torch.empty(B, T, nd * H, device=dev)
+        sv = torch.empty(B, T, nd, 4, H, device=dev)
+        dgi = torch.empty(B, T, nd * 3 * H, device=dev)
+        dgh = torch.empty_like(dgi)
+        dh0 = torch.empty(nd, B, H, device=dev)
+        if mc:
+            ws = torch.empty(int(_lib.load().b2p_gru_mc_workspace(B, H, nd)), device=dev, dtype=torch.uint8)
+            _lib.call("b2p_gru_fwd_mc", gi.data_ptr(), whh.data_ptr(), bhh.data_ptr(), h0.data_ptr(), out.data_ptr(),
+                      sv.data_ptr(), ws.data_ptr(), B, T, H, nd, _lib.stream_ptr())
+            f1 = ws[:4].clone()
+            _lib.call("b2p_gru_bwd_mc", dout.data_ptr(), whh.data_ptr(), out.data_ptr(), sv.data_ptr(), h0.data_ptr(),
+                      dgi.data_ptr(), dgh.data_ptr(), dh0.data_ptr(), ws.data_ptr(), B, T, H, nd, _lib.stream_ptr())
+            return out, sv, dgi, dgh, dh0, torch.cat([f1, ws[:4]])
+        buf = torch.empty(nd, B, H, device=dev)
+        _lib.call("b2p_gru_fwd", gi.data_ptr(), whh.data_ptr(), bhh.data_ptr(), h0.data_ptr(), out.data_ptr(),
+                  sv.data_ptr(), B, T, H, nd, _lib.stream_ptr())
+        _lib.call("b2p_gru_bwd", dout.data_ptr(), whh.data_ptr(), out.data_ptr(), sv.data_ptr(), h0.data_ptr(),
+                  dgi.data_ptr(), dgh.data_ptr(), dh0.data_ptr(), buf.data_ptr(), B, T, H, nd, _lib.stream_ptr())
+        return out, sv, dgi, dgh, dh0, None
+
+    ref = run(False)
+    got = run(True)
+    torch.cuda.synchronize()
+    assert int(got[5].abs().sum()) == 0, "a member timed out"
+    for a, r in zip(got[:5], ref[:5]):
+        assert _rel(a.cpu(), r.cpu()) < 2e-2
+    # graph replay: same results, every replay
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        run(True)
+    torch.cuda.current_stream().wait_stream(s)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        res = run(True)
+    for _ in range(3):
+        g.replay()
+        torch.cuda.synchronize()
+        assert int(res[5].abs().sum()) == 0
+        for a, b in zip(res[:5], got[:5]):
+            assert torch.equal(a, b)

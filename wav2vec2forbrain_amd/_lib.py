@@ -96,6 +96,10 @@ _SIGS = {
     "b2p_gru_lane_permute": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_i32, c_i32, c_u32, c_i32, c_p]),
     "b2p_gru_fwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_gru_bwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_gru_mc_supported": (c_i32, [c_i64]),
+    "b2p_gru_mc_workspace": (c_i64, [c_i64, c_i64, c_i32]),
+    "b2p_gru_fwd_mc": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_gru_bwd_mc": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_gru_hprev": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_attn16_fwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p, c_p]),
     "b2p_attn16_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p,

@@ -92,7 +92,11 @@ def _fp32_if(name: str):
 # accumulate into p.grad in the GEMM epilogue (beta = 1) instead of autograd's separate add.
 # join_wgrad() orders the side stream back into the main stream (train step, optimizer).
 _DIAG_SKIP_ACC = os.environ.get("B2P_DIAG_SKIP_SMALL_ACC") == "1"   # diagnostic only
-_PP_SPLIT = os.environ.get("B2P_PP_SPLIT", "0") == "1"   # measured no gain in the step (opt-in)
+_PP_SPLIT = os.environ.get("B2P_PP_SPLIT", "0") == "1"   # every eligible split-K GEMM on the ping-pong kernel
+# split-K GEMMs with at least this many outputs go to the 256 x 256 ping-pong kernel: the Conformer's
+# frozen weight gradients (4096 x 1024, 3072 x 1024; K = 7968 tokens) -8.6 ms per step; the base
+# model's (768 x 3072 and smaller) measured 0.2 ms slower on it, so they stay on the 128 x 128 split
+_PP_MIN_MN = int(os.environ.get("B2P_PP_MIN_MN", str(3 * 1024 * 1024)))
 
 
 class _Deferred:
@@ -395,7 +399,7 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
         ks = 1
         tpp = -(-M // 256) * -(-N // 256) * nz1 * nz2
         kpp = min(-(-160 // tpp), K // 1024)
-        if b16 and _PP_SPLIT and tpp * kpp >= 160 and kpp >= 2:
+        if b16 and (_PP_SPLIT or M * N * nz1 * nz2 >= _PP_MIN_MN) and tpp * kpp >= 160 and kpp >= 2:
             # 256x256 ping-pong tiles (gemm16.hip) over >= 1024-deep K slices, ~160-200 workgroups
             # (the frozen weight gradients, K = tokens): fewer, larger tiles than the 128 x 128 split
             ks = kpp
@@ -783,6 +787,13 @@ class Unfolded:
 
 # persistent MFMA recurrence in bf16 mode (B2P_GRU16=0 selects the per-step fp32 kernels, for A/B checks)
 _GRU16 = [os.environ.get("B2P_GRU16", "1") != "0"]
+# hidden sizes one CU cannot hold (Conformer H = 512): the multi-CU persistent kernels (csrc/grumc.hip)
+# in bf16 mode (B2P_GRUMC=0: per-step kernels, for A/B checks)
+_GRUMC = [os.environ.get("B2P_GRUMC", "1") != "0"]
+
+
+def _gru_mc_ws(B, H, ndir, dev):
+    return torch.empty(int(_lib.load().b2p_gru_mc_workspace(B, H, ndir)), device=dev, dtype=torch.uint8)
 
 
 def _ln_floats(B, T, H, ndir, R):
@@ -816,6 +827,7 @@ class _GRULayer(torch.autograd.Function):
         # bf16 mode: persistent MFMA recurrence (csrc/gru16.hip), which wants b_hh's r/z parts folded
         # into the input projection bias
         use16 = bf16_mode() and _GRU16[0] and bool(_lib.load().b2p_gru16_supported(H))
+        usemc = bf16_mode() and not use16 and _GRUMC[0] and bool(_lib.load().b2p_gru_mc_supported(H))
         if use16 and bhh[0] is not None:
             bih = [(b if b is not None else torch.zeros(G3, device=dev))
                    + torch.cat([bh[:2 * H], torch.zeros(H, device=dev)]) for b, bh in zip(bih, bhh)]
@@ -861,18 +873,22 @@ class _GRULayer(torch.autograd.Function):
                       _st())
             del giL
             _lib.call("b2p_gru_lane_permute", _p(hL), _p(out), B, T, H, ndir, 1, 1, 0x0, 0, _st())
+        elif usemc:
+            hL = None
+            _lib.call("b2p_gru_fwd_mc", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved),
+                      _p(_gru_mc_ws(B, H, ndir, dev)), B, T, H, ndir, _st())
         else:
             hL = None
             _lib.call("b2p_gru_fwd", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved), B, T, H, ndir,
                       _st())
         ctx.save_for_backward(x, out, saved, whh_s, h0, wperm, hL, U16, *wih)
-        ctx.meta = (unf_meta, H, ndir, B, T, IN, bih[0] is not None, bhh[0] is not None, use16)
+        ctx.meta = (unf_meta, H, ndir, B, T, IN, bih[0] is not None, bhh[0] is not None, use16, usemc)
         return out
 
     @staticmethod
     def backward(ctx, dout):
         x, out, saved, whh_s, h0, wperm, hL, U16, *wih = ctx.saved_tensors
-        unf_meta, H, ndir, B, T, IN, has_bih, has_bhh, use16 = ctx.meta
+        unf_meta, H, ndir, B, T, IN, has_bih, has_bhh, use16, usemc = ctx.meta
         dev = out.device
         dout = dout.contiguous()
         G3 = 3 * H
@@ -893,6 +909,13 @@ class _GRULayer(torch.autograd.Function):
             _lib.call("b2p_gru_lane_permute", _p(dgL), _p(dgi), B, T, H, ndir, 4, 3, 0xF210, 0, _st())
             _lib.call("b2p_gru_lane_permute", _p(dgL), _p(dgh), B, T, H, ndir, 4, 3, 0x2F10, 0, _st())
             del dgL
+        elif usemc:
+            ws = _gru_mc_ws(B, H, ndir, dev)
+            ev = torch.cuda.Event()
+            ev.record()
+            _lib.call("b2p_gru_bwd_mc", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi), _p(dgh), _p(dh0),
+                      _p(ws), B, T, H, ndir, _st())
+            flush_wgrad(ev)   # frozen-parameter gradient GEMMs beside the (H/64 x 4)-CU recurrence
         else:
             dhbuf = torch.empty(ndir, B, H, device=dev)
             ev = torch.cuda.Event()
