@@ -319,7 +319,8 @@ int b2p_gru_hprev(const float* out, const float* h0, float* hp, int64_t B, int64
  * granules. Same tensors and layouts as b2p_gru_fwd / b2p_gru_bwd (standard (B, T, ...) layouts);
  * bf16 MFMA operands, fp32 accumulation and state. workspace: b2p_gru_mc_workspace(B, H, ndir)
  * bytes, 16-byte aligned, zeroed by the call itself (the first int is a timeout flag: nonzero after
- * the call means a member never arrived). Needs (H/64) * ndir * ceil(B/16) co-resident CUs. */
+ * the call means a member never arrived; the second counts the recurrences whose members all ran
+ * on one XCD and exchanged through its L2). Needs (H/64) * ndir * ceil(B/16) co-resident CUs. */
 int b2p_gru_mc_supported(int64_t H);
 int64_t b2p_gru_mc_workspace(int64_t B, int64_t H, int ndir);
 int b2p_gru_fwd_mc(const float* gi, const float* whh, const float* bhh, const float* h0, float* out,

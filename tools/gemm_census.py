@@ -44,7 +44,8 @@ def report(out):
     f = glob.glob(os.path.join(out, "**", "*kernel_trace.csv"), recursive=True)[0]
     rows = list(csv.DictReader(open(f)))
     rows.sort(key=lambda r: int(r["Start_Timestamp"]))
-    gem = [r for r in rows if "gemm_kernel<" in r["Kernel_Name"] or "gemm16_kernel<" in r["Kernel_Name"]]
+    gem = [r for r in rows if "gemm_kernel<" in r["Kernel_Name"] or "gemm16_kernel<" in r["Kernel_Name"]
+           or "gemm16_pp_kernel<" in r["Kernel_Name"]]
     red = [r for r in rows if "splitk_reduce" in r["Kernel_Name"]]
     gem = gem[-len(log):]
     agg = {}

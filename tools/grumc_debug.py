@@ -30,6 +30,8 @@ for (B, T, H) in [(32, 249, 512), (33, 57, 512), (32, 249, 384)]:
                       sv.data_ptr(), ws.data_ptr(), B, T, H, nd, _lib.stream_ptr())
             _lib.call("b2p_gru_bwd_mc", dout.data_ptr(), whh.data_ptr(), out.data_ptr(), sv.data_ptr(), None,
                       dgi.data_ptr(), dgh.data_ptr(), None, ws.data_ptr(), B, T, H, nd, _lib.stream_ptr())
+            torch.cuda.synchronize()
+            HDR.append(ws[:8].view(torch.int32).tolist())
         else:
             buf = torch.empty(nd, B, H, device="cuda")
             _lib.call("b2p_gru_fwd", gi.data_ptr(), whh.data_ptr(), bhh.data_ptr(), None, out.data_ptr(),
@@ -39,8 +41,10 @@ for (B, T, H) in [(32, 249, 512), (33, 57, 512), (32, 249, 384)]:
         torch.cuda.synchronize()
         return out, sv, dgi, dgh
 
+    HDR = []
     ref = run(False)
     a = run(True)
     b = run(True)
-    print(B, T, H, "vs fp32 (maxrel, l2rel):", [rel(x, y) for x, y in zip(a, ref)],
+    hdr = HDR
+    print(B, T, H, "vs fp32 (maxrel, l2rel):", [rel(x, y) for x, y in zip(a, ref)], "hdr", hdr,
           "deterministic:", [bool(torch.equal(x, y)) for x, y in zip(a, b)], flush=True)

@@ -27,11 +27,23 @@ constexpr int BG = 16;        // batch rows per recurrence (MFMA N)
 constexpr int UPM = 64;       // hidden units per member
 constexpr int NTH = 256;      // 4 waves x 16 units
 constexpr unsigned SPIN_MAX = 1u << 22;
+constexpr int IDS_PER_GROUP = 16;   // members' XCC ids (P <= 16)
+constexpr int MAX_GROUPS = 32;      // (direction, 16-row batch group) recurrences per launch
+constexpr int64_t HDR_BYTES = 16 + (int64_t)MAX_GROUPS * IDS_PER_GROUP * 8;   // fail word + ids
 
 typedef __attribute__((address_space(1))) unsigned long long gu64;
 
-__device__ __forceinline__ void put_granule(unsigned long long* p, unsigned tag, unsigned v) {
-  __hip_atomic_store((gu64*)p, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+// Granule stores: sc1 (write-through to memory: visible to any XCD) or, when every member of the
+// recurrence runs on this XCD (checked at launch, see same_xcd), a workgroup-scope store (sc0: the
+// line stays in the XCD's L2, where the other members' sc1 loads read it, ~2x closer than memory).
+__device__ __forceinline__ void store_granule(unsigned long long* p, unsigned long long x, bool local) {
+  if (local)
+    __hip_atomic_store((gu64*)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  else
+    __hip_atomic_store((gu64*)p, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void put_granule(unsigned long long* p, unsigned tag, unsigned v, bool local) {
+  store_granule(p, ((unsigned long long)tag << 32) | v, local);
 }
 __device__ __forceinline__ unsigned long long get_granule(const unsigned long long* p) {
   return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -104,6 +116,41 @@ __device__ __forceinline__ bool place(int P, int ngroups, int& d, int& bg, int& 
   return m < P;
 }
 
+// Are all P members of this recurrence on one XCD? Each member publishes its XCC id once (sc1), every
+// member reads all of them; the answer is uniform across the group, so the group agrees on the store
+// flavour of every later granule. Placement is never assumed: any member elsewhere -> sc1 stores.
+__device__ __forceinline__ bool same_xcd(unsigned long long* ids, int P, int m, int* fail, bool& dead) {
+  __shared__ int all_same;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc &= 0xFu;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store((gu64*)(ids + m), (1ull << 32) | xcc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    all_same = 1;
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {   // one wave polls the P ids
+    unsigned long long x = 0;
+    bool ok = threadIdx.x >= P;
+    for (unsigned spins = 0; !__all(ok); ++spins) {
+      if (spins > SPIN_MAX) {
+        dead = true;
+        if (threadIdx.x == 0) __hip_atomic_store(fail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      if (!ok) {
+        x = get_granule(ids + threadIdx.x);
+        ok = (unsigned)(x >> 32) == 1u;
+      }
+    }
+    if (threadIdx.x < P && (unsigned)x != xcc) all_same = 0;
+  }
+  __syncthreads();
+  const bool same = all_same != 0 && !dead;
+  if (same && m == 0 && threadIdx.x == 0) atomicAdd(fail + 1, 1);   // diagnostic: groups on one XCD
+  return same;
+}
+
 // ------------------------------------------------------------------------------------------ forward
 // exchange slots: [group][2][P * 512] granules (h_s of member m, batch b, unit pair p at
 // m*512 + b*32 + p)
@@ -111,8 +158,8 @@ template <int H>
 __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi, const float* __restrict__ whh,
                                                     const float* __restrict__ bhh, const float* __restrict__ h0,
                                                     float* __restrict__ out, float* __restrict__ saved,
-                                                    unsigned long long* xch, int* fail, int B, int T, int ndir,
-                                                    int nbg) {
+                                                    unsigned long long* xch, unsigned long long* ids, int* fail, int B,
+                                                    int T, int ndir, int nbg) {
   constexpr int P = H / UPM;
   constexpr int KS = H / 32;
   constexpr int HPW = H / 2 + 4;              // u32 words per batch row of the h image (16-B stagger)
@@ -131,6 +178,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
   const float* W = whh + (int64_t)d * G3 * H;
   unsigned long long* xg = xch + (int64_t)(d * nbg + bg) * 2 * P * 512;
   bool dead = false;
+  const bool local = same_xcd(ids + (d * nbg + bg) * IDS_PER_GROUP, P, m, fail, dead);
 
   bf16x8 wf[3][KS];
 #pragma unroll
@@ -171,9 +219,9 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
 #pragma unroll
       for (int q = 0; q < 3; ++q) g[q] = *reinterpret_cast<const float4*>(gp + q * H);
   };
-  float4 gc[3], gx[3];
+  float4 gc[3];   // this step's input projection (the next step's is loaded into it once consumed)
 #pragma unroll
-  for (int q = 0; q < 3; ++q) gc[q] = gx[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int q = 0; q < 3; ++q) gc[q] = make_float4(0.f, 0.f, 0.f, 0.f);
   load_gi(0, gc);
   float st_h[4], st_r[4], st_z[4], st_n[4], st_g[4];   // this step's outputs
   auto store_out = [&](int s) {
@@ -187,7 +235,8 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
     *reinterpret_cast<float4*>(sv + 2 * H) = make_float4(st_n[0], st_n[1], st_n[2], st_n[3]);
     *reinterpret_cast<float4*>(sv + 3 * H) = make_float4(st_g[0], st_g[1], st_g[2], st_g[3]);
   };
-  auto step = [&](int s, float4 (&g)[3], float4 (&gn_next)[3]) {
+  for (int s = 0; s < T; ++s) {
+    float4 (&g)[3] = gc;
     if (s > 0) {   // h_{s-1} of every member: tags s, slot (s-1) & 1 -> image s & 1
       unsigned* img = hw + (s & 1) * BG * HPW;
       const unsigned tag = (unsigned)s;
@@ -227,19 +276,12 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
     // before it would delay it; then this step's outputs and the next step's input projection
     if (s + 1 < T) {
       unsigned long long* dst = xg + (s & 1) * P * 512 + m * 512 + lr * 32 + w * 8 + lq * 2;
-      put_granule(dst, (unsigned)(s + 1), pack2(hh[0], hh[1]));
-      put_granule(dst + 1, (unsigned)(s + 1), pack2(hh[2], hh[3]));
+      put_granule(dst, (unsigned)(s + 1), pack2(hh[0], hh[1]), local);
+      put_granule(dst + 1, (unsigned)(s + 1), pack2(hh[2], hh[3]), local);
     }
     store_out(s);
-    if (s + 1 < T) load_gi(s + 1, gn_next);
-  };
-  // unrolled by two with the input buffers swapped (no register copy of a pending load)
-  int s = 0;
-  for (; s + 1 < T; s += 2) {
-    step(s, gc, gx);
-    step(s + 1, gx, gc);
+    if (s + 1 < T) load_gi(s + 1, gc);
   }
-  if (s < T) step(s, gc, gx);
 }
 
 // ----------------------------------------------------------------------------------------- backward
@@ -260,8 +302,8 @@ __global__ void __launch_bounds__(NTH, 1) grumc_bwd(const float* __restrict__ do
                                                     const float* __restrict__ out, const float* __restrict__ saved,
                                                     const float* __restrict__ h0, float* __restrict__ dgi,
                                                     float* __restrict__ dgh, float* __restrict__ dh0,
-                                                    unsigned long long* xch, int* fail, int B, int T, int ndir,
-                                                    int nbg) {
+                                                    unsigned long long* xch, unsigned long long* ids, int* fail, int B,
+                                                    int T, int ndir, int nbg) {
   constexpr int P = H / UPM;
   constexpr int G3 = 3 * H;
   constexpr int KS = G3 / 32;                  // k-steps over all gate rows
@@ -280,6 +322,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_bwd(const float* __restrict__ do
   const float* W = whh + (int64_t)d * G3 * H;
   unsigned long long* xg = xch + (int64_t)(d * nbg + bg) * 2 * P * 1024;
   bool dead = false;
+  const bool local = same_xcd(ids + (d * nbg + bg) * IDS_PER_GROUP, P, m, fail, dead);
 
   // A = W^T in the interleaved k order: lane holds W[gate(k)*H + unit(k)][u0 + lr], k = 32s + 8lq + i
   bf16x8 wt[KS];
@@ -346,14 +389,18 @@ __global__ void __launch_bounds__(NTH, 1) grumc_bwd(const float* __restrict__ do
                  }
                }, fail, dead);
     __syncthreads();
-    f32x4 a = f32x4{0.f, 0.f, 0.f, 0.f};
+    // two independent accumulation chains (even / odd k-steps): the MFMA pipe never waits on the
+    // previous MFMA's result
+    f32x4 a0 = f32x4{0.f, 0.f, 0.f, 0.f}, a1 = a0;
     const uint16_t* grow = img + lr * GPH + 8 * lq;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      const bf16x8 bf = *reinterpret_cast<const bf16x8*>(grow + 32 * ks);
-      a = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[ks], bf, a, 0, 0, 0);
+    for (int ks = 0; ks < KS; ks += 2) {
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(grow + 32 * ks);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(grow + 32 * (ks + 1));
+      a0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[ks], b0, a0, 0, 0, 0);
+      a1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wt[ks + 1], b1, a1, 0, 0, 0);
     }
-    return a;
+    return f32x4{a0[0] + a1[0], a0[1] + a1[1], a0[2] + a1[2], a0[3] + a1[3]};
   };
   // one input buffer: step s-1's inputs are loaded once step s has consumed them (behind the publish,
   // so they overlap the other members' arrival)
@@ -381,8 +428,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_bwd(const float* __restrict__ do
       const unsigned tag = (unsigned)(s + 1);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        __hip_atomic_store((gu64*)(dst + i), dgh_granule(st_ar[i], st_az[i], st_an[i] * st_r[i], tag),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        store_granule(dst + i, dgh_granule(st_ar[i], st_az[i], st_an[i] * st_r[i], tag), local);
     }
     store_out(s);
     if (s > 0) load_in(s - 1, ic);
@@ -404,7 +450,7 @@ int grid_blocks(int P, int ngroups) { return ngroups <= 8 ? 8 * P : ngroups * P;
 
 template <int H>
 int launch_fwd(const float* gi, const float* whh, const float* bhh, const float* h0, float* out, float* saved,
-               unsigned long long* xch, int* fail, int B, int T, int ndir, hipStream_t st) {
+               unsigned long long* xch, unsigned long long* ids, int* fail, int B, int T, int ndir, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     B2P_CHECK_HIP(hipFuncSetAttribute((const void*)grumc_fwd<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -413,14 +459,15 @@ int launch_fwd(const float* gi, const float* whh, const float* bhh, const float*
   }
   const int nbg = (B + BG - 1) / BG;
   hipLaunchKernelGGL(grumc_fwd<H>, dim3(grid_blocks(H / UPM, ndir * nbg)), dim3(NTH), fwd_lds<H>(), st, gi, whh, bhh,
-                     h0, out, saved, xch, fail, B, T, ndir, nbg);
+                     h0, out, saved, xch, ids, fail, B, T, ndir, nbg);
   B2P_CHECK_LAUNCH();
   return 0;
 }
 
 template <int H>
 int launch_bwd(const float* dout, const float* whh, const float* out, const float* saved, const float* h0, float* dgi,
-               float* dgh, float* dh0, unsigned long long* xch, int* fail, int B, int T, int ndir, hipStream_t st) {
+               float* dgh, float* dh0, unsigned long long* xch, unsigned long long* ids, int* fail, int B, int T,
+               int ndir, hipStream_t st) {
   static bool attr = false;
   if (!attr) {
     B2P_CHECK_HIP(hipFuncSetAttribute((const void*)grumc_bwd<H>, hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -429,7 +476,7 @@ int launch_bwd(const float* dout, const float* whh, const float* out, const floa
   }
   const int nbg = (B + BG - 1) / BG;
   hipLaunchKernelGGL(grumc_bwd<H>, dim3(grid_blocks(H / UPM, ndir * nbg)), dim3(NTH), bwd_lds<H>(), st, dout, whh,
-                     out, saved, h0, dgi, dgh, dh0, xch, fail, B, T, ndir, nbg);
+                     out, saved, h0, dgi, dgh, dh0, xch, ids, fail, B, T, ndir, nbg);
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -448,10 +495,11 @@ extern "C" int b2p_gru_mc_supported(int64_t H) { return mc_supported(H) ? 1 : 0;
 extern "C" int64_t b2p_gru_mc_workspace(int64_t B, int64_t H, int ndir) {
   if (!mc_supported(H)) return 0;
   const int64_t nbg = (B + BG - 1) / BG, P = H / UPM;
-  return 16 + (int64_t)ndir * nbg * 2 * P * 1024 * 8;   // sized for the backward (2x the forward)
+  return HDR_BYTES + (int64_t)ndir * nbg * 2 * P * 1024 * 8;   // sized for the backward (2x the forward)
 }
 
-static int mc_prepare(void* ws, int64_t B, int64_t H, int ndir, hipStream_t st, unsigned long long** xch, int** fail) {
+static int mc_prepare(void* ws, int64_t B, int64_t H, int ndir, hipStream_t st, unsigned long long** xch,
+                      unsigned long long** ids, int** fail) {
   const int64_t bytes = b2p_gru_mc_workspace(B, H, ndir);
   // every polled word (tags) and the fail flag are zeroed before every launch, by a kernel (a node of
   // a captured graph, replayed first): granules of a previous launch never match this launch's tags.
@@ -462,7 +510,8 @@ static int mc_prepare(void* ws, int64_t B, int64_t H, int ndir, hipStream_t st, 
   hipLaunchKernelGGL(zero16_k, dim3((unsigned)(nb < 1024 ? nb : 1024)), dim3(256), 0, st, (uint4*)ws, n16);
   B2P_CHECK_LAUNCH();
   *fail = reinterpret_cast<int*>(ws);
-  *xch = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) + 16);
+  *ids = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) + 16);
+  *xch = reinterpret_cast<unsigned long long*>(reinterpret_cast<char*>(ws) + HDR_BYTES);
   return 0;
 }
 
@@ -475,14 +524,15 @@ extern "C" int b2p_gru_fwd_mc(const float* gi, const float* whh, const float* bh
   B2P_CHECK_ARG((((uintptr_t)workspace) & 15u) == 0, "gru_fwd_mc: workspace must be 16-byte aligned");
   if (B <= 0 || T <= 0) return 0;
   const int nbg = (int)((B + BG - 1) / BG);
-  B2P_CHECK_ARG(grid_blocks((int)(H / UPM), ndir * nbg) <= 256, "gru_fwd_mc: more recurrences than CUs");
+  B2P_CHECK_ARG(grid_blocks((int)(H / UPM), ndir * nbg) <= 256 && ndir * nbg <= MAX_GROUPS,
+                "gru_fwd_mc: more recurrences than CUs");
   hipStream_t st = (hipStream_t)stream;
-  unsigned long long* xch;
+  unsigned long long *xch, *ids;
   int* fail;
-  if (mc_prepare(workspace, B, H, ndir, st, &xch, &fail)) return 2;
-  if (H == 256) return launch_fwd<256>(gi, whh, bhh, h0, out, saved, xch, fail, (int)B, (int)T, ndir, st);
-  if (H == 384) return launch_fwd<384>(gi, whh, bhh, h0, out, saved, xch, fail, (int)B, (int)T, ndir, st);
-  return launch_fwd<512>(gi, whh, bhh, h0, out, saved, xch, fail, (int)B, (int)T, ndir, st);
+  if (mc_prepare(workspace, B, H, ndir, st, &xch, &ids, &fail)) return 2;
+  if (H == 256) return launch_fwd<256>(gi, whh, bhh, h0, out, saved, xch, ids, fail, (int)B, (int)T, ndir, st);
+  if (H == 384) return launch_fwd<384>(gi, whh, bhh, h0, out, saved, xch, ids, fail, (int)B, (int)T, ndir, st);
+  return launch_fwd<512>(gi, whh, bhh, h0, out, saved, xch, ids, fail, (int)B, (int)T, ndir, st);
 }
 
 extern "C" int b2p_gru_bwd_mc(const float* dout, const float* whh, const float* out, const float* saved,
@@ -494,12 +544,15 @@ extern "C" int b2p_gru_bwd_mc(const float* dout, const float* whh, const float* 
   B2P_CHECK_ARG((((uintptr_t)workspace) & 15u) == 0, "gru_bwd_mc: workspace must be 16-byte aligned");
   if (B <= 0 || T <= 0) return 0;
   const int nbg = (int)((B + BG - 1) / BG);
-  B2P_CHECK_ARG(grid_blocks((int)(H / UPM), ndir * nbg) <= 256, "gru_bwd_mc: more recurrences than CUs");
+  B2P_CHECK_ARG(grid_blocks((int)(H / UPM), ndir * nbg) <= 256 && ndir * nbg <= MAX_GROUPS,
+                "gru_bwd_mc: more recurrences than CUs");
   hipStream_t st = (hipStream_t)stream;
-  unsigned long long* xch;
+  unsigned long long *xch, *ids;
   int* fail;
-  if (mc_prepare(workspace, B, H, ndir, st, &xch, &fail)) return 2;
-  if (H == 256) return launch_bwd<256>(dout, whh, out, saved, h0, dgi, dgh, dh0, xch, fail, (int)B, (int)T, ndir, st);
-  if (H == 384) return launch_bwd<384>(dout, whh, out, saved, h0, dgi, dgh, dh0, xch, fail, (int)B, (int)T, ndir, st);
-  return launch_bwd<512>(dout, whh, out, saved, h0, dgi, dgh, dh0, xch, fail, (int)B, (int)T, ndir, st);
+  if (mc_prepare(workspace, B, H, ndir, st, &xch, &ids, &fail)) return 2;
+  if (H == 256)
+    return launch_bwd<256>(dout, whh, out, saved, h0, dgi, dgh, dh0, xch, ids, fail, (int)B, (int)T, ndir, st);
+  if (H == 384)
+    return launch_bwd<384>(dout, whh, out, saved, h0, dgi, dgh, dh0, xch, ids, fail, (int)B, (int)T, ndir, st);
+  return launch_bwd<512>(dout, whh, out, saved, h0, dgi, dgh, dh0, xch, ids, fail, (int)B, (int)T, ndir, st);
 }
