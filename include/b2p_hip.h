@@ -72,6 +72,7 @@ typedef struct {
 } b2p_operand;
 
 enum { B2P_ACT_NONE = 0, B2P_ACT_GELU = 1, B2P_ACT_SOFTSIGN = 2, B2P_ACT_SILU = 3 };
+enum { B2P_EPI_C16_FP16 = 1 };
 
 typedef struct {
   float* C;
@@ -86,7 +87,7 @@ typedef struct {
   const float* aux;           /* pre-activation for act_bwd                                    */
   int64_t ldaux, abs1, abs2;
   float drop_p;               /* dropout probability (0 = off); mask = f(drop_seed, index)     */
-  int32_t _pad0;
+  int32_t flags;              /* B2P_EPI_C16_FP16: C16 holds fp16 (not bf16) bits               */
   uint64_t drop_seed;
   const float* residual;      /* optional: added last                                          */
   int64_t ldr, rbs1, rbs2;
@@ -392,6 +393,27 @@ int b2p_accum_recs(const int64_t* recs, int ntensors, b2p_stream_t stream);
 /* dropout with an extra output scale: y = x * keep(seed, i) * scale / (1-p) (macaron half-step) */
 int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t seed, float scale,
                        b2p_stream_t stream);
+/* Output-dropout backward of a Conformer block in one pass (replaces b2p_dropout_scaled + a bf16
+ * cast + b2p_colsum of its result; reference TF conf Wav2Vec2ConformerFeedForward / SelfAttention /
+ * ConvolutionModule output dropout): y16 = bf16(mask(x) * scale / (1 - p)) over M x N (N % 4 == 0),
+ * and when part != NULL the per-256-row column partial sums of those fp32 values,
+ * part[b2p_drop_cast_colsum_parts(M)][N] (finish with b2p_colsum_parts). Same mask as
+ * b2p_dropout_scaled. */
+int64_t b2p_drop_cast_colsum_parts(int64_t M);
+int b2p_drop_cast_colsum(const float* x, uint16_t* y16, float* part, int64_t M, int64_t N, float p, uint64_t seed,
+                         float scale, b2p_stream_t stream);
+/* LayerNorm forward (TF conf / TF w2v nn.LayerNorm) writing the 16-bit GEMM operand copy y16 (fp16 when
+ * y16_fp16, else bf16); y (fp32) may be NULL. No dropout. */
+int b2p_layernorm_fwd_x16(const float* x, const float* gamma, const float* beta, float* y, uint16_t* y16, int y16_fp16,
+                          float* mean, float* rstd, int64_t rows, int64_t cols, float eps, b2p_stream_t stream);
+/* Forward rotary embedding (as b2p_rotary, inverse 0) written as a 16-bit operand (fp16 when fp16). */
+int b2p_rotary16(const float* x, const float* cos_t, const float* sin_t, uint16_t* out, int fp16, int64_t B, int64_t T,
+                 int64_t H, int64_t D, int64_t ld, b2p_stream_t stream);
+/* out = bf16(dropout(act(pre))) with the mask of a GEMM epilogue over the same flat index (n % 4 == 0):
+ * recomputes a Conformer FFN intermediate (TF conf Wav2Vec2ConformerFeedForward) for its weight
+ * gradient. */
+int b2p_act_dropout_cast16(const float* pre, uint16_t* out, int64_t n, int act, float p, uint64_t seed,
+                           b2p_stream_t stream);
 
 /* ------------------------------------------------------------------ Conformer
  * transformers Wav2Vec2Conformer{SelfAttention,ConvolutionModule,RotaryPositionalEmbedding}

@@ -689,3 +689,63 @@ def test_gru_mc_direct_and_graph_replay():
         assert int(res[5].abs().sum()) == 0
         for a, b in zip(res[:5], got[:5]):
             assert torch.equal(a, b)
+
+
+@pytest.mark.gpu
+def test_conformer_16bit_producers():
+    """The Conformer's 16-bit operand producers against torch fp32: LayerNorm with its fp16/bf16 copy,
+    rotary written as fp16/bf16, bf16(dropout(act(pre))) with the GEMM-epilogue mask, the fused
+    output-dropout backward (bf16 copy + column sums), and the GEMM epilogue's fp16 C16 flag."""
+    Fn = _fn()
+    from oracle.b2p2t_oracle import rotary_apply
+    torch.manual_seed(11)
+    M, D, nh = 300, 256, 4
+    dh = D // nh
+    x = torch.randn(M, D, device="cuda")
+    g, b = 1 + 0.1 * torch.randn(D, device="cuda"), 0.1 * torch.randn(D, device="cuda")
+    ref = F.layer_norm(x, (D,), g, b, 1e-5)
+    for half in (True, False):
+        y, y16, mean, rstd = Fn._ln_fwd_x16(x, g, b, 1e-5, half)
+        assert y16.dtype == (torch.float16 if half else torch.bfloat16)
+        assert _rel(y.cpu(), ref.cpu()) < 1e-5
+        assert torch.equal(y16, y.to(y16.dtype))        # the copy is the RNE rounding of y
+    # rotary16 == b2p_rotary (fp32) rounded
+    B, T = 3, 100
+    h = torch.randn(B * T, D, device="cuda")
+    cos_t, sin_t = Fn.rotary_tables(T, dh, 10000, "cuda")
+    r32 = rotary_apply(h.view(B, T, D).cpu(), nh, 10000).view(B * T, D)
+    for half in (True, False):
+        r16 = Fn._rotary16(h, cos_t, sin_t, B, T, nh, dh, half)
+        assert _rel(r16.float().cpu(), r32) < (1e-3 if half else 8e-3)
+    # act + dropout + bf16 cast with the epilogue's mask: compare with a GEMM whose epilogue applies
+    # the same act / dropout to x @ I (exact in fp32 operands)
+    K = 64
+    a = torch.randn(M, K, device="cuda")
+    eye = torch.eye(K, device="cuda")
+    pre = torch.empty(M, K, device="cuda")
+    fo = torch.empty(M, K, device="cuda")
+    seed = 1234
+    with Fn.precision("fp32"):
+        Fn.gemm(M, K, K, Fn.op(a, 0, K, True), Fn.op(eye, 0, K, True), fo, K, pre_out=pre, act=Fn.ACT["gelu"],
+                drop_p=0.1, seed=seed)
+    f16 = Fn._act_dropout_cast16(pre, Fn.ACT["gelu"], 0.1, seed)
+    assert torch.equal(f16, fo.to(torch.bfloat16))
+    # fused output-dropout backward: bf16(dropout(dy) * scale) and its column sums
+    dy = torch.randn(M, D, device="cuda")
+    ref32 = torch.empty_like(dy)
+    Fn._lib.call("b2p_dropout_scaled", dy.data_ptr(), ref32.data_ptr(), dy.numel(), 0.1, 77, 0.5, Fn._st())
+    y16, cs = Fn._drop_cast_colsum(dy, 0.1, 77, 0.5, True)
+    assert torch.equal(y16, ref32.to(torch.bfloat16))
+    assert _rel(cs.cpu(), ref32.sum(0).cpu()) < 1e-5
+    y16b, none = Fn._drop_cast_colsum(dy, 0.0, 0, 1.0, False)
+    assert none is None and torch.equal(y16b, dy.to(torch.bfloat16))
+    # GEMM epilogue writing C16 as fp16 (16-bit operands of both kinds)
+    N = 192
+    a16 = torch.randn(M, K, device="cuda").half()
+    w16 = torch.randn(N, K, device="cuda").half()
+    c32 = torch.empty(M, N, device="cuda")
+    c16 = torch.empty(M, N, device="cuda", dtype=torch.float16)
+    Fn.gemm(M, N, K, Fn.op(a16, 0, K, True), Fn.op(w16, 0, K, True), c32, N, C16=c16, c16_fp16=True)
+    refm = a16.float() @ w16.float().t()
+    assert _rel(c32.cpu(), refm.cpu()) < 1e-5
+    assert torch.equal(c16, c32.half())

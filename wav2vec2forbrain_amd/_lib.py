@@ -41,7 +41,7 @@ class Epilogue(ctypes.Structure):
         ("C", c_p), ("ldc", c_i64), ("cbs1", c_i64), ("cbs2", c_i64),
         ("alpha", c_f32), ("beta", c_f32), ("bias", c_p), ("biasbs1", c_i64), ("bias_gather", c_p), ("pre_out", c_p),
         ("act", c_i32), ("act_bwd", c_i32), ("aux", c_p), ("ldaux", c_i64), ("abs1", c_i64),
-        ("abs2", c_i64), ("drop_p", c_f32), ("_pad0", c_i32), ("drop_seed", c_u64),
+        ("abs2", c_i64), ("drop_p", c_f32), ("flags", c_i32), ("drop_seed", c_u64),
         ("residual", c_p), ("ldr", c_i64), ("rbs1", c_i64), ("rbs2", c_i64), ("C16", c_p),
         ("pre16", c_p), ("aux16", c_p), ("colsum_part", c_p),
     ]
@@ -120,6 +120,11 @@ _SIGS = {
     "b2p_posconv16_wgrad": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_seed_epoch_step": (c_i32, [c_p, c_p]),
     "b2p_dropout_scaled": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_f32, c_p]),
+    "b2p_drop_cast_colsum_parts": (c_i64, [c_i64]),
+    "b2p_drop_cast_colsum": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_f32, c_u64, c_f32, c_p]),
+    "b2p_layernorm_fwd_x16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_i64, c_i64, c_f32, c_p]),
+    "b2p_rotary16": (c_i32, [c_p, c_p, c_p, c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_p]),
+    "b2p_act_dropout_cast16": (c_i32, [c_p, c_p, c_i64, c_i32, c_f32, c_u64, c_p]),
     "b2p_rotary": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_glu_fwd": (c_i32, [c_p, c_p, c_i64, c_i64, c_p]),
     "b2p_glu_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_p]),
@@ -143,6 +148,7 @@ _SIGS = {
 
 # timing families (b2p_timing_*)
 TIMING_GEMM = 1
+EPI_C16_FP16 = 1   # b2p_epilogue.flags: C16 holds fp16 bits (include/b2p_hip.h B2P_EPI_C16_FP16)
 
 _lib = None
 

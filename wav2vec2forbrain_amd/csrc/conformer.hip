@@ -40,6 +40,54 @@ __global__ void rotary_k(const float* __restrict__ x, const float* __restrict__ 
   out[r * ld + (int64_t)h * D + d] = v;
 }
 
+// forward rotation written as a 16-bit GEMM operand (fp16 or bf16), 4 consecutive d per thread
+__global__ void rotary16_k(const float* __restrict__ x, const float* __restrict__ ct, const float* __restrict__ st,
+                           uint16_t* __restrict__ out, int64_t rows, int T, int H, int D, int64_t ld, int half16) {
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int D4 = D / 4;
+  if (i4 >= rows * H * D4) return;
+  const int d = (int)(i4 % D4) * 4;
+  const int h = (int)((i4 / D4) % H);
+  const int64_t r = i4 / ((int64_t)D4 * H);
+  const int t = (int)(r % T);
+  const float* xr = x + r * ld + (int64_t)h * D;
+  const int half = D / 2;
+  const float4 xv = *reinterpret_cast<const float4*>(xr + d);
+  const float4 ov = *reinterpret_cast<const float4*>(xr + (d < half ? d + half : d - half));
+  const float4 c = *reinterpret_cast<const float4*>(ct + (int64_t)t * D + d);
+  const float4 sn = *reinterpret_cast<const float4*>(st + (int64_t)t * D + d);
+  const float sg = d < half ? -1.f : 1.f;
+  float4 v;
+  v.x = xv.x * c.x + sg * ov.x * sn.x;
+  v.y = xv.y * c.y + sg * ov.y * sn.y;
+  v.z = xv.z * c.z + sg * ov.z * sn.z;
+  v.w = xv.w * c.w + sg * ov.w * sn.w;
+  *reinterpret_cast<uint2*>(out + r * ld + (int64_t)h * D + d) = b2p_pack16x4(v, half16 != 0);
+}
+
+// bf16(dropout(act(pre))): the FFN intermediate recomputed from its fp32 pre-activation for the
+// backward weight gradient (the forward GEMM epilogue wrote only the fp16 operand copy); same mask
+// index (flat element index) and scale as that epilogue. 4 elements per thread.
+__global__ void act_drop_cast16_k(const float* __restrict__ pre, uint16_t* __restrict__ out, int64_t n4, int act,
+                                  uint32_t thr, float scale, uint64_t seed, int use_mask,
+                                  const uint64_t* __restrict__ epoch) {
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 >= n4) return;
+  seed = b2p_seed_eff(seed, epoch);
+  const float4 p = reinterpret_cast<const float4*>(pre)[i4];
+  float v[4] = {p.x, p.y, p.z, p.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    float a = v[q];
+    if (act == B2P_ACT_GELU) a = b2p_gelu(a);
+    else if (act == B2P_ACT_SILU) a = b2p_silu(a);
+    else if (act == B2P_ACT_SOFTSIGN) a = a / (1.0f + fabsf(a));
+    if (use_mask) a = b2p_keep(seed, (uint64_t)(4 * i4 + q), thr) ? a * scale : 0.f;
+    v[q] = a;
+  }
+  reinterpret_cast<uint2*>(out)[i4] = b2p_pack_bf16x4(make_float4(v[0], v[1], v[2], v[3]));
+}
+
 __global__ void glu_fwd_k(const float* __restrict__ a, float* __restrict__ out, int64_t M, int64_t C) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M * C) return;
@@ -257,6 +305,53 @@ __global__ void dropout_scale_k(const float* __restrict__ x, float* __restrict__
   seed = b2p_seed_eff(seed, epoch);
   y[i] = (!use_mask || b2p_keep(seed, (uint64_t)i, thr)) ? x[i] * scale : 0.f;
 }
+
+// y16 = bf16(mask(x) * scale) over an M x N row-major tensor (N % 4 == 0, 16-B aligned rows), plus
+// optional per-256-row column partial sums of the fp32 values, part[blk][n] (the bias gradient of
+// the Linear that produced x; b2p_colsum_parts finishes it): the output-dropout backward of a
+// Conformer block (dropout, its bf16 GEMM operand and its bias gradient in one pass over dy).
+// Grid (ceil(N/128), ceil(M/256)); 32 float4 columns x 8 row lanes per block; mask index = m*N + n,
+// the element index dropout_scale_k and the forward GEMM epilogue use.
+__global__ void __launch_bounds__(256) drop_cast_colsum_k(const float* __restrict__ x, uint16_t* __restrict__ y16,
+                                                          float* __restrict__ part, int64_t M, int64_t N, uint32_t thr,
+                                                          float scale, uint64_t seed, int use_mask,
+                                                          const uint64_t* __restrict__ epoch) {
+  __shared__ float4 red[8][32];
+  const int c4 = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int64_t n = (int64_t)blockIdx.x * 128 + 4 * c4;
+  const int64_t m0 = (int64_t)blockIdx.y * 256;
+  const int64_t m1 = m0 + 256 < M ? m0 + 256 : M;
+  seed = b2p_seed_eff(seed, epoch);
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n < N) {
+#pragma unroll 4
+    for (int64_t m = m0 + rl; m < m1; m += 8) {
+      const int64_t i = m * N + n;
+      float4 v = *reinterpret_cast<const float4*>(x + i);
+      v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
+      if (use_mask) {
+        if (!b2p_keep(seed, (uint64_t)i, thr)) v.x = 0.f;
+        if (!b2p_keep(seed, (uint64_t)i + 1, thr)) v.y = 0.f;
+        if (!b2p_keep(seed, (uint64_t)i + 2, thr)) v.z = 0.f;
+        if (!b2p_keep(seed, (uint64_t)i + 3, thr)) v.w = 0.f;
+      }
+      *reinterpret_cast<uint2*>(y16 + i) = b2p_pack_bf16x4(v);
+      s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+    }
+  }
+  if (!part) return;
+  red[rl][c4] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    float4 t = red[0][c4];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) {
+      const float4 u = red[r][c4];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    *reinterpret_cast<float4*>(part + (int64_t)blockIdx.y * N + n) = t;
+  }
+}
 }  // namespace
 
 extern "C" int b2p_rotary(const float* x, const float* cos_t, const float* sin_t, float* out, int64_t B, int64_t T,
@@ -464,6 +559,51 @@ extern "C" int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, 
   if (n <= 0) return 0;
   hipLaunchKernelGGL(dropout_scale_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, y, n,
                      b2p_dropout_threshold(p), p > 0.f ? scale / (1.f - p) : scale, seed, p > 0.f ? 1 : 0,
+                     b2p_seed_epoch());
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int64_t b2p_drop_cast_colsum_parts(int64_t M) { return M > 0 ? (M + 255) / 256 : 0; }
+
+extern "C" int b2p_drop_cast_colsum(const float* x, uint16_t* y16, float* part, int64_t M, int64_t N, float p,
+                                    uint64_t seed, float scale, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && y16, "drop_cast_colsum: NULL");
+  B2P_CHECK_ARG(p >= 0.f && p < 1.f, "drop_cast_colsum: p in [0,1)");
+  B2P_CHECK_ARG(N % 4 == 0 && ((uintptr_t)x & 15u) == 0 && ((uintptr_t)y16 & 7u) == 0 &&
+                    ((uintptr_t)part & 15u) == 0,
+                "drop_cast_colsum: needs N % 4 == 0, 16-B aligned x / part, 8-B aligned y16");
+  if (M <= 0 || N <= 0) return 0;
+  const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 255) / 256));
+  hipLaunchKernelGGL(drop_cast_colsum_k, grid, dim3(256), 0, (hipStream_t)stream, x, y16, part, M, N,
+                     b2p_dropout_threshold(p), p > 0.f ? scale / (1.f - p) : scale, seed, p > 0.f ? 1 : 0,
+                     b2p_seed_epoch());
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_rotary16(const float* x, const float* cos_t, const float* sin_t, uint16_t* out, int fp16, int64_t B,
+                            int64_t T, int64_t H, int64_t D, int64_t ld, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && cos_t && sin_t && out, "rotary16: NULL pointer");
+  B2P_CHECK_ARG(D % 8 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15u) == 0 && ((uintptr_t)out & 7u) == 0,
+                "rotary16: head dim must be a multiple of 8 and rows 16-B aligned");
+  const int64_t n4 = B * T * H * (D / 4);
+  if (n4 <= 0) return 0;
+  hipLaunchKernelGGL(rotary16_k, dim3(nblk(n4)), dim3(256), 0, (hipStream_t)stream, x, cos_t, sin_t, out, B * T,
+                     (int)T, (int)H, (int)D, ld, fp16);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_act_dropout_cast16(const float* pre, uint16_t* out, int64_t n, int act, float p, uint64_t seed,
+                                      b2p_stream_t stream) {
+  B2P_CHECK_ARG(pre && out, "act_dropout_cast16: NULL pointer");
+  B2P_CHECK_ARG(p >= 0.f && p < 1.f, "act_dropout_cast16: p in [0,1)");
+  B2P_CHECK_ARG(n % 4 == 0 && ((uintptr_t)pre & 15u) == 0 && ((uintptr_t)out & 7u) == 0,
+                "act_dropout_cast16: n % 4 == 0 and aligned pointers required");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(act_drop_cast16_k, dim3(nblk(n / 4)), dim3(256), 0, (hipStream_t)stream, pre, out, n / 4, act,
+                     b2p_dropout_threshold(p), p > 0.f ? 1.f / (1.f - p) : 1.f, seed, p > 0.f ? 1 : 0,
                      b2p_seed_epoch());
   B2P_CHECK_LAUNCH();
   return 0;

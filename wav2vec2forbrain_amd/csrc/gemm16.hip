@@ -233,6 +233,23 @@ __device__ __forceinline__ void store_colsum(const EpiArgs& ea, float* Cs, int t
   }
 }
 
+// output tile of linear tile index t: row-major (grp = 0), or grouped (grp > 0): column sweeps over
+// bands of grp row tiles, so the workgroups resident on one XCD at a time share a few A row panels
+// and a few B column panels in that XCD's L2 instead of cycling through all of B
+__device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int grp, int& tm, int& tn) {
+  if (grp > 0) {
+    const int per = grp * tiles_n;
+    const int g = t / per, first = g * grp;
+    const int gs = tiles_m - first < grp ? tiles_m - first : grp;
+    const int r = t - g * per;
+    tn = r / gs;
+    tm = first + (r - tn * gs);
+  } else {
+    tm = t / tiles_n;
+    tn = t - tm * tiles_n;
+  }
+}
+
 // Tile configurations: BM x BN output tile, WGM x WGN waves of 64 x 64 each (4 x 4 MFMA tiles),
 // KT-deep k-tiles, S LDS stages (S-1 tiles in flight behind counted vmcnt waits + raw barriers).
 template <int BM_, int BN_, int KT_, int S_>
@@ -248,6 +265,7 @@ struct Cfg {
 };
 using CfgSmall = Cfg<128, 128, 32, 3>;   // 4 waves, 2 workgroups/CU (default)
 using CfgSmall64 = Cfg<128, 128, 64, 2>; // 4 waves, 2 workgroups/CU, half the barriers (small grids)
+using CfgSmall4 = Cfg<128, 128, 32, 4>; // 4 waves, 2 workgroups/CU, 3 k-tiles in flight (B2P_GEMM16_S4=1)
 using CfgBig = Cfg<256, 128, 64, 3>;     // 8 waves, 1 workgroup/CU (measured slower on the step's shapes:
                                          // lock-stepped waves leave the MFMA pipe idle at every barrier)
 
@@ -255,7 +273,7 @@ using CfgBig = Cfg<256, 128, 64, 3>;     // 8 waves, 1 workgroup/CU (measured sl
 // data movement is the same 16-bit copy either way
 template <class CF, bool AK, bool BK, bool ACONV, bool H16 = false>
 __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_desc d, const EpiArgs ea, int tiles_m,
-                                                                int tiles_n) {
+                                                                int tiles_n, int grp) {
   constexpr int BM = CF::BM, BN = CF::BN, KT = CF::KT, S = CF::S, NT = CF::NT;
   constexpr int A_BYTES = BM * KT * 2;
   constexpr int STAGE_BYTES = CF::STAGE;
@@ -278,7 +296,8 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_
   const int tiles = tiles_m * tiles_n;
   const int zz = wgid / tiles;
   const int t = wgid - zz * tiles;
-  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  int tm, tn;
+  tile_of(t, tiles_m, tiles_n, grp, tm, tn);
 
   const int ks = d.ksplit > 1 ? d.ksplit : 1;
   const int z = zz / ks, ksl = zz - z * ks;
@@ -416,7 +435,7 @@ __device__ __forceinline__ void pp_lgkm0() {
 
 template <bool AK, bool BK>
 __global__ void __launch_bounds__(PP_NT, 1) gemm16_pp_kernel(const b2p_gemm_desc d, const EpiArgs ea, int tiles_m,
-                                                            int tiles_n) {
+                                                            int tiles_n, int grp) {
   using SA = Src<256, PP_KT, AK, false, 8>;
   using SB = Src<256, PP_KT, BK, false, 8>;
   __shared__ __attribute__((aligned(1024))) char smem[PP_LDS];
@@ -433,7 +452,8 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm16_pp_kernel(const b2p_gemm_desc
   const int tiles = tiles_m * tiles_n;
   const int zz = wgid / tiles;
   const int t = wgid - zz * tiles;
-  const int tm = t / tiles_n, tn = t - tm * tiles_n;
+  int tm, tn;
+  tile_of(t, tiles_m, tiles_n, grp, tm, tn);
 
   const int ks = d.ksplit > 1 ? d.ksplit : 1;
   const int z = zz / ks, ksl = zz - z * ks;
@@ -569,24 +589,31 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm16_pp_kernel(const b2p_gemm_desc
 
 }  // namespace
 
+// row-tile band of the grouped tile order (tile_of); B2P_GEMM16_GROUP / B2P_GEMM16_GROUP_PP override
+static int gemm16_group(bool pp) {
+  static const int g_small = getenv("B2P_GEMM16_GROUP") ? atoi(getenv("B2P_GEMM16_GROUP")) : 0;
+  static const int g_pp = getenv("B2P_GEMM16_GROUP_PP") ? atoi(getenv("B2P_GEMM16_GROUP_PP")) : 0;
+  return pp ? g_pp : g_small;
+}
+
 template <class CF>
 static void launch_cfg(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st, dim3 grid, int tm, int tn) {
   const dim3 block(CF::NT);
   const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
   if (d.A.dtype == 2) {   // fp16 operands (precision 2): plain operand pairs only
-    if (AK && BK) hipLaunchKernelGGL((gemm16_kernel<CF, true, true, false, true>), grid, block, 0, st, d, ea, tm, tn);
-    else if (AK) hipLaunchKernelGGL((gemm16_kernel<CF, true, false, false, true>), grid, block, 0, st, d, ea, tm, tn);
-    else hipLaunchKernelGGL((gemm16_kernel<CF, false, false, false, true>), grid, block, 0, st, d, ea, tm, tn);
+    if (AK && BK) hipLaunchKernelGGL((gemm16_kernel<CF, true, true, false, true>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(false));
+    else if (AK) hipLaunchKernelGGL((gemm16_kernel<CF, true, false, false, true>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(false));
+    else hipLaunchKernelGGL((gemm16_kernel<CF, false, false, false, true>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(false));
     return;
   }
   if (AK && BK) {
-    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<CF, true, true, true>), grid, block, 0, st, d, ea, tm, tn);
-    else hipLaunchKernelGGL((gemm16_kernel<CF, true, true, false>), grid, block, 0, st, d, ea, tm, tn);
+    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<CF, true, true, true>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(false));
+    else hipLaunchKernelGGL((gemm16_kernel<CF, true, true, false>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(false));
   } else if (AK && !BK) {
-    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<CF, true, false, true>), grid, block, 0, st, d, ea, tm, tn);
-    else hipLaunchKernelGGL((gemm16_kernel<CF, true, false, false>), grid, block, 0, st, d, ea, tm, tn);
+    if (d.A.conv) hipLaunchKernelGGL((gemm16_kernel<CF, true, false, true>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(false));
+    else hipLaunchKernelGGL((gemm16_kernel<CF, true, false, false>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(false));
   } else {
-    hipLaunchKernelGGL((gemm16_kernel<CF, false, false, false>), grid, block, 0, st, d, ea, tm, tn);
+    hipLaunchKernelGGL((gemm16_kernel<CF, false, false, false>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(false));
   }
 }
 
@@ -626,9 +653,9 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
     const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 255) / 256);
     const dim3 grid((unsigned)tiles_pp), block(PP_NT);
     const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
-    if (AK && BK) hipLaunchKernelGGL((gemm16_pp_kernel<true, true>), grid, block, 0, st, d, ea, tm, tn);
-    else if (AK) hipLaunchKernelGGL((gemm16_pp_kernel<true, false>), grid, block, 0, st, d, ea, tm, tn);
-    else hipLaunchKernelGGL((gemm16_pp_kernel<false, false>), grid, block, 0, st, d, ea, tm, tn);
+    if (AK && BK) hipLaunchKernelGGL((gemm16_pp_kernel<true, true>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(true));
+    else if (AK) hipLaunchKernelGGL((gemm16_pp_kernel<true, false>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(true));
+    else hipLaunchKernelGGL((gemm16_pp_kernel<false, false>), grid, block, 0, st, d, ea, tm, tn, gemm16_group(true));
     return 0;
   }
   const int tm = (int)((d.M + 127) / 128), tn = (int)((d.N + 127) / 128);
@@ -646,7 +673,9 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   // replay, side stream beside): B2P_GEMM16_K64 = 0 never (default), 1 always, -1 by grid size.
   static int k64 = getenv("B2P_GEMM16_K64") ? atoi(getenv("B2P_GEMM16_K64")) : 0;
   const bool use64 = k64 == 1 || (k64 < 0 && nwg <= 512);
+  static int s4 = getenv("B2P_GEMM16_S4") ? atoi(getenv("B2P_GEMM16_S4")) : 0;
   if (use64 && !h16 && (ks == 1 || d.kchunk % 64 == 0)) launch_cfg<CfgSmall64>(d, ea, st, dim3((unsigned)nwg), tm, tn);
+  else if (s4) launch_cfg<CfgSmall4>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   else launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   return 0;
 }

@@ -52,7 +52,7 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, 
   }
   if (e.residual) v += e.residual[(int64_t)z1 * e.rbs1 + (int64_t)z2 * e.rbs2 + (int64_t)m * e.ldr + n];
   if (e.C) e.C[coff] = v;
-  if (e.C16) e.C16[coff] = b2p_bf16_bits(v);
+  if (e.C16) e.C16[coff] = b2p_16_bits(v, e.flags & B2P_EPI_C16_FP16);
 }
 
 // Four consecutive columns n .. n+3 of row m (n % 4 == 0), vectorised when ea.vec4 is set.
@@ -109,11 +109,8 @@ __device__ __forceinline__ float4 epilogue_store4(const EpiArgs& a, int z, int z
     v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
   }
   if (e.C) *reinterpret_cast<float4*>(e.C + coff) = make_float4(v[0], v[1], v[2], v[3]);
-  if (e.C16) {
-    const uint32_t lo = (uint32_t)b2p_bf16_bits(v[0]) | ((uint32_t)b2p_bf16_bits(v[1]) << 16);
-    const uint32_t hi = (uint32_t)b2p_bf16_bits(v[2]) | ((uint32_t)b2p_bf16_bits(v[3]) << 16);
-    *reinterpret_cast<uint2*>(e.C16 + coff) = make_uint2(lo, hi);
-  }
+  if (e.C16) *reinterpret_cast<uint2*>(e.C16 + coff) = b2p_pack16x4(make_float4(v[0], v[1], v[2], v[3]),
+                                                                       e.flags & B2P_EPI_C16_FP16);
   return make_float4(v[0], v[1], v[2], v[3]);
 }
 
@@ -133,7 +130,7 @@ __global__ void splitk_reduce(const float* __restrict__ ws, int ks, int64_t M, i
   float v = e.alpha * s;
   if (e.beta != 0.f) v += e.beta * e.C[coff];
   if (e.C) e.C[coff] = v;
-  if (e.C16) e.C16[coff] = b2p_bf16_bits(v);
+  if (e.C16) e.C16[coff] = b2p_16_bits(v, e.flags & B2P_EPI_C16_FP16);
 }
 
 

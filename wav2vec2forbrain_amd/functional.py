@@ -139,6 +139,18 @@ def _defer_acc(p, g) -> None:
     _Deferred.accs.append((p, g))
 
 
+def _defer_small(prms, grads):
+    """Small gradients of frozen parameters (LayerNorm / bias / BatchNorm / depthwise taps) queued for
+    the side stream's one multi-tensor accumulation instead of one autograd add launch each; the
+    returned list has None where a gradient was taken over."""
+    out = list(grads)
+    for k, (p, g) in enumerate(zip(prms, grads)):
+        if g is not None and _defer_ok(p):
+            _defer_acc(p, g)
+            out[k] = None
+    return out
+
+
 def _flush_accs(sd) -> None:
     """The queued small-gradient accumulations on side stream sd: a parameter without .grad takes
     the tensor itself, the rest are batched into b2p_accum_recs records {p.grad, g, numel}."""
@@ -330,7 +342,9 @@ def op(t, off=0, ld=0, k_inner=True, bs1=0, bs2=0, gather=None):
     o.gather1 = None if gather is None else gather.data_ptr()
     o.inner_is_k = 1 if k_inner else 0
     o.conv = 0
-    o.dtype = 1 if isinstance(t, torch.Tensor) and t.dtype == torch.bfloat16 else 0
+    o.dtype = 0
+    if isinstance(t, torch.Tensor):
+        o.dtype = 1 if t.dtype == torch.bfloat16 else (2 if t.dtype == torch.float16 else 0)
     return o
 
 
@@ -349,7 +363,7 @@ def conv_op(t, off, ld, T_out, T_in, stride, pad, Cg, sample_stride, k_inner=Tru
 def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1, nz2=1, alpha=1.0,
          beta=0.0, bias=None, biasbs1=0, bias_gather=None, pre_out=None, act=0, act_bwd=0, aux=None, ldaux=0, abs1=0, abs2=0,
          drop_p=0.0, seed=0, residual=None, r_off=0, ldr=0, rbs1=0, rbs2=0, timing=0, C16=None, pre16=None,
-         aux16=None, colsum_part=None):
+         aux16=None, colsum_part=None, c16_fp16=False):
     """C may be None when only the bf16 copy C16 (same strides) is wanted. Both operands bf16
     (Operand.dtype 1) selects the LDS-DMA kernel (gemm16.hip)."""
     d = GemmDesc()
@@ -376,8 +390,9 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     e.pre16 = _p(pre16, c_off) if pre16 is not None else None
     e.aux16 = _p(aux16, c_off) if aux16 is not None else None
     e.colsum_part = _p(colsum_part)
+    e.flags = _lib.EPI_C16_FP16 if c16_fp16 else 0
     d.ep = e
-    d.precision = 2 if (_state.fwd16 and _state.prec == 0 and A.dtype == 0) else _prec()
+    d.precision = 2 if ((_state.fwd16 and _state.prec == 0 and A.dtype == 0) or A.dtype == 2) else _prec()
     keep16 = None
     if _AUTO16 and _state.prec == 0 and A.dtype == 0 and B.dtype == 0 and _auto16_ok(M, N, K, A, B, nz1, nz2):
         # fp32 operands of a large plain GEMM: stage 16-bit copies (the rounding the fp32-operand
@@ -1704,12 +1719,14 @@ class _LayerNorm(torch.autograd.Function):
         x2 = x.view(-1, C)
         y, mean, rstd = _ln_fwd(x2, g, b, eps)
         ctx.save_for_backward(x2, g, mean, rstd)
+        ctx.prm = (g, b)
         return y.view(x.shape)
 
     @staticmethod
     def backward(ctx, dy):
         x2, g, mean, rstd = ctx.saved_tensors
         dx, dg, db, _ = _ln_bwd(dy.contiguous().view(x2.shape), x2, g, mean, rstd)
+        dg, db = _defer_small(ctx.prm, (dg, db))
         return dx.view(dy.shape), dg, db, None
 
 
@@ -1723,6 +1740,53 @@ def _dropout_scaled(x, p, seed, scale):
     return y
 
 
+def _drop_cast_colsum(dy, p, seed, scale, want_colsum):
+    """(bf16(dropout(dy) * scale), its column sums or None) in one pass over dy (M x N, fp32)."""
+    M, N = dy.shape
+    y16 = torch.empty(M, N, device=dy.device, dtype=BF16)
+    parts = None
+    if want_colsum:
+        parts = torch.empty(int(_lib.load().b2p_drop_cast_colsum_parts(M)), N, device=dy.device)
+    _lib.call("b2p_drop_cast_colsum", _p(dy), _p(y16), _p(parts), M, N, float(p), seed, float(scale), _st())
+    return y16, (colsum_from_parts(parts, torch.empty(N, device=dy.device)) if want_colsum else None)
+
+
+def _ln_fwd_x16(x2d, g, b, eps, half):
+    """LayerNorm (fp32 y, mean, rstd) plus its 16-bit GEMM operand copy (fp16 when half) in one pass."""
+    rows, cols = x2d.shape
+    y = torch.empty_like(x2d)
+    y16 = torch.empty(rows, cols, device=x2d.device, dtype=torch.float16 if half else BF16)
+    mean = torch.empty(rows, device=x2d.device)
+    rstd = torch.empty(rows, device=x2d.device)
+    _lib.call("b2p_layernorm_fwd_x16", _p(x2d), _p(g), _p(b), _p(y), _p(y16), int(half), _p(mean), _p(rstd), rows,
+              cols, float(eps), _st())
+    return y, y16, mean, rstd
+
+
+def _rotary16(h, cos_t, sin_t, B, T, nh, hd, half):
+    out = torch.empty(h.shape, device=h.device, dtype=torch.float16 if half else BF16)
+    _lib.call("b2p_rotary16", _p(h), _p(cos_t), _p(sin_t), _p(out), int(half), B, T, nh, hd, h.shape[-1], _st())
+    return out
+
+
+def _w_op16(w, half):
+    """(buffer, Operand) of a Linear / pointwise-conv weight [N][K...] as a 16-bit k-contiguous B operand:
+    fp16 (the forward_f16 precision; frozen copies cached by _cast_operand) or bf16 (weight16). Keep the
+    buffer alive until the GEMM is enqueued."""
+    N = w.shape[0]
+    K = w.numel() // N
+    if half:
+        return _cast_operand(op(w, 0, K, True), N, K, True, w.device)
+    w16 = weight16(w)
+    return w16, op(w16, 0, K, True)
+
+
+def _act_dropout_cast16(pre, act, p, seed):
+    out = torch.empty(pre.shape, device=pre.device, dtype=BF16)
+    _lib.call("b2p_act_dropout_cast16", _p(pre), _p(out), pre.numel(), act, float(p), seed, _st())
+    return out
+
+
 class _FFNBlock(torch.autograd.Function):
     """y = x + scale * dropout_h(W2 dropout_a(act(W1 LN(x) + b1)) + b2)   (macaron half-step, scale 0.5)"""
 
@@ -1734,19 +1798,36 @@ class _FFNBlock(torch.autograd.Function):
         NT, F = B * T, w1.shape[0]
         dev = x.device
         x2 = x.view(NT, D)
-        h, mean, rstd = _ln_fwd(x2, g, b, eps)
-        pre = torch.empty(NT, F, device=dev)
-        f = torch.empty(NT, F, device=dev)
-        gemm(NT, F, D, op(h, 0, D, True), op(w1, 0, D, True), f, F, bias=b1, pre_out=pre, act=act, drop_p=p_act,
-             seed=s_act)
         bs = b2 * scale if b2 is not None else None
         y = torch.empty(NT, D, device=dev)
-        gemm(NT, D, F, op(f, 0, F, True), op(w2, 0, F, True), y, D, alpha=scale, bias=bs, drop_p=p_hid, seed=s_hid,
-             residual=x2)
+        pre = torch.empty(NT, F, device=dev)
+        if bf16_mode():
+            # 16-bit operands written by their producers (LayerNorm, FFN1 epilogue): no cast passes;
+            # fp16 under forward_f16, else bf16. f exists only as that operand copy (the backward
+            # recomputes its bf16 form from pre)
+            half = _state.fwd16
+            h, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half)
+            f = torch.empty(NT, F, device=dev, dtype=torch.float16 if half else BF16)
+            w1b, w1op = _w_op16(w1, half)
+            gemm(NT, F, D, op(h16, 0, D, True), w1op, None, F, bias=b1, pre_out=pre, act=act, drop_p=p_act,
+                 seed=s_act, C16=f, c16_fp16=half)
+            del h16, w1b
+            w2b, w2op = _w_op16(w2, half)
+            gemm(NT, D, F, op(f, 0, F, True), w2op, y, D, alpha=scale, bias=bs, drop_p=p_hid, seed=s_hid,
+                 residual=x2)
+            del w2b
+        else:
+            h, mean, rstd = _ln_fwd(x2, g, b, eps)
+            f = torch.empty(NT, F, device=dev)
+            gemm(NT, F, D, op(h, 0, D, True), op(w1, 0, D, True), f, F, bias=b1, pre_out=pre, act=act, drop_p=p_act,
+                 seed=s_act)
+            gemm(NT, D, F, op(f, 0, F, True), op(w2, 0, F, True), y, D, alpha=scale, bias=bs, drop_p=p_hid,
+                 seed=s_hid, residual=x2)
         ctx.save_for_backward(x2, h, mean, rstd, pre, f, g, w1, w2)
         ctx.cfg = cfg
         ctx.shape = (B, T, D)
         ctx.has_b = (b1 is not None, b2 is not None)
+        ctx.prm = (g, b, w1, b1, w2, b2)
         return y.view(B, T, D)
 
     @staticmethod
@@ -1758,9 +1839,9 @@ class _FFNBlock(torch.autograd.Function):
         dev = x2.device
         ng = ctx.needs_input_grad
         dy = dy.contiguous().view(NT, D)
-        dz = _dropout_scaled(dy, p_hid, s_hid, scale)
         if bf16_mode():
-            return _FFNBlock._backward16(ctx, dy, dz, x2, h, mean, rstd, pre, f, g, w1, w2)
+            return _FFNBlock._backward16(ctx, dy, x2, h, mean, rstd, pre, f, g, w1, w2)
+        dz = _dropout_scaled(dy, p_hid, s_hid, scale)
         dw2 = db2 = dw1 = db1 = None
         if ng[5]:
             dw2 = torch.empty_like(w2)
@@ -1780,24 +1861,24 @@ class _FFNBlock(torch.autograd.Function):
         dh = torch.empty(NT, D, device=dev)
         mm_nn(dpre, w1, dh)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
-        return dx.view(ctx.shape), dg, db, dw1, db1, dw2, db2, None
+        return (dx.view(ctx.shape), *_defer_small(ctx.prm, (dg, db, dw1, db1, dw2, db2)), None)
 
     @staticmethod
-    def _backward16(ctx, dy, dz, x2, h, mean, rstd, pre, f, g, w1, w2):
-        """bf16-operand backward (same math): dz, f, h cast once; dpre produced in bf16 by the
-        backward-data GEMM with the FFN1 bias gradient as fused column sums; weight gradients of
-        frozen parameters deferred (accumulated into .grad by the GEMM)."""
+    def _backward16(ctx, dy, x2, h, mean, rstd, pre, f, g, w1, w2):
+        """bf16-operand backward (same math): the output dropout, its bf16 copy and the FFN2 bias
+        gradient in one pass over dy; f, h cast once; dpre produced in bf16 by the backward-data
+        GEMM with the FFN1 bias gradient as fused column sums; weight gradients of frozen
+        parameters deferred (accumulated into .grad by the GEMM)."""
         act, eps, p_act, p_hid, s_act, s_hid, scale = ctx.cfg
         NT, D = x2.shape
         F = w1.shape[0]
         dev = x2.device
         ng = ctx.needs_input_grad
-        dz16 = cast16(dz)
-        db2 = db1 = None
-        if ctx.has_b[1] and ng[6]:
-            db2 = torch.empty(D, device=dev)
-            colsum(dz, NT, D, db2)
-        dw2 = _wgrad16(w2, ng[5], dz16, D, cast16(f), F, NT)
+        dz16, db2 = _drop_cast_colsum(dy, p_hid, s_hid, scale, ctx.has_b[1] and ng[6])
+        db1 = None
+        f16 = f if f.dtype == BF16 else _act_dropout_cast16(pre, act, p_act, s_act)
+        dw2 = _wgrad16(w2, ng[5], dz16, D, f16, F, NT)
+        del f16
         dpre16 = torch.empty(NT, F, device=dev, dtype=BF16)
         parts = colsum_parts_buf(NT, F, dev) if (ctx.has_b[0] and ng[4]) else None
         gemm(NT, F, D, op(dz16, 0, D, True), op(weight16t(w2), 0, D, True), None, F, drop_p=p_act, seed=s_act,
@@ -1808,7 +1889,7 @@ class _FFNBlock(torch.autograd.Function):
         dh = torch.empty(NT, D, device=dev)
         gemm(NT, D, F, op(dpre16, 0, F, True), op(weight16t(w1), 0, F, True), dh, D)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
-        return dx.view(ctx.shape), dg, db, dw1, db1, dw2, db2, None
+        return (dx.view(ctx.shape), *_defer_small(ctx.prm, (dg, db, dw1, db1, dw2, db2)), None)
 
 
 def _wgrad16(w, need, dy16, M, x16, N, NT, ldy=None, ldx=None, dy_off=0):
@@ -1857,21 +1938,34 @@ class _ConformerAttnBlock(torch.autograd.Function):
         NT, hd = B * T, D // nh
         dev = x.device
         x2 = x.view(NT, D)
-        h, mean, rstd = _ln_fwd(x2, g, b, eps)
-        if cos_t is not None:
-            hr = torch.empty_like(h)
-            _lib.call("b2p_rotary", _p(h), _p(cos_t), _p(sin_t), _p(hr), B, T, nh, hd, D, 0, _st())
-        else:
-            hr = h
         # bf16 mode, head 64, T' <= 256: fused attention (csrc/attn16.hip, scores stay on-chip); the
         # QKV GEMMs then write only the bf16 operand, and the saved slots hold qkv16 / lse2 / dropout
         # keep bits / O16
         ctx.fused = bf16_mode() and attn16_ok(T, hd)
         qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16 if ctx.fused else torch.float32)
-        for i, (w, bb, src) in enumerate(((wq, bq, hr), (wk, bk, hr), (wv, bv, h))):
-            if ctx.fused:
-                gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), None, 3 * D, c_off=i * D, bias=bb, C16=qkv)
+        if bf16_mode():
+            # the Q/K/V operands come straight from their producers as 16-bit copies (LayerNorm, rotary):
+            # fp16 under forward_f16, else bf16; the fp32 rotated copy is never stored
+            half = _state.fwd16
+            h, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half)
+            hr16 = _rotary16(h, cos_t, sin_t, B, T, nh, hd, half) if cos_t is not None else h16
+            hr = None
+            for i, (w, bb, src) in enumerate(((wq, bq, hr16), (wk, bk, hr16), (wv, bv, h16))):
+                wbuf, wop = _w_op16(w, half)
+                if ctx.fused:
+                    gemm(NT, D, D, op(src, 0, D, True), wop, None, 3 * D, c_off=i * D, bias=bb, C16=qkv)
+                else:
+                    gemm(NT, D, D, op(src, 0, D, True), wop, qkv, 3 * D, c_off=i * D, bias=bb)
+                del wbuf
+            del h16, hr16
+        else:
+            h, mean, rstd = _ln_fwd(x2, g, b, eps)
+            if cos_t is not None:
+                hr = torch.empty_like(h)
+                _lib.call("b2p_rotary", _p(h), _p(cos_t), _p(sin_t), _p(hr), B, T, nh, hd, D, 0, _st())
             else:
+                hr = h
+            for i, (w, bb, src) in enumerate(((wq, bq, hr), (wk, bk, hr), (wv, bv, h))):
                 gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=bb)
         y = torch.empty(NT, D, device=dev)
         if ctx.fused:
@@ -1882,11 +1976,12 @@ class _ConformerAttnBlock(torch.autograd.Function):
             P, Pd, O = _attn_core_fwd(qkv, B, T, nh, hd, p_attn, seeds[0])
             gemm(NT, D, D, op(O, 0, D, True), op(wo, 0, D, True), y, D, bias=bo, drop_p=p_out, seed=seeds[1],
                  residual=x2)
-        ctx.save_for_backward(x2, h, hr if cos_t is not None else None, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo,
-                              cos_t, sin_t)
+        ctx.save_for_backward(x2, h, hr if (cos_t is not None and hr is not None) else None, mean, rstd, qkv, P, Pd,
+                              O, g, wq, wk, wv, wo, cos_t, sin_t)
         ctx.cfg = cfg
         ctx.shape = (B, T, D)
         ctx.has_b = [t is not None for t in (bq, bk, bv, bo)]
+        ctx.prm = (g, b, wq, bq, wk, bk, wv, bv, wo, bo)
         return y.view(B, T, D)
 
     @staticmethod
@@ -1899,10 +1994,10 @@ class _ConformerAttnBlock(torch.autograd.Function):
         ng = ctx.needs_input_grad
         hr_ = h if hr is None else hr
         dy = dy.contiguous().view(NT, D)
-        dz = _dropout_scaled(dy, p_out, seeds[1], 1.0)
         if bf16_mode() or ctx.fused:
-            return _ConformerAttnBlock._backward16(ctx, dy, dz, x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv,
+            return _ConformerAttnBlock._backward16(ctx, dy, x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv,
                                                    wo, cos_t, sin_t)
+        dz = _dropout_scaled(dy, p_out, seeds[1], 1.0)
         dwo = dbo = None
         if ng[9]:
             dwo = torch.empty_like(wo)
@@ -1935,10 +2030,10 @@ class _ConformerAttnBlock(torch.autograd.Function):
             for i, w in enumerate((wq, wk, wv)):
                 gemm(NT, D, D, op(dqkv, i * D, 3 * D, True), op(w, 0, D, False), dh, D, beta=0.0 if i == 0 else 1.0)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
-        return (dx.view(B, T, D), dg, db, *grads, dwo, dbo, None, None, None)
+        return (dx.view(B, T, D), *_defer_small(ctx.prm, (dg, db, *grads, dwo, dbo)), None, None, None)
 
     @staticmethod
-    def _backward16(ctx, dy, dz, x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo, cos_t, sin_t):
+    def _backward16(ctx, dy, x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo, cos_t, sin_t):
         """bf16-operand backward (same math): every GEMM operand cast once, Q/K (and V without
         rotary) input gradients as one GEMM over the concatenated transposed weights, frozen
         weight gradients deferred."""
@@ -1947,11 +2042,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
         NT, hd = B * T, D // nh
         dev = x2.device
         ng = ctx.needs_input_grad
-        dz16 = cast16(dz)
-        dbo = None
-        if ctx.has_b[3] and ng[10]:
-            dbo = torch.empty(D, device=dev)
-            colsum(dz, NT, D, dbo)
+        dz16, dbo = _drop_cast_colsum(dy, p_out, seeds[1], 1.0, ctx.has_b[3] and ng[10])
         dwo = _wgrad16(wo, ng[9], dz16, D, O if ctx.fused else cast16(O), D, NT)
         if ctx.fused:
             # qkv / P / Pd / O hold qkv16, lse2, the dropout keep bits and O16 (forward)
@@ -1966,11 +2057,23 @@ class _ConformerAttnBlock(torch.autograd.Function):
             del dO
             dqkv16 = cast16(dqkv)
         h16 = cast16(h)
-        hr16 = h16 if hr is None else cast16(hr)
+        if cos_t is None:
+            hr16 = h16
+        elif hr is None:   # the forward kept no fp32 rotated copy: rotate h again, into bf16
+            hr16 = _rotary16(h, cos_t, sin_t, B, T, nh, hd, False)
+        else:
+            hr16 = cast16(hr)
         grads = []
+        need_b = [ctx.has_b[i] and ng[4 + 2 * i] for i in range(3)]
+        dbqkv = None
+        if all(need_b):   # the three bias gradients as one column reduction over dqkv
+            dbqkv = torch.empty(3 * D, device=dev)
+            colsum(dqkv, NT, 3 * D, dbqkv)
         for i, (w, src16) in enumerate(((wq, hr16), (wk, hr16), (wv, h16))):
             gb = None
-            if ctx.has_b[i] and ng[4 + 2 * i]:
+            if dbqkv is not None:
+                gb = dbqkv[i * D:(i + 1) * D]
+            elif need_b[i]:
                 gb = torch.empty(D, device=dev)
                 colsum(_view_off(dqkv, i * D), NT, D, gb, ld=3 * D)
             grads += [_wgrad16(w, ng[3 + 2 * i], dqkv16, D, src16, D, NT, ldy=3 * D, dy_off=i * D), gb]
@@ -1985,7 +2088,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
         else:
             gemm(NT, D, 3 * D, op(dqkv16, 0, 3 * D, True), op(weight16t(wq, wk, wv), 0, 3 * D, True), dh, D)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
-        return (dx.view(B, T, D), dg, db, *grads, dwo, dbo, None, None, None)
+        return (dx.view(B, T, D), *_defer_small(ctx.prm, (dg, db, *grads, dwo, dbo)), None, None, None)
 
 
 # ------------------------------------------------------------------ synchronised BatchNorm
@@ -2046,9 +2149,16 @@ class _ConvModule(torch.autograd.Function):
         K = w_dw.shape[-1]
         dev = x.device
         x2 = x.view(NT, D)
-        h, mean, rstd = _ln_fwd(x2, g, b, eps)
         a = torch.empty(NT, 2 * D, device=dev)
-        gemm(NT, 2 * D, D, op(h, 0, D, True), op(w_pw1, 0, D, True), a, 2 * D)
+        if bf16_mode():   # the pointwise-conv operand written by the LayerNorm (fp16 under forward_f16)
+            half = _state.fwd16
+            h, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half)
+            wbuf, wop = _w_op16(w_pw1, half)
+            gemm(NT, 2 * D, D, op(h16, 0, D, True), wop, a, 2 * D)
+            del h16, wbuf
+        else:
+            h, mean, rstd = _ln_fwd(x2, g, b, eps)
+            gemm(NT, 2 * D, D, op(h, 0, D, True), op(w_pw1, 0, D, True), a, 2 * D)
         u = torch.empty(NT, D, device=dev)
         _lib.call("b2p_glu_fwd", _p(a), _p(u), NT, D, _st())
         c = torch.empty(NT, D, device=dev)
@@ -2076,6 +2186,7 @@ class _ConvModule(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.shape = (B, T, D, K)
         ctx.sync = sync
+        ctx.prm = (g, b, w_pw1, w_dw, bn_g, bn_b, w_pw2)
         return y.view(B, T, D)
 
     @staticmethod
@@ -2089,15 +2200,15 @@ class _ConvModule(torch.autograd.Function):
         dev = x2.device
         ng = ctx.needs_input_grad
         dy = dy.contiguous().view(NT, D)
-        do = _dropout_scaled(dy, p, seed, 1.0)
         b16 = bf16_mode()   # bf16 operands: each cast once, frozen weight gradients deferred
         ds = torch.empty(NT, D, device=dev)
         if b16:
-            do16 = cast16(do)
+            do16, _ = _drop_cast_colsum(dy, p, seed, 1.0, False)
             dpw2 = _wgrad16(w_pw2, ng[7], do16, D, cast16(s), D, NT)
             gemm(NT, D, D, op(do16, 0, D, True), op(weight16t(w_pw2), 0, D, True), ds, D)
             del do16
         else:
+            do = _dropout_scaled(dy, p, seed, 1.0)
             dpw2 = None
             if ng[7]:
                 dpw2 = torch.empty_like(w_pw2)
@@ -2130,7 +2241,7 @@ class _ConvModule(torch.autograd.Function):
                 mm_tn(da, h, dpw1.view(2 * D, D))
             mm_nn(da, w_pw1.view(2 * D, D), dh)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
-        return dx.view(B, T, D), dg, db, dpw1, ddw, dbn_g, dbn_b, dpw2, None, None, None
+        return (dx.view(B, T, D), *_defer_small(ctx.prm, (dg, db, dpw1, ddw, dbn_g, dbn_b, dpw2)), None, None, None)
 
 
 def conformer_ffn(x, ln, w1, b1, w2, b2, act, p_act, p_hid, training, scale=0.5):
