@@ -25,6 +25,13 @@ CONFIGS = [
     dict(name="conformer_large_b2", seed=45, B=2, L=288, in_lens=[288, 256], tgt_range=(10, 25), hidden_size=1024,
          layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512, gru_layers=3, bidirectional=True,
          fc_hidden=[256], learnable_h0=False, full_grad_max=4096, infeasible=False, conformer=True, dw_kernel=31),
+    # w2v_do_stable_layer_norm=True (pre-LN encoder, TF Wav2Vec2EncoderStableLayerNorm): tiny and base-size
+    dict(name="tiny_stable", seed=46, B=3, L=96, in_lens=[96, 88, 72], tgt_range=(2, 8), hidden_size=64, layers=2,
+         heads=4, ffn=128, pos_k=16, pos_groups=4, gru_hidden=32, gru_layers=2, bidirectional=True, fc_hidden=[],
+         learnable_h0=False, full_grad_max=65536, infeasible=False, stable=True),
+    dict(name="plumbing_stable", seed=47, B=2, L=512, in_lens=[512, 448], tgt_range=(20, 50), hidden_size=768,
+         layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2, bidirectional=True,
+         fc_hidden=[], learnable_h0=False, full_grad_max=4096, infeasible=False, stable=True),
     # the bench workloads themselves (BASELINE configs[1] and configs[2]) at bs=32, 1024-bin windows:
     # loss, per-parameter gradient norms and sampled gradient entries (inputs are regenerated from the
     # seed, not stored: x alone would be 33 MB)

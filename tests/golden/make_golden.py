@@ -62,7 +62,8 @@ def build_reference_model(cfg, tfw, bfe, w2v, base_args):
         encoder_bidirectional=cfg["bidirectional"], encoder_fc_hidden_sizes=cfg["fc_hidden"],
         encoder_learnable_inital_state=cfg["learnable_h0"])
     brain = bfe.bfe_w_preprocessing_from_config(args, None, name)
-    model = w2v.W2VBrainEncoderModel(w2v.W2VBrainEncoderModelArgs(), brain, name, None, True)
+    model = w2v.W2VBrainEncoderModel(w2v.W2VBrainEncoderModelArgs(w2v_do_stable_layer_norm=cfg.get("stable", False)),
+                                     brain, name, None, True)
     return model
 
 

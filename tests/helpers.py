@@ -29,7 +29,8 @@ def oracle_cfg(cfg):
                         fc_hidden_sizes=list(cfg["fc_hidden"]), learnable_initial_state=cfg["learnable_h0"],
                         hidden_size=cfg["hidden_size"], num_hidden_layers=cfg["layers"],
                         num_attention_heads=cfg["heads"], intermediate_size=cfg["ffn"],
-                        num_conv_pos_embeddings=cfg["pos_k"], num_conv_pos_embedding_groups=cfg["pos_groups"])
+                        num_conv_pos_embeddings=cfg["pos_k"], num_conv_pos_embedding_groups=cfg["pos_groups"],
+                        do_stable_layer_norm=cfg.get("stable", False))
 
 
 def w2v_cfg(cfg, train_dropouts=False):
@@ -64,7 +65,8 @@ def build_model(cfg, device="cuda", seed=None, train_dropouts=False):
         from wav2vec2forbrain_amd.model.w2v_conformer_custom_feat_extractor import W2VConformerBrainEncoderModel
         model = W2VConformerBrainEncoderModel(brain, name, w2v_config_override=w2v_cfg(cfg, train_dropouts))
     else:
-        model = W2VBrainEncoderModel(W2VBrainEncoderModelArgs(), brain, name, skip_loading_weights=True,
+        model = W2VBrainEncoderModel(W2VBrainEncoderModelArgs(w2v_do_stable_layer_norm=cfg.get("stable", False)),
+                                     brain, name, skip_loading_weights=True,
                                      w2v_config_override=w2v_cfg(cfg, train_dropouts))
     init_deterministic_(model, cfg["seed"] if seed is None else seed)
     return model.to(device)

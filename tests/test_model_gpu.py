@@ -32,7 +32,7 @@ def _run(name, mode):
     return model, out
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2",
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
                                   "base_bs32", "conformer_large_bs32"])
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
 def test_step_matches_reference_golden(name, mode):

@@ -10,7 +10,7 @@ import torch
 from tests.helpers import CFG, load_fixture, oracle_cfg, oracle_state, batch_dict, build_model
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2",
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
                                   "base_bs32", "conformer_large_bs32"])
 def test_state_dict_keys_match_reference(name):
     fx = load_fixture(name)
@@ -24,7 +24,7 @@ def test_state_dict_keys_match_reference(name):
 _SLOW = pytest.mark.skipif(os.environ.get("B2P_SLOW_ORACLE") != "1", reason="set B2P_SLOW_ORACLE=1")
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2",
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
                                   "base_bs32", pytest.param("conformer_large_bs32", marks=_SLOW)])
 def test_oracle_matches_reference_golden(name):
     cfg = CFG[name]

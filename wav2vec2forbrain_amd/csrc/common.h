@@ -117,8 +117,22 @@ __device__ __forceinline__ uint32_t b2p_hash(uint64_t seed, uint64_t idx) {
 __device__ __forceinline__ uint64_t b2p_seed_eff(uint64_t seed, const uint64_t* epoch) {
   return epoch ? seed + 0x9E3779B97F4A7C15ull * (*epoch) : seed;
 }
+// One hash serves two consecutive elements: element idx keeps iff its 16-bit half of
+// b2p_hash(seed, idx >> 1) (low half for even idx) is >= thr16 = round(p * 2^16), so the keep
+// probability is exact to 2^-16 and a 4-element group costs two hashes (b2p_keep4).
+__device__ __forceinline__ uint32_t b2p_thr16(uint32_t thr) { return (thr >> 16) + ((thr >> 15) & 1u); }
 __device__ __forceinline__ bool b2p_keep(uint64_t seed, uint64_t idx, uint32_t thr) {
-  return b2p_hash(seed, idx) >= thr;
+  const uint32_t h = b2p_hash(seed, idx >> 1);
+  return ((idx & 1) ? (h >> 16) : (h & 0xFFFFu)) >= b2p_thr16(thr);
+}
+// keep bits of elements idx .. idx+3, idx even
+__device__ __forceinline__ void b2p_keep4(uint64_t seed, uint64_t idx, uint32_t thr, bool k[4]) {
+  const uint32_t t = b2p_thr16(thr);
+  const uint32_t h0 = b2p_hash(seed, idx >> 1), h1 = b2p_hash(seed, (idx >> 1) + 1);
+  k[0] = (h0 & 0xFFFFu) >= t;
+  k[1] = (h0 >> 16) >= t;
+  k[2] = (h1 & 0xFFFFu) >= t;
+  k[3] = (h1 >> 16) >= t;
 }
 
 __device__ __forceinline__ float warp_sum(float v) {

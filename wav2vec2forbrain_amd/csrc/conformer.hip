@@ -330,10 +330,12 @@ __global__ void __launch_bounds__(256) drop_cast_colsum_k(const float* __restric
       float4 v = *reinterpret_cast<const float4*>(x + i);
       v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale;
       if (use_mask) {
-        if (!b2p_keep(seed, (uint64_t)i, thr)) v.x = 0.f;
-        if (!b2p_keep(seed, (uint64_t)i + 1, thr)) v.y = 0.f;
-        if (!b2p_keep(seed, (uint64_t)i + 2, thr)) v.z = 0.f;
-        if (!b2p_keep(seed, (uint64_t)i + 3, thr)) v.w = 0.f;
+        bool k[4];
+        b2p_keep4(seed, (uint64_t)i, thr, k);   // i % 4 == 0
+        if (!k[0]) v.x = 0.f;
+        if (!k[1]) v.y = 0.f;
+        if (!k[2]) v.z = 0.f;
+        if (!k[3]) v.w = 0.f;
       }
       *reinterpret_cast<uint2*>(y16 + i) = b2p_pack_bf16x4(v);
       s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;

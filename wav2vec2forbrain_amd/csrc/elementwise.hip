@@ -179,10 +179,12 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
       o.w = (v[i].w - mu) * rs * g.w + bb.w;
       if (drop_p > 0.f) {
         const uint64_t base = (uint64_t)row * cols + 4 * c;
-        o.x = b2p_keep(seed, base + 0, thr) ? o.x * dscale : 0.f;
-        o.y = b2p_keep(seed, base + 1, thr) ? o.y * dscale : 0.f;
-        o.z = b2p_keep(seed, base + 2, thr) ? o.z * dscale : 0.f;
-        o.w = b2p_keep(seed, base + 3, thr) ? o.w * dscale : 0.f;
+        bool kk[4];
+        b2p_keep4(seed, base, thr, kk);   // base % 4 == 0
+        o.x = kk[0] ? o.x * dscale : 0.f;
+        o.y = kk[1] ? o.y * dscale : 0.f;
+        o.z = kk[2] ? o.z * dscale : 0.f;
+        o.w = kk[3] ? o.w * dscale : 0.f;
       }
       if (y) yr[c] = o;
       if (y16) reinterpret_cast<uint2*>(y16 + row * cols)[c] = b2p_pack16x4(o, y16_half);
@@ -224,10 +226,12 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
         float4 d = dyr[c];
         if (drop_p > 0.f) {
           const uint64_t base = (uint64_t)row * cols + 4 * c;
-          d.x = b2p_keep(seed, base + 0, thr) ? d.x * dscale : 0.f;
-          d.y = b2p_keep(seed, base + 1, thr) ? d.y * dscale : 0.f;
-          d.z = b2p_keep(seed, base + 2, thr) ? d.z * dscale : 0.f;
-          d.w = b2p_keep(seed, base + 3, thr) ? d.w * dscale : 0.f;
+          bool kk[4];
+          b2p_keep4(seed, base, thr, kk);   // base % 4 == 0
+          d.x = kk[0] ? d.x * dscale : 0.f;
+          d.y = kk[1] ? d.y * dscale : 0.f;
+          d.z = kk[2] ? d.z * dscale : 0.f;
+          d.w = kk[3] ? d.w * dscale : 0.f;
         }
         const float4 xv = xr[c], g = g4[c];
         xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
@@ -257,10 +261,12 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
         if (dxd) {   // gradient of the dropout that produced this LN's input (residual branch)
           const uint64_t base = (uint64_t)row * cols + 4 * c;
           float4 q;
-          q.x = b2p_keep(seed2, base + 0, thr2) ? o.x * dscale2 : 0.f;
-          q.y = b2p_keep(seed2, base + 1, thr2) ? o.y * dscale2 : 0.f;
-          q.z = b2p_keep(seed2, base + 2, thr2) ? o.z * dscale2 : 0.f;
-          q.w = b2p_keep(seed2, base + 3, thr2) ? o.w * dscale2 : 0.f;
+          bool kk[4];
+          b2p_keep4(seed2, base, thr2, kk);   // base % 4 == 0
+          q.x = kk[0] ? o.x * dscale2 : 0.f;
+          q.y = kk[1] ? o.y * dscale2 : 0.f;
+          q.z = kk[2] ? o.z * dscale2 : 0.f;
+          q.w = kk[3] ? o.w * dscale2 : 0.f;
           reinterpret_cast<float4*>(dxd + row * cols)[c] = q;
           if (d16) reinterpret_cast<uint2*>(d16 + row * cols)[c] = b2p_pack_bf16x4(q);
           dd[i].x += q.x; dd[i].y += q.y; dd[i].z += q.z; dd[i].w += q.w;

@@ -87,8 +87,10 @@ __device__ __forceinline__ float4 epilogue_store4(const EpiArgs& a, int z, int z
   if (e.drop_p > 0.0f) {
     const uint64_t idx = ((uint64_t)z * (uint64_t)a.M + (uint64_t)m) * (uint64_t)a.N + (uint64_t)n;
     const uint64_t sd = b2p_seed_eff(e.drop_seed, a.epoch);
+    bool k[4];
+    b2p_keep4(sd, idx, a.drop_thr, k);   // idx % 4 == 0 (vec4: N % 4 == 0, n % 4 == 0)
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = b2p_keep(sd, idx + q, a.drop_thr) ? v[q] * a.drop_scale : 0.0f;
+    for (int q = 0; q < 4; ++q) v[q] = k[q] ? v[q] * a.drop_scale : 0.0f;
   }
   if (e.act_bwd != B2P_ACT_NONE) {
     const int64_t ao = (int64_t)z1 * e.abs1 + (int64_t)z2 * e.abs2 + (int64_t)m * e.ldaux + n;

@@ -1176,7 +1176,11 @@ class _PosConvLN(torch.autograd.Function):
             gemm(B * T, Og, K * Ig, A, op(wp, 0, K * Ig, True, bs1=Og * K * Ig), xsum, D, cbs1=Og, nz1=groups,
                  bias=cbias, biasbs1=Og, pre_out=pre, act=ACT["gelu"], residual=e, rbs1=Og, ldr=D)
             keep = e
-        y, mean, rstd = _ln_fwd(xsum.view(B * T, D), ln_g, ln_b, eps, drop_p, seed)
+        if ln_g is not None:
+            y, mean, rstd = _ln_fwd(xsum.view(B * T, D), ln_g, ln_b, eps, drop_p, seed)
+        else:   # stable-LN encoder (TF w2v Wav2Vec2EncoderStableLayerNorm): dropout(x + pos), no LayerNorm
+            y = _dropout_raw(xsum.view(B * T, D), drop_p, seed) if drop_p > 0 else xsum.view(B * T, D)
+            mean = rstd = None
         ctx.save_for_backward(keep, wg, wv, w, norms, pre, xsum, ln_g, mean, rstd)
         ctx.meta = (groups, drop_p, seed, B, T, D, O, Ig, K)
         ctx.fast = fast
@@ -1188,7 +1192,11 @@ class _PosConvLN(torch.autograd.Function):
         groups, drop_p, seed, B, T, D, O, Ig, K = ctx.meta
         dev = e.device
         dy = dy.contiguous().view(B * T, D)
-        dxsum, dlg, dlb, _ = _ln_bwd(dy, xsum.view(B * T, D), ln_g, mean, rstd, True, None, drop_p, seed)
+        if ln_g is not None:
+            dxsum, dlg, dlb, _ = _ln_bwd(dy, xsum.view(B * T, D), ln_g, mean, rstd, True, None, drop_p, seed)
+        else:
+            dxsum = _dropout_raw(dy, drop_p, seed) if drop_p > 0 else dy
+            dlg = dlb = None
         if ctx.fast:
             return _posconv16_bwd(ctx, e, wg, wv, w, norms, pre, dxsum, dlg, dlb)
         dpre = _act_bwd(dxsum, pre.view(B * T, D), ACT["gelu"])
@@ -1252,6 +1260,7 @@ def _posconv16_bwd(ctx, e16, wg, wv, w, norms, pre, dxsum, dlg, dlb):
 
 
 def pos_conv_ln(e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, training):
+    """dropout(LN(e + gelu(posconv(e)))); ln_g = ln_b = None: dropout(e + gelu(posconv(e))) (stable-LN)."""
     p = drop_p if training else 0.0
     return _PosConvLN.apply(e.contiguous(), wg, wv, cbias, ln_g, ln_b, groups, eps, p, SEEDS.next() if p > 0 else 0)
 

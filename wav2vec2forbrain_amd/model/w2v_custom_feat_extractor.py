@@ -11,6 +11,7 @@ functional.{pos_conv_ln, encoder_layer, dropout, linear, ctc_loss} (HIP).
 """
 from __future__ import annotations
 
+import dataclasses
 import math
 from typing import Optional
 
@@ -72,6 +73,24 @@ class Wav2Vec2EncoderLayer(nn.Module):
                                 c.attention_dropout, c.hidden_dropout, c.activation_dropout, self.training)
 
 
+class Wav2Vec2EncoderLayerStableLayerNorm(Wav2Vec2EncoderLayer):
+    """Pre-LN layer (TF Wav2Vec2EncoderLayerStableLayerNorm.forward), same parameters and names:
+    x = x + drop(Attn(LN(x))); x = x + FFN(final_LN(x)), FFN = drop(W2 drop(GELU(W1 x + b1)) + b2).
+    Runs on the pre-LN blocks the Conformer uses (functional.conformer_attention without rotary,
+    functional.conformer_ffn with a full residual step)."""
+
+    def forward(self, hidden_states):
+        c = self.config
+        if c.hidden_act not in ("gelu",):
+            raise NotImplementedError(f"hidden_act {c.hidden_act!r} for the wav2vec2 encoder layer")
+        a, f = self.attention, self.feed_forward
+        x = Fn.conformer_attention(hidden_states, self.layer_norm, a.q_proj, a.k_proj, a.v_proj, a.out_proj,
+                                   c.num_attention_heads, None, c.attention_dropout, c.hidden_dropout, self.training)
+        return Fn.conformer_ffn(x, self.final_layer_norm, f.intermediate_dense.weight, f.intermediate_dense.bias,
+                                f.output_dense.weight, f.output_dense.bias, Fn.ACT["gelu"], c.activation_dropout,
+                                c.hidden_dropout, self.training, scale=1.0)
+
+
 class Wav2Vec2PositionalConvEmbedding(nn.Module):
     def __init__(self, config: w2v_config.W2VConfig):
         super().__init__()
@@ -118,15 +137,40 @@ class Wav2Vec2Encoder(nn.Module):
         return hidden_states
 
 
+class Wav2Vec2EncoderStableLayerNorm(Wav2Vec2Encoder):
+    """TF Wav2Vec2EncoderStableLayerNorm.forward (reference :18-19 with w2v_do_stable_layer_norm=True):
+    x = dropout(x + gelu(posconv(x))) (no LayerNorm before the layers); pre-LN layers under LayerDrop;
+    final LayerNorm after them. Same parameter names as the post-LN encoder."""
+
+    def __init__(self, config: w2v_config.W2VConfig):
+        super().__init__(config)
+        self.layers = nn.ModuleList([Wav2Vec2EncoderLayerStableLayerNorm(config)
+                                     for _ in range(config.num_hidden_layers)])
+
+    def forward(self, hidden_states):
+        c = self.config
+        g, v, cb = self.pos_conv_embed.weights()
+        hidden_states = Fn.pos_conv_ln(hidden_states, g, v, cb, None, None, self.pos_conv_embed.groups,
+                                       c.layer_norm_eps, c.hidden_dropout, self.training)
+        graph_ld = self.training and c.layerdrop > 0 and Fn.capturing() and Fn.GRAPH_LAYERDROP
+        for layer in self.layers:
+            dropout_probability = torch.rand([])
+            if graph_ld:
+                hidden_states = Fn.layerdrop_layer(layer, hidden_states, c.layerdrop)
+                continue
+            if not (self.training and bool(dropout_probability < c.layerdrop)):
+                hidden_states = layer(hidden_states)
+        return Fn.layer_norm(hidden_states, self.layer_norm.weight, self.layer_norm.bias, c.layer_norm_eps)
+
+
 class Wav2Vec2WithoutFeatExtrModel(nn.Module):
     """Reference :156-191 (encoder only, attention_mask=None, no adapter)."""
 
     def __init__(self, config: w2v_config.W2VConfig):
         super().__init__()
         self.config = config
-        if config.do_stable_layer_norm:
-            raise NotImplementedError("w2v_do_stable_layer_norm=True (pre-LN encoder) is not built yet")
-        self.encoder = Wav2Vec2Encoder(config)
+        # reference :18-19,36-41: do_stable_layer_norm = w2v_do_stable_layer_norm selects the pre-LN encoder
+        self.encoder = Wav2Vec2EncoderStableLayerNorm(config) if config.do_stable_layer_norm else Wav2Vec2Encoder(config)
 
     def forward(self, input_values):
         return self.encoder(input_values)
@@ -165,8 +209,10 @@ class W2VBrainEncoderModel(B2TModel):
                  w2v_config_override: Optional[w2v_config.W2VConfig] = None):
         super().__init__()
         self.brain_encoder = brain_encoder
-        cfg = w2v_config_override if w2v_config_override is not None else w2v_config.from_pretrained(
-            wav2vec_checkpoint, do_stable_layer_norm=config.w2v_do_stable_layer_norm)
+        if w2v_config_override is not None:   # explicit architecture; the stable-LN switch still follows the args
+            cfg = dataclasses.replace(w2v_config_override, do_stable_layer_norm=config.w2v_do_stable_layer_norm)
+        else:
+            cfg = w2v_config.from_pretrained(wav2vec_checkpoint, do_stable_layer_norm=config.w2v_do_stable_layer_norm)
         self.w2v_encoder = Wav2Vec2WithoutFeatExtrForCTC(cfg)
         if not skip_loading_weights:
             print(f"Note: pretrained weights for {wav2vec_checkpoint} are not downloadable offline; "
