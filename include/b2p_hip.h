@@ -126,6 +126,14 @@ int b2p_gemm(const b2p_gemm_desc* d, b2p_stream_t stream);
  * when a counter is set (NULL restores eager semantics); b2p_seed_epoch_step increments it (the
  * captured step's first node), so each replay draws new masks. */
 int b2p_set_seed_epoch(const uint64_t* dev_counter);
+/* LayerDrop gate (TF w2v / TF conf encoder LayerDrop inside a captured step): every GEMM and fused-
+ * attention launch issued while a gate is set reads the device int *dev_flag when it runs; 0 skips
+ * the GEMM's K loop (accumulators stay 0, the epilogue still writes finite outputs) and the
+ * attention work (its backward writes zero gradients). NULL: ungated (default). */
+int b2p_set_gate(const int32_t* dev_flag);
+/* *flag = keep (1) / skip (0) of one layer for this replay: the draw b2p_layerdrop_select makes for
+ * the same (p, seed) (step counter of b2p_set_seed_epoch mixed in). */
+int b2p_layerdrop_flag(int32_t* flag, float p, uint64_t seed, b2p_stream_t stream);
 int b2p_seed_epoch_step(uint64_t* dev_counter, b2p_stream_t stream);
 
 /* ------------------------------------------------------------------ elementwise / reductions */

@@ -93,7 +93,20 @@ struct DropCfg {
   uint32_t thr;
   float scale;                // 1 / (1 - p)
   const uint64_t* epoch;      // graph-replay seed offset (b2p_seed_eff), NULL in eager launches
+  const int32_t* gate;        // LayerDrop gate (b2p_gate): closed -> fwd does nothing, bwd writes zeros
 };
+
+// closed-gate backward: zero this block's 64 rows x 64 columns of dqkv at column col (fp32 and/or bf16)
+__device__ __forceinline__ void zero_block(float* dqkv, uint16_t* dqkv16, int64_t row0, int r0, int T, int64_t ld,
+                                           int64_t col, int tid) {
+  for (int i = tid; i < 64 * 16; i += 256) {
+    const int r = r0 + (i >> 4);
+    if (r >= T) continue;
+    const int64_t o = (row0 + r) * ld + col + 4 * (i & 15);
+    if (dqkv) *reinterpret_cast<float4*>(dqkv + o) = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (dqkv16) *reinterpret_cast<uint2*>(dqkv16 + o) = make_uint2(0u, 0u);
+  }
+}
 template <bool DROP>
 __device__ __forceinline__ float keep_scale(const DropCfg& dc, uint64_t idx) {
   if (!DROP) return 1.f;
@@ -107,6 +120,7 @@ __global__ void __launch_bounds__(256) attn16_fwd_k(const uint16_t* __restrict__
                                                     float* __restrict__ lse2, int T, int nh, float scale, DropCfg dc,
                                                     uint32_t* __restrict__ maskw) {
   constexpr bool DROP = DM != 0;
+  if (b2p_gated_off(dc.gate)) return;   // LayerDrop: this replay skips the layer (outputs unused)
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* Kimg = smem;
@@ -223,6 +237,11 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
   const int64_t ld = 3 * (int64_t)D;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
   const int64_t row0 = (int64_t)b * T;
+  if (b2p_gated_off(dc.gate)) {   // LayerDrop: zero dK, dV (the bias reduction reads them)
+    zero_block(dqkv, dqkv16, row0, kb * 64, T, ld, D + h * DH, tid);
+    zero_block(dqkv, dqkv16, row0, kb * 64, T, ld, 2 * D + h * DH, tid);
+    return;
+  }
   load_image(Qimg, qkv, row0, T, ld, h * DH, tid);
   load_image(dOimg, dO16, row0, T, D, h * DH, tid);
   {
@@ -324,6 +343,10 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
   const int64_t ld = 3 * (int64_t)D;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
   const int64_t row0 = (int64_t)b * T;
+  if (b2p_gated_off(dc.gate)) {   // LayerDrop: zero dQ (the bias reduction reads it)
+    zero_block(dqkv, dqkv16, row0, qb * 64, T, ld, h * DH, tid);
+    return;
+  }
   load_image(Kimg, qkv, row0, T, ld, D + h * DH, tid);
   load_image(Vimg, qkv, row0, T, ld, 2 * D + h * DH, tid);
   const int q = qb * 64 + w * 16 + lr;
@@ -399,6 +422,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
 DropCfg drop_cfg(float p, uint64_t seed) {
   DropCfg d;
   d.epoch = b2p_seed_epoch();
+  d.gate = b2p_gate();
   d.seed = seed;
   d.thr = b2p_dropout_threshold(p);
   d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;

@@ -34,6 +34,10 @@ __device__ __forceinline__ float b2p_bf16_to_f32(uint16_t b) {
 // ---------------------------------------------------------------------------
 // device counter added to every dropout seed (NULL: none); set by b2p_set_seed_epoch (lib.cpp)
 const uint64_t* b2p_seed_epoch();
+// LayerDrop gate set by b2p_set_gate (lib.cpp): GEMMs under a closed gate skip their K loop (acc = 0,
+// epilogue still runs, so every output stays finite), fused attention skips its work
+const int32_t* b2p_gate();
+__device__ __forceinline__ bool b2p_gated_off(const int32_t* gate) { return gate && *gate == 0; }
 void b2p_set_error(const char* fmt, ...);
 
 #define B2P_CHECK_ARG(cond, ...)                 \

@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
 #define AS_(b) (smem + (b) * (BM + BN) * LS)
 #define BS_(b) (smem + (b) * (BM + BN) * LS + BM * LS)
 
-  const int nk = K > kbeg ? (K - kbeg + KB - 1) / KB : 0;
+  const int nk = (K > kbeg && !b2p_gated_off(ea.gate)) ? (K - kbeg + KB - 1) / KB : 0;
   la.load(sa, tid, kbeg, K);
   lb.load(sb, tid, kbeg, K);
   la.store(AS_(0), tid);

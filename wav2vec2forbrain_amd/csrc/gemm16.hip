@@ -307,7 +307,7 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_
   const int kchunk = ks > 1 ? (int)d.kchunk : (int)d.K;
   const int kbeg = ksl * kchunk;
   const int K = ((int)d.K < kbeg + kchunk) ? (int)d.K : kbeg + kchunk;
-  const int nk = K > kbeg ? (K - kbeg + KT - 1) / KT : 0;
+  const int nk = (K > kbeg && !b2p_gated_off(ea.gate)) ? (K - kbeg + KT - 1) / KT : 0;
 
   SA sa;
   SB sb;
@@ -463,7 +463,7 @@ __global__ void __launch_bounds__(PP_NT, 1) gemm16_pp_kernel(const b2p_gemm_desc
   const int kchunk = ks > 1 ? (int)d.kchunk : (int)d.K;
   const int kbeg = ksl * kchunk;
   const int K = ((int)d.K < kbeg + kchunk) ? (int)d.K : kbeg + kchunk;
-  const int nk = K > kbeg ? (K - kbeg + PP_KT - 1) / PP_KT : 0;
+  const int nk = (K > kbeg && !b2p_gated_off(ea.gate)) ? (K - kbeg + PP_KT - 1) / PP_KT : 0;
 
   SA sa;
   SB sb;

@@ -28,6 +28,7 @@ struct EpiArgs {
   float drop_scale;
   int32_t vec4;   // every C-shaped tensor allows 16-B (C16: 8-B) accesses at n % 4 == 0
   const uint64_t* epoch;   // graph-replay dropout seed offset (b2p_seed_eff)
+  const int32_t* gate;     // LayerDrop gate (b2p_gate): closed -> no K loop
 };
 
 __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, int z2, int m, int n,
@@ -155,6 +156,7 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
   if (e.residual) v = v && a16(e.residual) && s4(e.ldr) && s4(e.rbs1) && s4(e.rbs2);
   ea.vec4 = v ? 1 : 0;
   ea.epoch = b2p_seed_epoch();
+  ea.gate = b2p_gate();
   return ea;
 }
 

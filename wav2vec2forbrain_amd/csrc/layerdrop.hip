@@ -63,6 +63,11 @@ __global__ void __launch_bounds__(256) ld_route_k(const float4* __restrict__ dou
   }
 }
 
+// the gate of one layer for this replay: flag = keep (1) or skip (0), the draw ld_select_k makes
+__global__ void ld_flag_k(int32_t* flag, uint32_t thr, uint64_t seed, const uint64_t* __restrict__ epoch) {
+  if (threadIdx.x == 0) *flag = dev_keep(seed, epoch, thr) ? 1 : 0;
+}
+
 inline unsigned grid_for(int64_t n4) {
   const int64_t b = (n4 + 255) / 256;
   return (unsigned)(b < 4096 ? (b > 0 ? b : 1) : 4096);
@@ -107,6 +112,15 @@ extern "C" int b2p_layerdrop_route(const float* dout, float* d_keep, float* d_sk
   if (n4 <= 0) return 0;
   hipLaunchKernelGGL(ld_route_k, dim3(grid_for(n4)), dim3(256), 0, (hipStream_t)stream, (const float4*)dout,
                      (float4*)d_keep, (float4*)d_skip, n4, b2p_dropout_threshold(p), seed, b2p_seed_epoch());
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_layerdrop_flag(int32_t* flag, float p, uint64_t seed, b2p_stream_t stream) {
+  B2P_CHECK_ARG(flag != nullptr, "layerdrop_flag: NULL flag");
+  B2P_CHECK_ARG(p >= 0.f && p < 1.f, "layerdrop_flag: p must be in [0,1)");
+  hipLaunchKernelGGL(ld_flag_k, dim3(1), dim3(64), 0, (hipStream_t)stream, flag, b2p_dropout_threshold(p), seed,
+                     b2p_seed_epoch());
   B2P_CHECK_LAUNCH();
   return 0;
 }

@@ -25,6 +25,14 @@ extern "C" int b2p_set_seed_epoch(const uint64_t* dev_counter) {
   g_seed_epoch = dev_counter;
   return 0;
 }
+// LayerDrop gate of the layer being issued (device int, 0 = this replay skips the layer); NULL =
+// ungated. Read by the GEMM and fused-attention launchers into their kernel arguments.
+static const int32_t* g_gate = nullptr;
+const int32_t* b2p_gate() { return g_gate; }
+extern "C" int b2p_set_gate(const int32_t* dev_flag) {
+  g_gate = dev_flag;
+  return 0;
+}
 extern "C" int b2p_version(void) { return 1; }
 extern "C" int b2p_abi_sizes(int64_t* out3) {
   if (!out3) {

@@ -16,6 +16,7 @@ Operators (reference call sites in each docstring):
 from __future__ import annotations
 
 import contextlib
+import functools
 import ctypes
 import math
 import threading
@@ -36,9 +37,46 @@ class _State:
     fwd16 = False   # forward_f16(): fp32-operand GEMMs of a forward pass on fp16 MFMA
     nosplit = False  # no split-K (deferred weight gradients issued on concurrent side streams)
     sync_bn = None   # process group for synchronised BatchNorm statistics (sync_batchnorm())
+    gate = None      # LayerDrop gate (device int32) of the layer being issued in a captured step
 
 
 _state = _State()
+
+
+@contextlib.contextmanager
+def _gated(flag):
+    """GEMM / fused-attention launches inside read the device LayerDrop flag (b2p_set_gate)."""
+    old = _state.gate
+    if flag is old:
+        yield
+        return
+    _state.gate = flag
+    _lib.call("b2p_set_gate", None if flag is None else flag.data_ptr())
+    try:
+        yield
+    finally:
+        _state.gate = old
+        _lib.call("b2p_set_gate", None if old is None else old.data_ptr())
+
+
+def _gate_aware(cls):
+    """An encoder-layer autograd Function whose backward runs under the gate its forward ran under
+    (a layer skipped by this replay's LayerDrop draw skips its backward GEMMs too)."""
+    fwd, bwd = cls.forward, cls.backward
+
+    @functools.wraps(fwd)
+    def forward(ctx, *args):
+        ctx.gate = _state.gate
+        return fwd(ctx, *args)
+
+    @functools.wraps(bwd)
+    def backward(ctx, *grads):
+        with _gated(ctx.gate):
+            return bwd(ctx, *grads)
+
+    cls.forward = staticmethod(forward)
+    cls.backward = staticmethod(backward)
+    return cls
 
 
 def _prec() -> int:
@@ -172,6 +210,18 @@ def _flush_accs(sd) -> None:
     _Deferred.accs.clear()
 
 
+def _gate_wrap(run):
+    """A deferred launch keeps the LayerDrop gate of the layer that queued it."""
+    gate = _state.gate
+    if gate is None:
+        return run
+
+    def gated():
+        with _gated(gate):
+            run()
+    return gated
+
+
 def _defer_wgemm_rows(ps, fn, *tensors) -> None:
     """Like _defer_wgemm for parameters whose gradients are row blocks of ONE GEMM output (Q, K, V
     weights of the fused QKV projection): their .grad are views of one buffer, so a single GEMM
@@ -211,7 +261,7 @@ def _defer_wgemm_rows(ps, fn, *tensors) -> None:
                     r += n
         finally:
             _state.prec = old
-    _Deferred.queue.append((run, tensors, id(ps[0])))
+    _Deferred.queue.append((_gate_wrap(run), tensors, id(ps[0])))
 
 
 def _defer_wgemm(p, fn, *tensors) -> None:
@@ -229,7 +279,7 @@ def _defer_wgemm(p, fn, *tensors) -> None:
                 fn(p.grad, 1.0)
         finally:
             _state.prec = old
-    _Deferred.queue.append((run, tensors, id(p)))
+    _Deferred.queue.append((_gate_wrap(run), tensors, id(p)))
 
 
 def flush_wgrad(after=None) -> None:
@@ -1120,6 +1170,11 @@ def capturing() -> bool:
     return torch.cuda.is_available() and torch.cuda.is_current_stream_capturing()
 
 
+# B2P_LAYERDROP_GATE=0: a skipped layer still computes (diagnostic / A-B of the gate)
+LAYERDROP_GATE = os.environ.get("B2P_LAYERDROP_GATE", "1") != "0"
+_GATE_FLAGS: list = []
+
+
 def layerdrop_layer(layer, x, p):
     """One encoder layer under LayerDrop inside a captured step (see csrc/layerdrop.hip): the layer
     always runs, its output or its input is selected by the device draw of this replay, and float
@@ -1130,7 +1185,17 @@ def layerdrop_layer(layer, x, p):
         LAYERDROP_LOG.append(seed)
     bufs = [b for b in layer.buffers() if b.is_floating_point() and b.numel() % 4 == 0]
     olds = [b.clone() for b in bufs]
-    y = layer(x)
+    y = None
+    if LAYERDROP_GATE:
+        # the layer's GEMMs and fused attention (forward, backward, deferred weight gradients) read
+        # this replay's draw and do no work when it skips the layer; the select below still routes
+        flag = torch.empty(1, dtype=torch.int32, device=x.device)
+        _GATE_FLAGS.append(flag)      # referenced by the captured graph's kernels: kept for its life
+        _lib.call("b2p_layerdrop_flag", _p(flag), float(p), seed, _st())
+        with _gated(flag):
+            y = layer(x)
+    else:
+        y = layer(x)
     for b, o in zip(bufs, olds):
         _lib.call("b2p_layerdrop_select", _p(o), _p(b), _p(b), None, None, None, b.numel(), float(p), seed, _st())
     return _LayerDropSelect.apply(x, y, float(p), seed)
@@ -1349,6 +1414,7 @@ def _attn16_bwd(qkv16, dO16, lse2, B, T, nh, dh, p_attn, seed, want32=True, mask
 # =====================================================================================
 # post-LN transformer encoder layer (Wav2Vec2EncoderLayer)
 # =====================================================================================
+@_gate_aware
 class _EncoderLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cfg, wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
@@ -1447,6 +1513,7 @@ class _EncoderLayer(torch.autograd.Function):
         return (dx, None, *grads_w, dwo, dbo, dg1, dbe1, dw1, db1, dw2, db2, dg2, dbe2)
 
 
+@_gate_aware
 class _EncoderLayer16(torch.autograd.Function):
     """bf16-operand variant of _EncoderLayer (same math, same dropout masks): Q/K/V fused into one
     GEMM over the concatenated bf16 weight, every projection reading bf16 copies written by the
@@ -1720,6 +1787,7 @@ def ctc_greedy_cer(logits, targets, vocab, blank=0, eos=2, delim=4):
 # Conformer (transformers Wav2Vec2ConformerEncoderLayer, rotary variant) — reference
 # src/model/w2v_conformer_custom_feat_extractor.py:62-112
 # =====================================================================================
+@_gate_aware
 class _LayerNorm(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, g, b, eps):
@@ -1796,6 +1864,7 @@ def _act_dropout_cast16(pre, act, p, seed):
     return out
 
 
+@_gate_aware
 class _FFNBlock(torch.autograd.Function):
     """y = x + scale * dropout_h(W2 dropout_a(act(W1 LN(x) + b1)) + b2)   (macaron half-step, scale 0.5)"""
 
@@ -1936,6 +2005,7 @@ def rotary_tables(T, D, base, device):
     return _ROT[key]
 
 
+@_gate_aware
 class _ConformerAttnBlock(torch.autograd.Function):
     """y = x + dropout(linear_out(Attn(q=k=rotary(LN x), v=LN x)))  (TF conf Wav2Vec2ConformerSelfAttention)"""
 
@@ -2146,6 +2216,7 @@ def sync_batchnorm(group):
         _state.sync_bn = old
 
 
+@_gate_aware
 class _ConvModule(torch.autograd.Function):
     """y = x + dropout(pw2(act(BN(dwconv(GLU(pw1(LN x)))))))   (TF conf Wav2Vec2ConformerConvolutionModule)"""
 
