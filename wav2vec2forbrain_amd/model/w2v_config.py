@@ -63,10 +63,29 @@ PRESETS: dict[str, W2VConfig] = {
 }
 
 
+def from_local_dir(path: str) -> W2VConfig:
+    """Architecture of a local HF checkpoint directory (its config.json: Wav2Vec2Config /
+    Wav2Vec2ConformerConfig fields; unknown fields ignored)."""
+    import json
+    import os
+    with open(os.path.join(path, "config.json")) as f:
+        js = json.load(f)
+    cfg = W2VConfig()
+    for k, v in js.items():
+        if hasattr(cfg, k) and k != "conformer":
+            setattr(cfg, k, v)
+    cfg.conformer = "conformer" in str(js.get("model_type", ""))
+    return cfg
+
+
 def from_pretrained(name: str, **overrides) -> W2VConfig:
-    if name not in PRESETS:
-        raise KeyError(f"no offline preset for {name!r}; known: {sorted(PRESETS)}")
-    cfg = copy.deepcopy(PRESETS[name])
+    import os
+    if os.path.isdir(name) and os.path.exists(os.path.join(name, "config.json")):
+        cfg = from_local_dir(name)
+    elif name not in PRESETS:
+        raise KeyError(f"no offline preset for {name!r} and no local checkpoint directory; known: {sorted(PRESETS)}")
+    else:
+        cfg = copy.deepcopy(PRESETS[name])
     for k, v in overrides.items():
         if not hasattr(cfg, k):
             raise AttributeError(f"W2VConfig has no field {k!r}")

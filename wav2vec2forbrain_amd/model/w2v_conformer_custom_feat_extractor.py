@@ -167,6 +167,9 @@ class W2VConformerBrainEncoderModel(B2TModel):
         if not cfg.conformer:
             cfg.conformer = True
         self.w2v_encoder = Wav2Vec2ConformerWithoutFeatExtrForCTC(cfg)
+        if w2v_config_override is None:   # reference :27-33 always loads the checkpoint's weights
+            from .w2v_custom_feat_extractor import _load_or_note
+            _load_or_note(self.w2v_encoder, wav2vec_checkpoint)
         self.blank = 0
         self.sync_metrics = True
         # bf16 mode: the Conformer's forward GEMMs on fp16 MFMA (Fn.forward_f16: removes the CTC-loss

@@ -198,6 +198,20 @@ class Wav2Vec2WithoutFeatExtrForCTC(nn.Module):
         return logits, hidden_states
 
 
+def _load_or_note(w2v_encoder, wav2vec_checkpoint: str) -> None:
+    """Reference from_pretrained weight load (:43-51) from a local HF checkpoint directory; hub names
+    are unreachable offline (weights then come from load_state_dict / --from_checkpoint)."""
+    import os
+    if os.path.isdir(wav2vec_checkpoint):
+        from ..util.hf_weights import load_pretrained_w2v
+        rep = load_pretrained_w2v(w2v_encoder, wav2vec_checkpoint)
+        print(f"loaded {rep['loaded']} tensors from {wav2vec_checkpoint} (dropped {len(rep['dropped'])}; "
+              f"positional-conv weight norm: {rep['pos_conv']})")
+    else:
+        print(f"Note: pretrained weights for {wav2vec_checkpoint} are not downloadable offline; "
+              "load them with load_state_dict / --from_checkpoint or pass a local checkpoint directory")
+
+
 class W2VBrainEncoderModel(B2TModel):
     """Reference :22-136. `wav2vec_checkpoint` selects an offline architecture preset (the hub is
     unreachable); pretrained weights are loaded through load_state_dict / from_checkpoint."""
@@ -215,8 +229,7 @@ class W2VBrainEncoderModel(B2TModel):
             cfg = w2v_config.from_pretrained(wav2vec_checkpoint, do_stable_layer_norm=config.w2v_do_stable_layer_norm)
         self.w2v_encoder = Wav2Vec2WithoutFeatExtrForCTC(cfg)
         if not skip_loading_weights:
-            print(f"Note: pretrained weights for {wav2vec_checkpoint} are not downloadable offline; "
-                  "load them with load_state_dict / --from_checkpoint")
+            _load_or_note(self.w2v_encoder, wav2vec_checkpoint)
         if head is not None or pre_w2v_head_for_additional_loss is not None:
             raise NotImplementedError("head / pre_w2v_head_for_additional_loss are not on the b2p2t_gru+w2v path")
         self.head = None
