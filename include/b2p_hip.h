@@ -253,6 +253,17 @@ int b2p_ctc_greedy_wer(const float* logits, int64_t B, int64_t T, int64_t C, con
 int b2p_ctc_greedy_cer(const float* logits, int64_t B, int64_t T, int64_t C, const int64_t* target, int64_t S,
                        int blank, int eos, int delim, const uint8_t* tok_chars, const int32_t* tok_len,
                        int32_t* char_errs, int32_t* nchars, b2p_stream_t stream);
+/* CTC prefix beam search without a language model (csrc/beam.hip; the LM-free part of the
+ * reference's pyctcdecode test decode, src/train/evaluator.py:189-210): logits (B, T, C) raw scores
+ * (log-softmax applied per frame), lens (B) frames to decode per sample (NULL: T), beam width
+ * <= 128, C <= 64; characters below token_min_logp are skipped unless they are the frame's argmax,
+ * candidates below best + beam_prune_logp dropped. workspace: b2p_ctc_beam_workspace(B, T, beam)
+ * int32. Outputs: out_tokens (B, T) collapsed token ids of the best prefix (-1 padded), out_len (B),
+ * out_score (B) its log probability (log p_b + p_nb). */
+int64_t b2p_ctc_beam_workspace(int64_t B, int64_t T, int64_t beam);
+int b2p_ctc_prefix_beam(const float* logits, int64_t B, int64_t T, int64_t C, const int32_t* lens, int64_t beam,
+                        int blank, float token_min_logp, float beam_prune_logp, int32_t* workspace,
+                        int32_t* out_tokens, int32_t* out_len, float* out_score, b2p_stream_t stream);
 
 /* Grouped positional conv of wav2vec2 on bf16 MFMA (csrc/posconv16.hip; 48 channels per group,
  * 128 taps, padding 64 + SamePad, T <= 256), replacing the implicit-conv GEMMs of

@@ -113,3 +113,40 @@ def test_ctc_greedy_cer_matches_host_evaluator(tmp_path):
     assert errs.cpu().tolist() == errs_ref
     assert nch.cpu().tolist() == n_ref
     assert abs(float(cer) - sum(errs_ref) / sum(n_ref)) < 1e-6
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("beam,tmin,prune", [(16, -5.0, -10.0), (48, -1e30, -1e30), (1, -5.0, -10.0)])
+def test_ctc_prefix_beam_matches_oracle(beam, tmin, prune):
+    """Device prefix beam search (csrc/beam.hip) == its CPU restatement (oracle/ctc_beam_oracle.py):
+    same best prefix and log probability, with and without pyctcdecode's pruning, ragged lengths."""
+    from wav2vec2forbrain_amd import functional as Fn
+    from oracle.ctc_beam_oracle import ctc_prefix_beam
+    g = torch.Generator().manual_seed(5)
+    B, T, C = 6, 50, 32
+    logits = torch.randn(B, T, C, generator=g) * 2.5
+    logits[:, :, 0] += 2.0            # blank-heavy, as CTC outputs are
+    lens = torch.tensor([50, 47, 31, 50, 1, 0], dtype=torch.int32)
+    tok, n, score = Fn.ctc_prefix_beam(logits.cuda(), lens.cuda(), beam=beam, token_min_logp=tmin,
+                                       beam_prune_logp=prune)
+    tok, n, score = tok.cpu().numpy(), n.cpu().numpy(), score.cpu().numpy()
+    for b in range(B):
+        ref, ref_score = ctc_prefix_beam(logits[b].numpy(), beam, 0, tmin, prune, int(lens[b]))
+        assert tuple(tok[b, :n[b]]) == ref, (b, tok[b, :n[b]], ref)
+        assert (tok[b, n[b]:] == -1).all()
+        assert abs(float(score[b]) - float(ref_score)) <= 1e-4 * max(1.0, abs(float(ref_score))), (b, score[b], ref_score)
+
+
+@pytest.mark.gpu
+def test_ctc_prefix_beam_peaked_path_equals_greedy():
+    """With one dominant class per frame the beam search returns the greedy (collapsed) path."""
+    from wav2vec2forbrain_amd import functional as Fn
+    g = torch.Generator().manual_seed(6)
+    B, T, C = 3, 40, 32
+    ids = torch.randint(0, C, (B, T), generator=g)
+    logits = torch.full((B, T, C), -8.0)
+    logits.scatter_(2, ids.unsqueeze(-1), 8.0)
+    tok, n, _ = Fn.ctc_prefix_beam(logits.cuda(), beam=8)
+    for b in range(B):
+        col = [int(v) for i, v in enumerate(ids[b]) if (i == 0 or v != ids[b, i - 1]) and v != 0]
+        assert list(tok[b, :n[b]].cpu().numpy()) == col

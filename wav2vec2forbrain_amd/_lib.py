@@ -113,6 +113,8 @@ _SIGS = {
     "b2p_adam_recs": (c_i32, [c_p, c_i32, c_f32, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_p, c_p]),
     "b2p_set_seed_epoch": (c_i32, [c_p]),
     "b2p_ctc_greedy_wer": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p]),
+    "b2p_ctc_beam_workspace": (c_i64, [c_i64, c_i64, c_i64]),
+    "b2p_ctc_prefix_beam": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_f32, c_f32, c_p, c_p, c_p, c_p, c_p]),
     "b2p_ctc_greedy_cer": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "b2p_transpose_bf16": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_posconv16_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),

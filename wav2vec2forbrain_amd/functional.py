@@ -1743,6 +1743,25 @@ def ctc_greedy_wer(logits, targets, blank=0, eos=2, delim=4):
     return wer, errs, nw, tok, ntok
 
 
+def ctc_prefix_beam(logits, lens=None, beam=100, blank=0, token_min_logp=-5.0, beam_prune_logp=-10.0):
+    """LM-free CTC prefix beam search on the device (csrc/beam.hip): the decoding of the reference's
+    test evaluator (pyctcdecode via Wav2Vec2ProcessorWithLM, src/train/evaluator.py:189-210) without
+    its KenLM model. logits (B, T, C) raw scores; lens (B,) frames per sample (None: T); defaults are
+    pyctcdecode's beam width / pruning constants. Returns (tokens (B, T) int32, -1 padded; lengths
+    (B,) int32; log probabilities (B,) of the best prefixes)."""
+    _chk(logits, "ctc_prefix_beam.logits")
+    B, T, C = logits.shape
+    dev = logits.device
+    lens32 = None if lens is None else lens.to(device=dev, dtype=torch.int32).contiguous()
+    ws = torch.empty(int(_lib.load().b2p_ctc_beam_workspace(B, T, beam)), device=dev, dtype=torch.int32)
+    tok = torch.empty(B, T, device=dev, dtype=torch.int32)
+    n = torch.empty(B, device=dev, dtype=torch.int32)
+    score = torch.empty(B, device=dev)
+    _lib.call("b2p_ctc_prefix_beam", _p(logits), B, T, C, _p(lens32), beam, blank, float(token_min_logp),
+              float(beam_prune_logp), _p(ws), _p(tok), _p(n), _p(score), _st())
+    return tok, n, score
+
+
 _TOKCHARS: dict = {}
 
 

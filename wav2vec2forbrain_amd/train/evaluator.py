@@ -163,11 +163,35 @@ class EvaluatorWithW2vLMDecoder(DefaultEvaluator):
                  processor_checkpoint: str = "", track_non_test_predictions: bool = False,
                  lm_decode_test_predictions: bool = False, lm_decode_beam_width=None, lm_decode_beam_prune_logp=None,
                  lm_decode_token_min_logp=None, lm_decode_alpha=None, lm_decode_beta=None,
-                 lm_decode_score_boundary=None):
+                 lm_decode_score_boundary=None, beam_decode_test_predictions: bool = False):
         super().__init__(tokenizer, mode, track_non_test_predictions)
+        # LM-free CTC prefix beam search on the device (csrc/beam.hip) with the LM decode's beam width /
+        # pruning: test-mode metrics word/char_error_rate_beam_decode (the LM decode needs hub assets)
+        self.beam_decode = bool(beam_decode_test_predictions)
+        self.beam_cfg = dict(beam=lm_decode_beam_width or 100,
+                             beam_prune_logp=-10.0 if lm_decode_beam_prune_logp is None else lm_decode_beam_prune_logp,
+                             token_min_logp=-5.0 if lm_decode_token_min_logp is None else lm_decode_token_min_logp)
         if lm_decode_test_predictions and mode == "test":
             raise NotImplementedError(
                 f"LM decoding needs Wav2Vec2ProcessorWithLM.from_pretrained({processor_checkpoint!r}) and its KenLM "
                 "model, which are not available offline")
         self.lm_decode_beam_width = lm_decode_beam_width
         self.lm_decode_alpha, self.lm_decode_beta = lm_decode_alpha, lm_decode_beta
+
+    def beam_decode_predictions(self, predictions: ModelOutput) -> list[str]:
+        """Best prefixes of the device beam search as strings (cut after </s>, like the greedy path)."""
+        from .. import functional as Fn
+        blank, _, _ = _ids(self.tokenizer)
+        tok, n, _ = Fn.ctc_prefix_beam(predictions.logits.detach().float().contiguous(), predictions.logit_lens,
+                                       blank=blank, **self.beam_cfg)
+        tok, n = tok.cpu().numpy(), n.cpu().numpy()
+        return [cut_after_eos_token(self.tokenizer.decode(list(tok[b, :n[b]]), group_tokens=False))
+                for b in range(tok.shape[0])]
+
+    def _track_batch(self, predictions: ModelOutput, sample) -> float:
+        if self.beam_decode and self.mode == "test" and sample.target is not None and predictions.logits.is_cuda:
+            labels = self.tokenizer.batch_decode(sample.target.cpu().numpy(), group_tokens=False)
+            pred = self.beam_decode_predictions(predictions)
+            predictions.metrics.update({"word_error_rate_beam_decode": word_error_rate(pred, labels),
+                                        "char_error_rate_beam_decode": char_error_rate(pred, labels)})
+        return super()._track_batch(predictions, sample)
