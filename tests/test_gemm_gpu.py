@@ -412,3 +412,31 @@ def test_auto16_staged_operands(fwd16, M, N, K):
                 assert (outs[0] - outs[1]).abs().max().item() <= 1e-4 * scale
     finally:
         Fn._AUTO16 = old
+
+
+def test_scalar_epilogue_odd_n():
+    """N % 4 != 0 takes the scalar epilogue (epilogue_store): bias, act' on an fp32 aux, residual,
+    C16 copy against torch; the bf16-only extensions (pre16 / aux16 / colsum_part) refuse such shapes
+    with an error instead of reading past the rows (advisor round 1)."""
+    Fn = _fn()
+    torch.manual_seed(8)
+    M, N, K = 77, 262, 96
+    a = torch.randn(M, K, device="cuda")
+    w = torch.randn(N, K, device="cuda")
+    bias = torch.randn(N, device="cuda")
+    aux = torch.randn(M, N, device="cuda")
+    res = torch.randn(M, N, device="cuda")
+    c = torch.empty(M, N, device="cuda")
+    c16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    with Fn.precision("fp32"):
+        Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), c, N, bias=bias, act_bwd=Fn.ACT["gelu"], aux=aux,
+                residual=res, C16=c16)
+    x = aux.clone().requires_grad_(True)
+    gl = torch.autograd.grad(F.gelu(x).sum(), x)[0]
+    ref = (a @ w.t() + bias) * gl + res
+    _close(c, ref, "fp32")
+    assert torch.equal(c16, c.to(torch.bfloat16))
+    a16, w16 = a.to(torch.bfloat16), w.to(torch.bfloat16)
+    pre16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(RuntimeError):
+        Fn.gemm(M, N, K, Fn.op(a16, 0, K, True), Fn.op(w16, 0, K, True), None, N, pre16=pre16, C16=c16)

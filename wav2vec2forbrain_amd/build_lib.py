@@ -38,7 +38,7 @@ def _compile(src: str, hmt: float, verbose: bool) -> str:
     if audit:   # per-kernel resource usage (VGPRs, LDS, scratch) saved beside the object
         cmd.append("-Rpass-analysis=kernel-resource-usage")
     if verbose:
-        print(f"build_lib: hipcc {os.path.basename(src)}", flush=True)
+        print(f"build_lib: hipcc {os.path.basename(src)}", file=sys.stderr, flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src}:\n{r.stdout}\n{r.stderr}")
@@ -59,7 +59,7 @@ def build(verbose: bool = False, jobs: int | None = None) -> str:
         t0 = time.perf_counter()
         path = _build_locked(verbose, jobs)
         if verbose:
-            print(f"build_lib: {path} ready in {time.perf_counter() - t0:.1f} s", flush=True)
+            print(f"build_lib: {path} ready in {time.perf_counter() - t0:.1f} s", file=sys.stderr, flush=True)
         return path
 
 
@@ -83,7 +83,7 @@ def _build_locked(verbose: bool, jobs: int | None) -> str:
     tmp = LIB + ".tmp"
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:
-        print(" ".join(cmd), flush=True)
+        print(" ".join(cmd), file=sys.stderr, flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
