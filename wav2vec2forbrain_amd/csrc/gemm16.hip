@@ -265,6 +265,8 @@ struct Cfg {
 };
 using CfgSmall = Cfg<128, 128, 32, 3>;   // 4 waves, 2 workgroups/CU (default)
 using CfgSmall64 = Cfg<128, 128, 64, 2>; // 4 waves, 2 workgroups/CU, half the barriers (small grids)
+using CfgN64 = Cfg<128, 64, 32, 3>;     // 2 waves, 128 x 64 tiles: twice the workgroups for N <= 1024 grids
+                                         // (k-contiguous operands only: the mn-contiguous swizzle needs 128)
 using CfgSmall4 = Cfg<128, 128, 32, 4>; // 4 waves, 2 workgroups/CU, 3 k-tiles in flight (B2P_GEMM16_S4=1)
 using CfgBig = Cfg<256, 128, 64, 3>;     // 8 waves, 1 workgroup/CU (measured slower on the step's shapes:
                                          // lock-stepped waves leave the MFMA pipe idle at every barrier)
@@ -673,6 +675,20 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   // replay, side stream beside): B2P_GEMM16_K64 = 0 never (default), 1 always, -1 by grid size.
   static int k64 = getenv("B2P_GEMM16_K64") ? atoi(getenv("B2P_GEMM16_K64")) : 0;
   const bool use64 = k64 == 1 || (k64 < 0 && nwg <= 512);
+  // narrow grids (N = 768 / 1024 projections: 378-504 tiles of 128 x 128 for 256 CUs) on 128 x 64 tiles:
+  // B2P_GEMM16_N64 = 1 when the 128 x 128 grid has < 512 tiles (default 0: measured slower, 59.3 -> 57.1
+  // steps/s on the base step; the 2-wave workgroups hide less latency than the 4-wave 128 x 128 ones)
+  static int n64 = getenv("B2P_GEMM16_N64") ? atoi(getenv("B2P_GEMM16_N64")) : 0;
+  if (n64 && d.A.inner_is_k && d.B.inner_is_k && !d.A.conv && nwg < 512 && d.N <= 1024 &&
+      (ks == 1 || d.kchunk % 32 == 0)) {
+    const int tn64 = (int)((d.N + 63) / 64);
+    const dim3 grid((unsigned)((int64_t)tm * tn64 * nz)), block(CfgN64::NT);
+    if (h16) hipLaunchKernelGGL((gemm16_kernel<CfgN64, true, true, false, true>), grid, block, 0, st, d, ea, tm, tn64,
+                                gemm16_group(false));
+    else hipLaunchKernelGGL((gemm16_kernel<CfgN64, true, true, false>), grid, block, 0, st, d, ea, tm, tn64,
+                            gemm16_group(false));
+    return 0;
+  }
   static int s4 = getenv("B2P_GEMM16_S4") ? atoi(getenv("B2P_GEMM16_S4")) : 0;
   if (use64 && !h16 && (ks == 1 || d.kchunk % 64 == 0)) launch_cfg<CfgSmall64>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   else if (s4) launch_cfg<CfgSmall4>(d, ea, st, dim3((unsigned)nwg), tm, tn);
