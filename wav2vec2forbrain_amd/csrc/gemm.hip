@@ -485,8 +485,15 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   if (rc) return rc;
   if (d.ksplit > 1) {
     const int64_t total = (int64_t)d.nz1 * d.nz2 * d.M * d.N;
-    hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d.workspace,
-                       d.ksplit, d.M, d.N, d.nz2, d.ep, total);
+    const b2p_epilogue& e = d.ep;
+    const bool v4 = d.N % 4 == 0 && e.ldc % 4 == 0 && e.cbs1 % 4 == 0 && e.cbs2 % 4 == 0 &&
+                    ((uintptr_t)e.C & 15u) == 0 && ((uintptr_t)e.C16 & 7u) == 0 && ((uintptr_t)d.workspace & 15u) == 0;
+    if (v4)
+      hipLaunchKernelGGL(splitk_reduce4, dim3((unsigned)((total / 4 + 255) / 256)), dim3(256), 0, st, d.workspace,
+                         d.ksplit, d.M, d.N, d.nz2, d.ep, total / 4);
+    else
+      hipLaunchKernelGGL(splitk_reduce, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, d.workspace,
+                         d.ksplit, d.M, d.N, d.nz2, d.ep, total);
   }
   B2P_CHECK_LAUNCH();
   b2p_timing_end(d.timing_family, st, d.flops);

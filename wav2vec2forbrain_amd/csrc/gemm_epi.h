@@ -136,6 +136,31 @@ __global__ void splitk_reduce(const float* __restrict__ ws, int ks, int64_t M, i
   if (e.C16) e.C16[coff] = b2p_16_bits(v, e.flags & B2P_EPI_C16_FP16);
 }
 
+// the same with 4 consecutive columns per thread (N % 4 == 0, ldc % 4 == 0, cbs % 4 == 0, C 16-B and
+// C16 8-B aligned): 16-B slab loads, 4x fewer instructions per byte
+__global__ void __launch_bounds__(256) splitk_reduce4(const float* __restrict__ ws, int ks, int64_t M, int64_t N,
+                                                      int nz2, b2p_epilogue e, int64_t total4) {
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i4 >= total4) return;
+  const int64_t MN = M * N, i = 4 * i4;
+  const int64_t z = i / MN, r = i - z * MN;
+  const int64_t m = r / N, n = r - m * N;
+  const float* p = ws + z * ks * MN + r;
+  float4 s = *reinterpret_cast<const float4*>(p);
+  for (int q = 1; q < ks; ++q) {
+    const float4 v = *reinterpret_cast<const float4*>(p + (int64_t)q * MN);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const int64_t z1 = z / nz2, z2 = z - z1 * nz2;
+  const int64_t coff = z1 * e.cbs1 + z2 * e.cbs2 + m * e.ldc + n;
+  float4 v = make_float4(e.alpha * s.x, e.alpha * s.y, e.alpha * s.z, e.alpha * s.w);
+  if (e.beta != 0.f) {
+    const float4 c = *reinterpret_cast<const float4*>(e.C + coff);
+    v.x += e.beta * c.x; v.y += e.beta * c.y; v.z += e.beta * c.z; v.w += e.beta * c.w;
+  }
+  if (e.C) *reinterpret_cast<float4*>(e.C + coff) = v;
+  if (e.C16) *reinterpret_cast<uint2*>(e.C16 + coff) = b2p_pack16x4(v, e.flags & B2P_EPI_C16_FP16);
+}
 
 inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
   EpiArgs ea;
