@@ -415,7 +415,7 @@ int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t se
 /* Output-dropout backward of a Conformer block in one pass (replaces b2p_dropout_scaled + a bf16
  * cast + b2p_colsum of its result; reference TF conf Wav2Vec2ConformerFeedForward / SelfAttention /
  * ConvolutionModule output dropout): y16 = bf16(mask(x) * scale / (1 - p)) over M x N (N % 4 == 0),
- * and when part != NULL the per-256-row column partial sums of those fp32 values,
+ * and when part != NULL the per-64-row column partial sums of those fp32 values,
  * part[b2p_drop_cast_colsum_parts(M)][N] (finish with b2p_colsum_parts). Same mask as
  * b2p_dropout_scaled. */
 int64_t b2p_drop_cast_colsum_parts(int64_t M);

@@ -88,6 +88,37 @@ __global__ void act_drop_cast16_k(const float* __restrict__ pre, uint16_t* __res
   reinterpret_cast<uint2*>(out)[i4] = b2p_pack_bf16x4(make_float4(v[0], v[1], v[2], v[3]));
 }
 
+// b2p_rotary with 4 consecutive d per thread (D % 8 == 0, 16-B aligned rows): forward and transpose
+__global__ void rotary4_k(const float* __restrict__ x, const float* __restrict__ ct, const float* __restrict__ st,
+                          float* __restrict__ out, int64_t rows, int T, int H, int D, int64_t ld, int inverse) {
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int D4 = D / 4;
+  if (i4 >= rows * H * D4) return;
+  const int d = (int)(i4 % D4) * 4;
+  const int h = (int)((i4 / D4) % H);
+  const int64_t r = i4 / ((int64_t)D4 * H);
+  const int t = (int)(r % T);
+  const float* xr = x + r * ld + (int64_t)h * D;
+  const int half = D / 2;
+  const int od = d < half ? d + half : d - half;
+  const float4 xv = *reinterpret_cast<const float4*>(xr + d);
+  const float4 ov = *reinterpret_cast<const float4*>(xr + od);
+  const float4 c = *reinterpret_cast<const float4*>(ct + (int64_t)t * D + d);
+  float4 v;
+  if (!inverse) {   // x*cos + rotate_half(x)*sin, rotate_half = cat(-x2, x1)
+    const float4 sn = *reinterpret_cast<const float4*>(st + (int64_t)t * D + d);
+    const float sg = d < half ? -1.f : 1.f;
+    v = make_float4(xv.x * c.x + sg * ov.x * sn.x, xv.y * c.y + sg * ov.y * sn.y, xv.z * c.z + sg * ov.z * sn.z,
+                    xv.w * c.w + sg * ov.w * sn.w);
+  } else {          // dx[d] = dy[d] cos[d] + (d < half ? dy[d+half] sin[d+half] : -dy[d-half] sin[d-half])
+    const float4 so = *reinterpret_cast<const float4*>(st + (int64_t)t * D + od);
+    const float sg = d < half ? 1.f : -1.f;
+    v = make_float4(xv.x * c.x + sg * ov.x * so.x, xv.y * c.y + sg * ov.y * so.y, xv.z * c.z + sg * ov.z * so.z,
+                    xv.w * c.w + sg * ov.w * so.w);
+  }
+  *reinterpret_cast<float4*>(out + r * ld + (int64_t)h * D + d) = v;
+}
+
 __global__ void glu_fwd_k(const float* __restrict__ a, float* __restrict__ out, int64_t M, int64_t C) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= M * C) return;
@@ -306,11 +337,12 @@ __global__ void dropout_scale_k(const float* __restrict__ x, float* __restrict__
   y[i] = (!use_mask || b2p_keep(seed, (uint64_t)i, thr)) ? x[i] * scale : 0.f;
 }
 
+constexpr int DCC_ROWS = 64;   // rows per block (~1000 blocks over an 8k x 1024 tensor: enough loads in flight)
 // y16 = bf16(mask(x) * scale) over an M x N row-major tensor (N % 4 == 0, 16-B aligned rows), plus
-// optional per-256-row column partial sums of the fp32 values, part[blk][n] (the bias gradient of
+// optional per-DCC_ROWS-row column partial sums of the fp32 values, part[blk][n] (the bias gradient of
 // the Linear that produced x; b2p_colsum_parts finishes it): the output-dropout backward of a
 // Conformer block (dropout, its bf16 GEMM operand and its bias gradient in one pass over dy).
-// Grid (ceil(N/128), ceil(M/256)); 32 float4 columns x 8 row lanes per block; mask index = m*N + n,
+// Grid (ceil(N/128), ceil(M/DCC_ROWS)); 32 float4 columns x 8 row lanes per block; mask index = m*N + n,
 // the element index dropout_scale_k and the forward GEMM epilogue use.
 __global__ void __launch_bounds__(256) drop_cast_colsum_k(const float* __restrict__ x, uint16_t* __restrict__ y16,
                                                           float* __restrict__ part, int64_t M, int64_t N, uint32_t thr,
@@ -319,8 +351,8 @@ __global__ void __launch_bounds__(256) drop_cast_colsum_k(const float* __restric
   __shared__ float4 red[8][32];
   const int c4 = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int64_t n = (int64_t)blockIdx.x * 128 + 4 * c4;
-  const int64_t m0 = (int64_t)blockIdx.y * 256;
-  const int64_t m1 = m0 + 256 < M ? m0 + 256 : M;
+  const int64_t m0 = (int64_t)blockIdx.y * DCC_ROWS;
+  const int64_t m1 = m0 + DCC_ROWS < M ? m0 + DCC_ROWS : M;
   seed = b2p_seed_eff(seed, epoch);
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (n < N) {
@@ -362,8 +394,12 @@ extern "C" int b2p_rotary(const float* x, const float* cos_t, const float* sin_t
   B2P_CHECK_ARG(D % 2 == 0, "rotary: head dim must be even");
   const int64_t n = B * T * H * D;
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(rotary_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, cos_t, sin_t, out, B * T, (int)T,
-                     (int)H, (int)D, ld, inverse);
+  if (D % 8 == 0 && ld % 4 == 0 && ((uintptr_t)x & 15u) == 0 && ((uintptr_t)out & 15u) == 0)
+    hipLaunchKernelGGL(rotary4_k, dim3(nblk(n / 4)), dim3(256), 0, (hipStream_t)stream, x, cos_t, sin_t, out, B * T,
+                       (int)T, (int)H, (int)D, ld, inverse);
+  else
+    hipLaunchKernelGGL(rotary_k, dim3(nblk(n)), dim3(256), 0, (hipStream_t)stream, x, cos_t, sin_t, out, B * T,
+                       (int)T, (int)H, (int)D, ld, inverse);
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -566,7 +602,7 @@ extern "C" int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, 
   return 0;
 }
 
-extern "C" int64_t b2p_drop_cast_colsum_parts(int64_t M) { return M > 0 ? (M + 255) / 256 : 0; }
+extern "C" int64_t b2p_drop_cast_colsum_parts(int64_t M) { return M > 0 ? (M + DCC_ROWS - 1) / DCC_ROWS : 0; }
 
 extern "C" int b2p_drop_cast_colsum(const float* x, uint16_t* y16, float* part, int64_t M, int64_t N, float p,
                                     uint64_t seed, float scale, b2p_stream_t stream) {
@@ -576,7 +612,7 @@ extern "C" int b2p_drop_cast_colsum(const float* x, uint16_t* y16, float* part, 
                     ((uintptr_t)part & 15u) == 0,
                 "drop_cast_colsum: needs N % 4 == 0, 16-B aligned x / part, 8-B aligned y16");
   if (M <= 0 || N <= 0) return 0;
-  const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + 255) / 256));
+  const dim3 grid((unsigned)((N + 127) / 128), (unsigned)((M + DCC_ROWS - 1) / DCC_ROWS));
   hipLaunchKernelGGL(drop_cast_colsum_k, grid, dim3(256), 0, (hipStream_t)stream, x, y16, part, M, N,
                      b2p_dropout_threshold(p), p > 0.f ? scale / (1.f - p) : scale, seed, p > 0.f ? 1 : 0,
                      b2p_seed_epoch());

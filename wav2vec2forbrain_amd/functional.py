@@ -20,6 +20,7 @@ import functools
 import ctypes
 import math
 import threading
+import weakref
 
 import os
 
@@ -658,8 +659,23 @@ def bump_param_epoch(params) -> None:
         _PARAM_EPOCH[id(p)] = _PARAM_EPOCH.get(id(p), 0) + 1
 
 
+class _Stamp:
+    """Identity + content stamp of the source weights of a cached 16-bit copy. Weak references make
+    a freed weight a miss even when a new tensor reuses its id, storage and version counter (models
+    built one after another in one process)."""
+    __slots__ = ("key", "refs")
+
+    def __init__(self, ws):
+        self.key = tuple((id(w), w.data_ptr(), tuple(w.shape), w._version, _PARAM_EPOCH.get(id(w), 0)) for w in ws)
+        self.refs = tuple(weakref.ref(w) for w in ws)
+
+    def __eq__(self, other):
+        return (isinstance(other, _Stamp) and self.key == other.key
+                and all(a() is not None and a() is b() for a, b in zip(self.refs, other.refs)))
+
+
 def _stamp(ws):
-    return tuple((id(w), w.data_ptr(), tuple(w.shape), w._version, _PARAM_EPOCH.get(id(w), 0)) for w in ws)
+    return _Stamp(ws)
 
 
 def _cache_ok(ws) -> bool:
