@@ -422,9 +422,11 @@ int64_t b2p_drop_cast_colsum_parts(int64_t M);
 int b2p_drop_cast_colsum(const float* x, uint16_t* y16, float* part, int64_t M, int64_t N, float p, uint64_t seed,
                          float scale, b2p_stream_t stream);
 /* LayerNorm forward (TF conf / TF w2v nn.LayerNorm) writing the 16-bit GEMM operand copy y16 (fp16 when
- * y16_fp16, else bf16); y (fp32) may be NULL. No dropout. */
+ * y16_fp16, else bf16) and optionally a bf16 copy y16b (the backward's weight-gradient operand);
+ * y (fp32) may be NULL. No dropout. */
 int b2p_layernorm_fwd_x16(const float* x, const float* gamma, const float* beta, float* y, uint16_t* y16, int y16_fp16,
-                          float* mean, float* rstd, int64_t rows, int64_t cols, float eps, b2p_stream_t stream);
+                          uint16_t* y16b, float* mean, float* rstd, int64_t rows, int64_t cols, float eps,
+                          b2p_stream_t stream);
 /* Forward rotary embedding (as b2p_rotary, inverse 0) written as a 16-bit operand (fp16 when fp16). */
 int b2p_rotary16(const float* x, const float* cos_t, const float* sin_t, uint16_t* out, int fp16, int64_t B, int64_t T,
                  int64_t H, int64_t D, int64_t ld, b2p_stream_t stream);
@@ -445,6 +447,9 @@ int b2p_rotary(const float* x, const float* cos_t, const float* sin_t, float* ou
 int b2p_glu_fwd(const float* a, float* out, int64_t M, int64_t C, b2p_stream_t stream);
 int b2p_glu_bwd(const float* a, const float* dout, float* da, int64_t M, int64_t C,
                 b2p_stream_t stream);
+/* GLU backward (TF conf Wav2Vec2ConformerConvolutionModule nn.GLU(dim=1)) written as the bf16 operand
+ * of the pointwise-conv-1 backward GEMMs: da16 (M, 2C), C % 4 == 0. */
+int b2p_glu_bwd16(const float* a, const float* dout, uint16_t* da16, int64_t M, int64_t C, b2p_stream_t stream);
 /* depthwise Conv1d(C, C, K, padding=(K-1)/2, groups=C, bias=False), channels-last (B, T, C);
  * w (C, K). Backward writes dx and/or dw (deterministic partial sums). */
 int b2p_dwconv_fwd(const float* x, const float* w, float* y, int64_t B, int64_t T, int64_t C,

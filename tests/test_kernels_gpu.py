@@ -705,10 +705,21 @@ def test_conformer_16bit_producers():
     g, b = 1 + 0.1 * torch.randn(D, device="cuda"), 0.1 * torch.randn(D, device="cuda")
     ref = F.layer_norm(x, (D,), g, b, 1e-5)
     for half in (True, False):
-        y, y16, mean, rstd = Fn._ln_fwd_x16(x, g, b, 1e-5, half)
+        y, y16, mean, rstd, y16b = Fn._ln_fwd_x16(x, g, b, 1e-5, half, want_b16=True)
         assert y16.dtype == (torch.float16 if half else torch.bfloat16)
         assert _rel(y.cpu(), ref.cpu()) < 1e-5
         assert torch.equal(y16, y.to(y16.dtype))        # the copy is the RNE rounding of y
+        assert torch.equal(y16b, y.to(torch.bfloat16))
+        _, y16n, _, _ = Fn._ln_fwd_x16(x, g, b, 1e-5, half, want32=False)   # no fp32 output
+        assert torch.equal(y16n, y16)
+    # GLU backward written as bf16 == bf16(b2p_glu_bwd)
+    a = torch.randn(M, 2 * D, device="cuda")
+    du = torch.randn(M, D, device="cuda")
+    da = torch.empty(M, 2 * D, device="cuda")
+    Fn._lib.call("b2p_glu_bwd", a.data_ptr(), du.data_ptr(), da.data_ptr(), M, D, Fn._st())
+    da16 = torch.empty(M, 2 * D, device="cuda", dtype=torch.bfloat16)
+    Fn._lib.call("b2p_glu_bwd16", a.data_ptr(), du.data_ptr(), da16.data_ptr(), M, D, Fn._st())
+    assert torch.equal(da16, da.to(torch.bfloat16))
     # rotary16 == b2p_rotary (fp32) rounded
     B, T = 3, 100
     h = torch.randn(B * T, D, device="cuda")

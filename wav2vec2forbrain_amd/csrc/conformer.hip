@@ -139,6 +139,24 @@ __global__ void glu_bwd_k(const float* __restrict__ a, const float* __restrict__
   da[m * 2 * C + C + c] = d * x * s * (1.f - s);
 }
 
+// GLU backward written straight as the bf16 operand of the pointwise-conv-1 backward GEMMs, 4 channels
+// per thread (C % 4 == 0): da16[m][c] = bf16(d*s), da16[m][C + c] = bf16(d*x*s*(1-s))
+__global__ void glu_bwd16_k(const float* __restrict__ a, const float* __restrict__ dout, uint16_t* __restrict__ da16,
+                            int64_t M, int64_t C) {
+  const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t C4 = C / 4;
+  if (i4 >= M * C4) return;
+  const int64_t m = i4 / C4, c = (i4 - m * C4) * 4;
+  const float4 x = *reinterpret_cast<const float4*>(a + m * 2 * C + c);
+  const float4 g = *reinterpret_cast<const float4*>(a + m * 2 * C + C + c);
+  const float4 d = *reinterpret_cast<const float4*>(dout + m * C + c);
+  const float s0 = b2p_sigmoid(g.x), s1 = b2p_sigmoid(g.y), s2 = b2p_sigmoid(g.z), s3 = b2p_sigmoid(g.w);
+  *reinterpret_cast<uint2*>(da16 + m * 2 * C + c) = b2p_pack_bf16x4(make_float4(d.x * s0, d.y * s1, d.z * s2, d.w * s3));
+  *reinterpret_cast<uint2*>(da16 + m * 2 * C + C + c) =
+      b2p_pack_bf16x4(make_float4(d.x * x.x * s0 * (1.f - s0), d.y * x.y * s1 * (1.f - s1), d.z * x.z * s2 * (1.f - s2),
+                                  d.w * x.w * s3 * (1.f - s3)));
+}
+
 // depthwise conv, channels-last, zero 'same' padding p = (K-1)/2: y[b,t,c] = sum_k w[c,k] x[b,t+k-p,c]
 __global__ void dwconv_fwd_k(const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ y,
                              int64_t B, int64_t T, int64_t C, int K) {
@@ -643,6 +661,17 @@ extern "C" int b2p_act_dropout_cast16(const float* pre, uint16_t* out, int64_t n
   hipLaunchKernelGGL(act_drop_cast16_k, dim3(nblk(n / 4)), dim3(256), 0, (hipStream_t)stream, pre, out, n / 4, act,
                      b2p_dropout_threshold(p), p > 0.f ? 1.f / (1.f - p) : 1.f, seed, p > 0.f ? 1 : 0,
                      b2p_seed_epoch());
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_glu_bwd16(const float* a, const float* dout, uint16_t* da16, int64_t M, int64_t C,
+                             b2p_stream_t stream) {
+  B2P_CHECK_ARG(a && dout && da16, "glu_bwd16: NULL pointer");
+  B2P_CHECK_ARG(C % 4 == 0 && ((uintptr_t)a & 15u) == 0 && ((uintptr_t)dout & 15u) == 0 && ((uintptr_t)da16 & 7u) == 0,
+                "glu_bwd16: needs C %% 4 == 0 and aligned pointers");
+  if (M * C <= 0) return 0;
+  hipLaunchKernelGGL(glu_bwd16_k, dim3(nblk(M * C / 4)), dim3(256), 0, (hipStream_t)stream, a, dout, da16, M, C);
   B2P_CHECK_LAUNCH();
   return 0;
 }

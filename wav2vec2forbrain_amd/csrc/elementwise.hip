@@ -137,7 +137,8 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
                                                 float* __restrict__ mean, float* __restrict__ rstd,
                                                 int64_t rows, int cols, float eps, uint32_t thr, float dscale,
                                                 uint64_t seed, float drop_p, uint16_t* __restrict__ y16,
-                                                const uint64_t* __restrict__ epoch, int y16_half = 0) {
+                                                const uint64_t* __restrict__ epoch, int y16_half = 0,
+                                                uint16_t* __restrict__ y16b = nullptr) {
   seed = b2p_seed_eff(seed, epoch);
   const int lane = threadIdx.x & 63;
   const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -188,6 +189,7 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
       }
       if (y) yr[c] = o;
       if (y16) reinterpret_cast<uint2*>(y16 + row * cols)[c] = b2p_pack16x4(o, y16_half);
+      if (y16b) reinterpret_cast<uint2*>(y16b + row * cols)[c] = b2p_pack_bf16x4(o);
     }
   }
 }
@@ -546,15 +548,16 @@ extern "C" int b2p_layernorm_fwd16(const float* x, const float* gamma, const flo
 }
 
 extern "C" int b2p_layernorm_fwd_x16(const float* x, const float* gamma, const float* beta, float* y, uint16_t* y16,
-                                     int y16_fp16, float* mean, float* rstd, int64_t rows, int64_t cols, float eps,
-                                     b2p_stream_t stream) {
+                                     int y16_fp16, uint16_t* y16b, float* mean, float* rstd, int64_t rows,
+                                     int64_t cols, float eps, b2p_stream_t stream) {
   B2P_CHECK_ARG(x && gamma && beta && y16 && mean && rstd, "layernorm_fwd_x16: NULL pointer");
   B2P_CHECK_ARG(cols % 4 == 0 && cols <= 64 * 4 * LN_MAXV, "layernorm_fwd_x16: cols must be %%4 and <= 1024");
-  B2P_CHECK_ARG(((uintptr_t)y16 & 7u) == 0, "layernorm_fwd_x16: y16 must be 8-byte aligned");
+  B2P_CHECK_ARG(((uintptr_t)y16 & 7u) == 0 && ((uintptr_t)y16b & 7u) == 0,
+                "layernorm_fwd_x16: y16 / y16b must be 8-byte aligned");
   if (rows <= 0) return 0;
   hipLaunchKernelGGL(ln_fwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, y,
                      mean, rstd, rows, (int)cols, eps, 0u, 1.f, (uint64_t)0, 0.f, y16, b2p_seed_epoch(),
-                     y16_fp16 ? 1 : 0);
+                     y16_fp16 ? 1 : 0, y16b);
   B2P_CHECK_LAUNCH();
   return 0;
 }

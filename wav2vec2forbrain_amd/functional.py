@@ -1863,15 +1863,19 @@ def _drop_cast_colsum(dy, p, seed, scale, want_colsum):
     return y16, (colsum_from_parts(parts, torch.empty(N, device=dy.device)) if want_colsum else None)
 
 
-def _ln_fwd_x16(x2d, g, b, eps, half):
-    """LayerNorm (fp32 y, mean, rstd) plus its 16-bit GEMM operand copy (fp16 when half) in one pass."""
+def _ln_fwd_x16(x2d, g, b, eps, half, want32=True, want_b16=False):
+    """LayerNorm (fp32 y unless want32=False, mean, rstd) plus its 16-bit GEMM operand copy (fp16 when
+    half) in one pass; want_b16 adds a bf16 copy (the backward's weight-gradient operand) as a 5th value."""
     rows, cols = x2d.shape
-    y = torch.empty_like(x2d)
+    y = torch.empty_like(x2d) if want32 else None
     y16 = torch.empty(rows, cols, device=x2d.device, dtype=torch.float16 if half else BF16)
+    y16b = torch.empty(rows, cols, device=x2d.device, dtype=BF16) if want_b16 else None
     mean = torch.empty(rows, device=x2d.device)
     rstd = torch.empty(rows, device=x2d.device)
-    _lib.call("b2p_layernorm_fwd_x16", _p(x2d), _p(g), _p(b), _p(y), _p(y16), int(half), _p(mean), _p(rstd), rows,
-              cols, float(eps), _st())
+    _lib.call("b2p_layernorm_fwd_x16", _p(x2d), _p(g), _p(b), _p(y), _p(y16), int(half), _p(y16b), _p(mean),
+              _p(rstd), rows, cols, float(eps), _st())
+    if want_b16:
+        return y, y16, mean, rstd, y16b
     return y, y16, mean, rstd
 
 
@@ -1919,7 +1923,11 @@ class _FFNBlock(torch.autograd.Function):
             # fp16 under forward_f16, else bf16. f exists only as that operand copy (the backward
             # recomputes its bf16 form from pre)
             half = _state.fwd16
-            h, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half)
+            if half:   # h kept only as the bf16 weight-gradient operand of the backward (no fp32 copy)
+                _, h16, mean, rstd, h = _ln_fwd_x16(x2, g, b, eps, half, want32=False, want_b16=True)
+            else:
+                _, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half, want32=False)
+                h = h16
             f = torch.empty(NT, F, device=dev, dtype=torch.float16 if half else BF16)
             w1b, w1op = _w_op16(w1, half)
             gemm(NT, F, D, op(h16, 0, D, True), w1op, None, F, bias=b1, pre_out=pre, act=act, drop_p=p_act,
@@ -1952,7 +1960,7 @@ class _FFNBlock(torch.autograd.Function):
         dev = x2.device
         ng = ctx.needs_input_grad
         dy = dy.contiguous().view(NT, D)
-        if bf16_mode():
+        if bf16_mode() or h.dtype != torch.float32:
             return _FFNBlock._backward16(ctx, dy, x2, h, mean, rstd, pre, f, g, w1, w2)
         dz = _dropout_scaled(dy, p_hid, s_hid, scale)
         dw2 = db2 = dw1 = db1 = None
@@ -1998,7 +2006,7 @@ class _FFNBlock(torch.autograd.Function):
              act_bwd=act, aux=pre, C16=dpre16, colsum_part=parts)
         if parts is not None:
             db1 = colsum_from_parts(parts, torch.empty(F, device=dev))
-        dw1 = _wgrad16(w1, ng[3], dpre16, F, cast16(h), D, NT)
+        dw1 = _wgrad16(w1, ng[3], dpre16, F, h if h.dtype == BF16 else cast16(h), D, NT)
         dh = torch.empty(NT, D, device=dev)
         gemm(NT, D, F, op(dpre16, 0, F, True), op(weight16t(w1), 0, F, True), dh, D)
         dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
@@ -2061,7 +2069,11 @@ class _ConformerAttnBlock(torch.autograd.Function):
             # the Q/K/V operands come straight from their producers as 16-bit copies (LayerNorm, rotary):
             # fp16 under forward_f16, else bf16; the fp32 rotated copy is never stored
             half = _state.fwd16
-            h, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half)
+            if half:   # fp16 operand for the forward GEMMs, bf16 copy for the V weight gradient
+                h, h16, mean, rstd, h16b = _ln_fwd_x16(x2, g, b, eps, half, want_b16=True)
+            else:
+                h, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half)
+                h16b = h16
             hr16 = _rotary16(h, cos_t, sin_t, B, T, nh, hd, half) if cos_t is not None else h16
             hr = None
             for i, (w, bb, src) in enumerate(((wq, bq, hr16), (wk, bk, hr16), (wv, bv, h16))):
@@ -2073,6 +2085,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
                 del wbuf
             del h16, hr16
         else:
+            h16b = None
             h, mean, rstd = _ln_fwd(x2, g, b, eps)
             if cos_t is not None:
                 hr = torch.empty_like(h)
@@ -2091,7 +2104,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
             gemm(NT, D, D, op(O, 0, D, True), op(wo, 0, D, True), y, D, bias=bo, drop_p=p_out, seed=seeds[1],
                  residual=x2)
         ctx.save_for_backward(x2, h, hr if (cos_t is not None and hr is not None) else None, mean, rstd, qkv, P, Pd,
-                              O, g, wq, wk, wv, wo, cos_t, sin_t)
+                              O, g, wq, wk, wv, wo, cos_t, sin_t, h16b)
         ctx.cfg = cfg
         ctx.shape = (B, T, D)
         ctx.has_b = [t is not None for t in (bq, bk, bv, bo)]
@@ -2100,7 +2113,8 @@ class _ConformerAttnBlock(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo, cos_t, sin_t = ctx.saved_tensors
+        x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo, cos_t, sin_t, h16b = ctx.saved_tensors
+        ctx.h16b = h16b
         nh, eps, p_attn, p_out, seeds = ctx.cfg
         B, T, D = ctx.shape
         NT, hd = B * T, D // nh
@@ -2170,7 +2184,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
             dqkv = _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, hd, p_attn, seeds[0])
             del dO
             dqkv16 = cast16(dqkv)
-        h16 = cast16(h)
+        h16 = ctx.h16b if ctx.h16b is not None else cast16(h)
         if cos_t is None:
             hr16 = h16
         elif hr is None:   # the forward kept no fp32 rotated copy: rotate h again, into bf16
@@ -2267,7 +2281,11 @@ class _ConvModule(torch.autograd.Function):
         a = torch.empty(NT, 2 * D, device=dev)
         if bf16_mode():   # the pointwise-conv operand written by the LayerNorm (fp16 under forward_f16)
             half = _state.fwd16
-            h, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half)
+            if half:      # h kept only as the bf16 operand of the pw1 weight gradient
+                _, h16, mean, rstd, h = _ln_fwd_x16(x2, g, b, eps, half, want32=False, want_b16=True)
+            else:
+                _, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half, want32=False)
+                h = h16
             wbuf, wop = _w_op16(w_pw1, half)
             gemm(NT, 2 * D, D, op(h16, 0, D, True), wop, a, 2 * D)
             del h16, wbuf
@@ -2315,7 +2333,7 @@ class _ConvModule(torch.autograd.Function):
         dev = x2.device
         ng = ctx.needs_input_grad
         dy = dy.contiguous().view(NT, D)
-        b16 = bf16_mode()   # bf16 operands: each cast once, frozen weight gradients deferred
+        b16 = bf16_mode() or h.dtype != torch.float32   # bf16 operands: each cast once, frozen wgrads deferred
         ds = torch.empty(NT, D, device=dev)
         if b16:
             do16, _ = _drop_cast_colsum(dy, p, seed, 1.0, False)
@@ -2342,14 +2360,15 @@ class _ConvModule(torch.autograd.Function):
         ddw = torch.empty_like(w_dw) if ng[4] else None
         wsd = torch.empty(int(_lib.load().b2p_dwconv_bwd_workspace(B, T, D, K)), device=dev)
         _lib.call("b2p_dwconv_bwd", _p(u), _p(w_dw), _p(dc), _p(du), _p(ddw), B, T, D, K, _p(wsd), _st())
-        da = torch.empty(NT, 2 * D, device=dev)
-        _lib.call("b2p_glu_bwd", _p(a), _p(du), _p(da), NT, D, _st())
         dh = torch.empty(NT, D, device=dev)
-        if b16:
-            da16 = cast16(da)
-            dpw1 = _wgrad16(w_pw1, ng[3], da16, 2 * D, cast16(h), D, NT)
+        if b16:   # the GLU backward writes the bf16 GEMM operand directly
+            da16 = torch.empty(NT, 2 * D, device=dev, dtype=BF16)
+            _lib.call("b2p_glu_bwd16", _p(a), _p(du), _p(da16), NT, D, _st())
+            dpw1 = _wgrad16(w_pw1, ng[3], da16, 2 * D, h if h.dtype == BF16 else cast16(h), D, NT)
             gemm(NT, D, 2 * D, op(da16, 0, 2 * D, True), op(weight16t(w_pw1), 0, 2 * D, True), dh, D)
         else:
+            da = torch.empty(NT, 2 * D, device=dev)
+            _lib.call("b2p_glu_bwd", _p(a), _p(du), _p(da), NT, D, _st())
             dpw1 = None
             if ng[3]:
                 dpw1 = torch.empty_like(w_pw1)
