@@ -65,21 +65,23 @@ void b2p_set_error(const char* fmt, ...);
 // ---------------------------------------------------------------------------
 // erf(z) for z >= 0 given e = exp(-z*z): Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7), one
 // reciprocal + four FMAs, branch-free (the library erff is a ~30-instruction piecewise polynomial;
-// in the GEMM epilogues the GELU / GELU' of every FFN element is VALU work beside the MFMAs)
+// in the GEMM epilogues the GELU / GELU' of every FFN element is VALU work beside the MFMAs).
+// Every step is an explicit FMA / multiply so the packed two-element forms below (v_pk_fma_f32 /
+// v_pk_mul_f32: half the VALU issue of the epilogue's GELU) are bit-identical to the scalar ones.
 __device__ __forceinline__ float b2p_erf_pos(float z, float e) {
   const float t = __builtin_amdgcn_rcpf(fmaf(0.3275911f, z, 1.0f));
   float p = fmaf(1.061405429f, t, -1.453152027f);
   p = fmaf(p, t, 1.421413741f);
   p = fmaf(p, t, -0.284496736f);
   p = fmaf(p, t, 0.254829592f);
-  return 1.0f - p * t * e;
+  return fmaf(-(p * t), e, 1.0f);
 }
 // Phi(x) = 0.5 * (1 + erf(x / sqrt 2)), with exp(-x^2/2) returned for the GELU derivative
 __device__ __forceinline__ float b2p_phi(float x, float& e) {
   const float z = fabsf(x) * 0.70710678118654752440f;
-  e = __expf(-z * z);
+  e = __expf(-(z * z));
   const float er = b2p_erf_pos(z, e);
-  return 0.5f * (1.0f + copysignf(er, x));
+  return fmaf(0.5f, copysignf(er, x), 0.5f);
 }
 __device__ __forceinline__ float b2p_gelu(float x) {
   // exact-erf GELU (transformers ACT2FN["gelu"] == torch.nn.functional.gelu), erf to 1.5e-7
@@ -90,6 +92,32 @@ __device__ __forceinline__ float b2p_gelu_grad(float x) {
   float e;
   const float cdf = b2p_phi(x, e);
   return fmaf(x * 0.39894228040143267794f, e, cdf);   // Phi(x) + x * pdf(x), pdf = e / sqrt(2 pi)
+}
+typedef float b2p_f2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ b2p_f2 b2p_fma2(b2p_f2 a, b2p_f2 b, b2p_f2 c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ b2p_f2 b2p_splat2(float v) { return b2p_f2{v, v}; }
+// Phi of two elements (packed): same operation sequence as b2p_phi
+__device__ __forceinline__ b2p_f2 b2p_phi2(b2p_f2 x, b2p_f2& e) {
+  const b2p_f2 z = b2p_f2{fabsf(x.x), fabsf(x.y)} * b2p_splat2(0.70710678118654752440f);
+  const b2p_f2 nz = -(z * z);
+  e = b2p_f2{__expf(nz.x), __expf(nz.y)};
+  const b2p_f2 d = b2p_fma2(b2p_splat2(0.3275911f), z, b2p_splat2(1.0f));
+  const b2p_f2 t = b2p_f2{__builtin_amdgcn_rcpf(d.x), __builtin_amdgcn_rcpf(d.y)};
+  b2p_f2 p = b2p_fma2(b2p_splat2(1.061405429f), t, b2p_splat2(-1.453152027f));
+  p = b2p_fma2(p, t, b2p_splat2(1.421413741f));
+  p = b2p_fma2(p, t, b2p_splat2(-0.284496736f));
+  p = b2p_fma2(p, t, b2p_splat2(0.254829592f));
+  const b2p_f2 er = b2p_fma2(-(p * t), e, b2p_splat2(1.0f));
+  return b2p_fma2(b2p_splat2(0.5f), b2p_f2{copysignf(er.x, x.x), copysignf(er.y, x.y)}, b2p_splat2(0.5f));
+}
+__device__ __forceinline__ b2p_f2 b2p_gelu2(b2p_f2 x) {
+  b2p_f2 e;
+  return x * b2p_phi2(x, e);
+}
+__device__ __forceinline__ b2p_f2 b2p_gelu_grad2(b2p_f2 x) {
+  b2p_f2 e;
+  const b2p_f2 cdf = b2p_phi2(x, e);
+  return b2p_fma2(x * b2p_splat2(0.39894228040143267794f), e, cdf);
 }
 __device__ __forceinline__ float b2p_sigmoid(float x) { return 1.0f / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float b2p_silu(float x) { return x * b2p_sigmoid(x); }

@@ -81,7 +81,10 @@ __device__ __forceinline__ float4 epilogue_store4(const EpiArgs& a, int z, int z
   }
   if (e.pre_out) *reinterpret_cast<float4*>(e.pre_out + coff) = make_float4(v[0], v[1], v[2], v[3]);
   if (e.pre16) *reinterpret_cast<uint2*>(e.pre16 + coff) = b2p_pack_bf16x4(make_float4(v[0], v[1], v[2], v[3]));
-  if (e.act != B2P_ACT_NONE) {
+  if (e.act == B2P_ACT_GELU) {   // packed: two elements per VALU instruction
+    const b2p_f2 g0 = b2p_gelu2(b2p_f2{v[0], v[1]}), g1 = b2p_gelu2(b2p_f2{v[2], v[3]});
+    v[0] = g0.x; v[1] = g0.y; v[2] = g1.x; v[3] = g1.y;
+  } else if (e.act != B2P_ACT_NONE) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) v[q] = apply_act(v[q], e.act);
   }
@@ -103,8 +106,13 @@ __device__ __forceinline__ float4 epilogue_store4(const EpiArgs& a, int z, int z
     } else {
       x = *reinterpret_cast<const float4*>(e.aux + ao);
     }
-    v[0] *= act_grad(x.x, e.act_bwd); v[1] *= act_grad(x.y, e.act_bwd);
-    v[2] *= act_grad(x.z, e.act_bwd); v[3] *= act_grad(x.w, e.act_bwd);
+    if (e.act_bwd == B2P_ACT_GELU) {
+      const b2p_f2 g0 = b2p_gelu_grad2(b2p_f2{x.x, x.y}), g1 = b2p_gelu_grad2(b2p_f2{x.z, x.w});
+      v[0] *= g0.x; v[1] *= g0.y; v[2] *= g1.x; v[3] *= g1.y;
+    } else {
+      v[0] *= act_grad(x.x, e.act_bwd); v[1] *= act_grad(x.y, e.act_bwd);
+      v[2] *= act_grad(x.z, e.act_bwd); v[3] *= act_grad(x.w, e.act_bwd);
+    }
   }
   if (e.residual) {
     const float4 r = *reinterpret_cast<const float4*>(
