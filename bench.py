@@ -248,6 +248,10 @@ def main():
     # graph mode: backward is captured, so the bucket all-reduce runs after each replay instead of
     # from the backward hooks
     reducer = GradBucketReducer(brain_params, overlap=not use_graph) if world > 1 else None
+    if world > 1 and use_graph and hasattr(model, "sync_batchnorm"):
+        # no collective is captured into the replayed step: the Conformer's BatchNorm uses per-rank
+        # statistics there (DDP's default); eager steps (--graph 0) synchronise them
+        model.sync_batchnorm = False
     # the frozen w2v's weight gradients (computed, as the reference does) run beside the GRU backward
     if os.environ.get("B2P_DIAG_NO_FROZEN_GRAD") == "1":   # diagnostic only (not the reference's work)
         for n, p in model.named_parameters():
