@@ -467,6 +467,36 @@ __global__ void conv_perm_k(const float* __restrict__ in, float* __restrict__ ou
   else out[perm] = in[ref];
 }
 
+// the same permutation through LDS, one output channel o per block: (I x K) <-> (K x I) transposed in
+// a padded tile (row stride K + 1: conflict-free column reads), both global passes coalesced
+__global__ void __launch_bounds__(256) conv_perm_tile_k(const float* __restrict__ in, float* __restrict__ out,
+                                                        int I, int K, int inverse) {
+  extern __shared__ float tile[];   // I * (K + 1)
+  const int64_t base = (int64_t)blockIdx.x * I * K;
+  const int n = I * K;
+  if (!inverse) {   // in (i, k) -> out (k, i)
+    for (int t = threadIdx.x; t < n; t += 256) {
+      const int i = t / K, k = t - i * K;
+      tile[i * (K + 1) + k] = in[base + t];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < n; t += 256) {
+      const int k = t / I, i = t - k * I;
+      out[base + t] = tile[i * (K + 1) + k];
+    }
+  } else {          // in (k, i) -> out (i, k)
+    for (int t = threadIdx.x; t < n; t += 256) {
+      const int k = t / I, i = t - k * I;
+      tile[i * (K + 1) + k] = in[base + t];
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < n; t += 256) {
+      const int i = t / K, k = t - i * K;
+      out[base + t] = tile[i * (K + 1) + k];
+    }
+  }
+}
+
 __global__ void conv_tflip_k(const float* __restrict__ w, float* __restrict__ out, int64_t G, int64_t Og,
                              int64_t I, int64_t K) {
   const int64_t idx = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -799,8 +829,13 @@ extern "C" int b2p_conv_weight_permute(const float* in, float* out, int64_t O, i
   B2P_CHECK_ARG(in && out && in != out, "conv_weight_permute: bad pointers");
   const int64_t n = O * I * ntaps;
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(conv_perm_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, in, out, O, I, ntaps,
-                     inverse);
+  const size_t lds = (size_t)I * (ntaps + 1) * sizeof(float);
+  if (lds <= 64 * 1024 && O < (1ll << 31))
+    hipLaunchKernelGGL(conv_perm_tile_k, dim3((unsigned)O), dim3(256), lds, (hipStream_t)stream, in, out, (int)I,
+                       (int)ntaps, inverse);
+  else
+    hipLaunchKernelGGL(conv_perm_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, in, out, O, I, ntaps,
+                       inverse);
   B2P_CHECK_LAUNCH();
   return 0;
 }
