@@ -240,3 +240,34 @@ def test_step_graph_replay_matches_eager(adam_in_graph, train_w2v):
     for n in ga:
         d = float((ga[n] - gb[n]).norm())
         assert d <= 1e-5 * float(ga[n].norm()) + 1e-7, n
+
+
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_conf"])
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_eval_forward_matches_oracle(name, mode):
+    """Eval / predict forward (reference train_loop.py:89-109 runs val/test under
+    torch.no_grad with the model in eval mode): the model built with the checkpoints' 0.1 dropouts and
+    LayerDrop, switched to eval, gives the oracle's eval-mode loss. For the Conformer the BatchNorm
+    uses its running statistics (b2p_batchnorm_eval), set here to non-trivial values."""
+    from oracle.b2p2t_oracle import forward_loss, conformer_forward_loss
+    from wav2vec2forbrain_amd import functional as Fn
+    cfg = CFG[name]
+    model = build_model(cfg, train_dropouts=True)
+    g = torch.Generator().manual_seed(11)
+    for n, bt in model.named_buffers():
+        if n.endswith("running_mean"):
+            bt.copy_((0.2 * torch.randn(bt.shape, generator=g)).to(bt.device))
+        elif n.endswith("running_var"):
+            bt.copy_((0.5 + torch.rand(bt.shape, generator=g)).to(bt.device))
+    model.eval()
+    b = batch_dict(cfg)
+    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    with torch.no_grad(), Fn.precision(mode):
+        out = model(make_b2t_batch(b["x"], b["target"], b["day_idxs"], b["input_lens"], b["target_lens"]).cuda())
+    sd = {k: v.detach().cpu() for k, v in model.state_dict().items()}
+    with torch.no_grad():
+        ocfg = oracle_cfg(cfg)
+        ref = float(conformer_forward_loss(sd, b, ocfg, training=False) if cfg.get("conformer")
+                    else forward_loss(sd, b, ocfg, training=False))
+    rtol = LOSS_RTOL_FP32 if mode == "fp32" else LOSS_RTOL_BF16
+    assert abs(out.metrics["ctc_loss"] - ref) <= rtol * abs(ref), (out.metrics["ctc_loss"], ref)
