@@ -5,8 +5,11 @@ Workload (BASELINE.json configs[1]): wav2vec2-base architecture (768/12L/12H/307
 hub unreachable), GRU H256x2 bidirectional, fc [] -> 768, bs=32 per GPU, 1024-bin x 256-channel
 synthetic windows (x ~ N(0,1)), train mode (dropout 0.1 / LayerDrop 0.1 as the checkpoint config),
 unfreeze_strategy=brain_encoder (Adam over the brain encoder; the frozen w2v still computes weight
-gradients, as the reference does). One step = forward + backward + DDP gradient all-reduce (N>1)
-+ Adam + CTC loss readback (.item(), as the reference's forward does), inputs pre-staged in HBM.
+gradients, as the reference does). One step = Trainer.train_step (train/train_loop.py, the step
+run.py executes; reference src/train/train_loop.py:41-84): forward + backward + DDP gradient
+all-reduce (N>1) + Adam, replayed as a captured HIP graph, plus the CTC loss readback (into pinned
+host memory, stream-ordered), inputs pre-staged in HBM. N=1 base runs add a nested record for the
+north-star target (configs[2], Conformer-large bs=32) with its own parity and CPU baseline.
 
 usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        N>1: python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
@@ -26,38 +29,50 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 BF16_DENSE_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 MFMA (MI355X_MICROARCH.md, chip table)
-# train-step FLOPs, base bs=32 L=1024 = 3 x 1738.7 GFLOP forward
-STEP_TFLOP_BASE_BS32 = 5.216
-
-
 # train-step FLOPs per config at bs=32, L=1024
-STEP_TFLOP = {"base": 5.216, "conformer": 30.06}
+STEP_TFLOP = {"base": 5.216, "conformer": 30.06, "large": 16.14}
 
 
 def make_config(bs, L, kind="base"):
-    if kind == "conformer":
-        # BASELINE configs[2]: wav2vec2-conformer-rope-large (1024/24L/16H/4096, k31), README brain
-        # encoder H512x3, fc [256]
-        return dict(name="bench_conformer", seed=42, B=bs, L=L, in_lens=[L] * bs, tgt_range=(60, 120),
-                    hidden_size=1024, layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512,
-                    gru_layers=3, bidirectional=True, fc_hidden=[256], learnable_h0=False, full_grad_max=0,
-                    infeasible=False, conformer=True, dw_kernel=31)
-    return dict(name="bench_base", seed=42, B=bs, L=L, in_lens=[L] * bs, tgt_range=(60, 120), hidden_size=768,
-                layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2,
-                bidirectional=True, fc_hidden=[], learnable_h0=False, full_grad_max=0, infeasible=False)
+    from wav2vec2forbrain_amd.workloads import bench_config
+    return bench_config(kind, bs, L)
 
 
 def build(cfg, device, train_dropouts=True):
-    from tests.helpers import build_model
+    from wav2vec2forbrain_amd.workloads import build_model
     return build_model(cfg, device=device, train_dropouts=train_dropouts)
 
 
 def batch_on(cfg, device):
-    from tests.golden.configs import make_batch
-    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    from wav2vec2forbrain_amd.workloads import device_batch
+    return device_batch(cfg, device)
+
+
+def oracle_batch(cfg):
+    from wav2vec2forbrain_amd.workloads import make_batch
     x, day, il, tgt, tl = make_batch(cfg)
-    b = make_b2t_batch(x, tgt, day, il, tl)
-    return b.cuda() if device != "cpu" else b
+    return dict(x=x, day_idxs=day, input_lens=il, target=tgt, target_lens=tl)
+
+
+def oracle_cfg(cfg, train_dropouts=False):
+    """The oracle's config for a workload (oracle/ is the CPU checker: imported only here, in the
+    cpu_baseline / parity legs after the timed region)."""
+    from oracle.b2p2t_oracle import OracleConfig, ConformerOracleConfig
+    kw = dict(gru_hidden=cfg["gru_hidden"], gru_layers=cfg["gru_layers"], bidirectional=cfg["bidirectional"],
+              fc_hidden_sizes=list(cfg["fc_hidden"]), learnable_initial_state=cfg["learnable_h0"],
+              hidden_size=cfg["hidden_size"], num_hidden_layers=cfg["layers"], num_attention_heads=cfg["heads"],
+              intermediate_size=cfg["ffn"], num_conv_pos_embeddings=cfg["pos_k"],
+              num_conv_pos_embedding_groups=cfg["pos_groups"])
+    if cfg.get("conformer"):
+        c = ConformerOracleConfig(conv_depthwise_kernel_size=cfg["dw_kernel"], **kw)
+    else:
+        c = OracleConfig(do_stable_layer_norm=cfg.get("stable", False), **kw)
+    if train_dropouts:
+        c.hidden_dropout = c.activation_dropout = c.attention_dropout = c.final_dropout = 0.1
+        c.layerdrop = 0.1
+        if cfg.get("conformer"):
+            c.conformer_conv_dropout = 0.1
+    return c
 
 
 def host_cpu_info():
@@ -94,99 +109,192 @@ def host_cpu_info():
     return min(caps), n_phys, model
 
 
-def cpu_baseline(bs=32, L=1024, kind="base", steps=5):
-    """The CPU oracle (torch-CPU fp32 restatement, oracle/b2p2t_oracle.py) timed on the host cores:
-    SURVEY 8(d5) — same workload (train mode, the same dropouts, fwd + bwd + Adam over the brain
-    encoder) at the bench's batch size, 1 warm-up step, median of `steps` timed steps."""
+
+
+def brain_keys(sd):
+    return [k for k in sd if k.startswith("brain_encoder.") and sd[k].is_floating_point() and "gaussian" not in k]
+
+
+def oracle_steps(cfg, sd, steps, train_dropouts, lr=1e-3):
+    """`steps` CPU oracle training steps (oracle/b2p2t_oracle.py, torch-CPU fp32: forward, backward,
+    Adam over the brain encoder as unfreeze_strategy=brain_encoder does) from state dict `sd`, each
+    timed on the host cores. Returns (losses, seconds per step, threads, physical cores, CPU model)."""
     from oracle.b2p2t_oracle import loss_and_grads, conformer_loss_and_grads, adam_step
-    from tests.helpers import oracle_cfg
     threads, n_phys, model_name = host_cpu_info()
     torch.set_num_threads(threads)
-    cfg = make_config(bs, L, kind)
-    ocfg = oracle_cfg(cfg)
-    ocfg.hidden_dropout = ocfg.activation_dropout = ocfg.attention_dropout = ocfg.final_dropout = 0.1
-    ocfg.layerdrop = 0.1
-    if kind == "conformer":
-        ocfg.conformer_conv_dropout = 0.1
-    model = build(cfg, "cpu")
-    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
-    from tests.golden.configs import make_batch
-    x, day, il, tgt, tl = make_batch(cfg)
-    b = dict(x=x, day_idxs=day, input_lens=il, target=tgt, target_lens=tl)
-    brain = [k for k in sd if k.startswith("brain_encoder.") and sd[k].is_floating_point()
-             and "gaussian" not in k]
+    ocfg = oracle_cfg(cfg, train_dropouts)
+    b = oracle_batch(cfg)
+    sd = dict(sd)
+    brain = brain_keys(sd)
     state = {k: (torch.zeros_like(sd[k]), torch.zeros_like(sd[k])) for k in brain}
-
-    def step(i):
-        if kind == "conformer":
+    losses, times = [], []
+    for i in range(steps):
+        t0 = time.perf_counter()
+        if cfg.get("conformer"):
             loss, grads, _bn = conformer_loss_and_grads(sd, b, ocfg, training=True)
         else:
             loss, grads = loss_and_grads(sd, b, ocfg, training=True)
         for k in brain:
             m, v = state[k]
-            sd[k], m, v = adam_step(sd[k], grads[k], m, v, i + 1, 1e-3)
+            sd[k], m, v = adam_step(sd[k], grads[k], m, v, i + 1, lr)
             state[k] = (m, v)
-        return float(loss)
-
-    step(0)
-    times = []
-    for i in range(steps):
-        t0 = time.perf_counter()
-        step(i + 1)
         times.append(time.perf_counter() - t0)
+        losses.append(float(loss))
+    return losses, times, threads, n_phys, model_name
+
+
+def cpu_record(times, threads, n_phys, model_name, sample):
     med = sorted(times)[len(times) // 2]
     return {"value": round(1.0 / med, 5), "unit": "steps/s", "cores": threads, "kind": "port",
             "host_physical_cores": n_phys, "cpu_model": model_name,
-            "sample": f"oracle fwd+bwd+Adam (fp32, torch-CPU, {threads} threads), bs={bs} L={L} train mode, "
-                      f"median of {steps} steps after 1 warm-up: {med:.2f} s/step "
-                      f"(all: {', '.join(f'{t:.2f}' for t in times)})"}
+            "sample": f"{sample}: median {med:.2f} s/step (all: {', '.join(f'{t:.2f}' for t in times)})"}
 
 
-def parity_check(cfg, device, kind="base", steps=2):
-    """north_star parity: per-step CTC loss of the HIP bf16 step vs the fp32 CPU oracle on identical
-    weights and inputs, deterministic mode (dropout 0, LayerDrop 0; the reference's Philox masks
-    cannot be reproduced), `steps` consecutive steps with Adam (lr 1e-3) over the brain encoder, so
-    step 2 also checks the optimizer update. Tolerance 1e-3 rel (BASELINE.json north_star)."""
-    from oracle.b2p2t_oracle import loss_and_grads, conformer_loss_and_grads, adam_step
-    from tests.helpers import oracle_cfg
-    from wav2vec2forbrain_amd.optim import HipAdam
+def cpu_baseline(cfg, steps=5):
+    """the CPU oracle (the build's torch-CPU fp32 restatement) timed on the host cores on
+    the bench workload itself — train mode with the same dropouts / LayerDrop, fwd + bwd + Adam over the
+    brain encoder, same batch size — 1 warm-up step, median of `steps` timed steps."""
+    model = build(cfg, "cpu")
+    sd = {k: v.detach().clone() for k, v in model.state_dict().items()}
+    del model
+    _, times, threads, n_phys, model_name = oracle_steps(cfg, sd, steps + 1, train_dropouts=True)
+    return cpu_record(times[1:], threads, n_phys, model_name,
+                      f"oracle fwd+bwd+Adam (fp32, torch-CPU, {threads} threads), bs={cfg['B']} L={cfg['L']} train mode, "
+                      f"{steps} steps after 1 warm-up")
+
+
+def parity_check(cfg, device, steps=2):
+    """north_star parity: the CTC loss of `steps` consecutive Trainer steps (HIP, bf16, HipAdam over the
+    brain encoder, lr 1e-3) vs the fp32 CPU oracle on identical weights and inputs, deterministic
+    mode (dropout 0, LayerDrop 0: the reference's Philox masks cannot be reproduced); steps > 1 also
+    check the optimizer update. Tolerance 1e-3 rel (BASELINE.json north_star). Returns the record and
+    the oracle's per-step times (the Conformer's CPU baseline reuses them)."""
+    from wav2vec2forbrain_amd.train.train_loop import Trainer
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
     model = build(cfg, device, train_dropouts=False)
     model.train()
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
+    trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
     batch = batch_on(cfg, device)
-    hip = []
-    for _ in range(steps):
-        opt.zero_grad()
-        out = model(batch)
-        out.loss.backward()
-        opt.step()
-        hip.append(float(out.metrics["ctc_loss"]))
+    hip = [float(trainer._eager_body(batch).metrics["ctc_loss"]) for _ in range(steps)]
     torch.cuda.synchronize()
-    del model, opt
-    threads, _, _ = host_cpu_info()
-    torch.set_num_threads(threads)
-    ocfg = oracle_cfg(cfg)
-    from tests.golden.configs import make_batch
-    x, day, il, tgt, tl = make_batch(cfg)
-    b = dict(x=x, day_idxs=day, input_lens=il, target=tgt, target_lens=tl)
-    brain = [k for k in sd if k.startswith("brain_encoder.") and sd[k].is_floating_point() and "gaussian" not in k]
-    state = {k: (torch.zeros_like(sd[k]), torch.zeros_like(sd[k])) for k in brain}
-    ref = []
-    for i in range(steps):
-        if kind == "conformer":
-            loss, grads, _bn = conformer_loss_and_grads(sd, b, ocfg, training=True)
-        else:
-            loss, grads = loss_and_grads(sd, b, ocfg, training=True)
-        ref.append(float(loss))
-        for k in brain:
-            m, v = state[k]
-            sd[k], m, v = adam_step(sd[k], grads[k], m, v, i + 1, 1e-3)
-            state[k] = (m, v)
+    del trainer, model
+    free_device()
+    ref, times, threads, n_phys, model_name = oracle_steps(cfg, sd, steps, train_dropouts=False)
     rel = [abs(h - r) / abs(r) for h, r in zip(hip, ref)]
-    return {"mode": "deterministic (dropout 0, LayerDrop 0), bf16 HIP step vs fp32 CPU oracle, same weights/inputs",
-            "steps": steps, "hip_ctc_loss": [round(v, 6) for v in hip], "oracle_ctc_loss": [round(v, 6) for v in ref],
-            "max_rel_err": float(f"{max(rel):.3e}"), "tolerance": 1e-3, "pass": max(rel) <= 1e-3}
+    rec = {"mode": "deterministic (dropout 0, LayerDrop 0), bf16 HIP Trainer steps vs fp32 CPU oracle, same "
+                   "weights/inputs, Adam lr 1e-3 over the brain encoder between steps",
+           "steps": steps, "hip_ctc_loss": [round(v, 6) for v in hip], "oracle_ctc_loss": [round(v, 6) for v in ref],
+           "rel_err": [float(f"{r:.3e}") for r in rel], "max_rel_err": float(f"{max(rel):.3e}"), "tolerance": 1e-3,
+           "pass": max(rel) <= 1e-3}
+    return rec, (times, threads, n_phys, model_name)
+
+
+def free_device():
+    import gc
+    gc.collect()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+
+
+def log(msg):
+    print(f"bench: {msg}", file=sys.stderr, flush=True)
+
+
+def timed_run(kind, args, world, rank, device, use_graph):
+    """W warm-up steps + K timed steps of the Trainer's training step (train/train_loop.py, the step
+    run.py executes) on the workload, then the GEMM-timing pass. Graph mode: the first W steps run
+    eagerly, the next one captures the step (untimed), the K timed steps are replays."""
+    from wav2vec2forbrain_amd import functional as Fn, _lib
+    from wav2vec2forbrain_amd.train.train_loop import Trainer
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+    cfg = make_config(args.bs, args.seq, kind)
+    model = build(cfg, device)
+    model.train()
+    # the reference reads ctc_loss.item() inside forward (w2v_custom_feat_extractor.py:94): a host sync
+    # per step. The bench keeps the loss on the device and reads every step's value into pinned host
+    # memory (stream-ordered) instead, and reads them all after the timed region.
+    for m in model.modules():
+        if hasattr(m, "sync_metrics"):
+            m.sync_metrics = False
+    trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+    trainer.use_graphs = use_graph and trainer.use_graphs
+    trainer.capture_after = args.warmup
+    batch = batch_on(cfg, device)
+
+    def metrics(out):
+        # the loss, plus (--evaluator) the train evaluator's greedy-decode WER computed on the device
+        # (SURVEY 8(d1) "with the evaluator"; the reference does it on the host every step)
+        loss = out.loss.detach().reshape(1)
+        if not args.evaluator:
+            return loss
+        wer = Fn.ctc_greedy_wer(out.logits.detach(), batch.target)[0]
+        return torch.cat([loss, wer.reshape(1).float()])
+
+    for _ in range(args.warmup + (1 if trainer.use_graphs else 0)):
+        metrics(trainer.train_step(batch))
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    loss_host = torch.zeros(args.steps, 2 if args.evaluator else 1, dtype=torch.float32).pin_memory()
+    g0 = trainer.graph_steps
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        loss_host[i].copy_(metrics(trainer.train_step(batch)), non_blocking=True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    replayed = trainer.graph_steps - g0
+    Fn.check_gru_status()   # a multi-CU GRU timeout in any timed step raises here
+    # GEMM roofline: HIP events around every GEMM launch of the same number of eager Trainer steps,
+    # right after the timed region (a captured graph cannot carry per-launch events); the kernels and
+    # their shapes are the ones the graph replays.
+    gemm = (0.0, 0, 0.0)
+    if not args.no_roofline:
+        _lib.check(_lib.load().b2p_timing_enable(_lib.TIMING_GEMM, 100000), "timing_enable")
+        Fn.set_gemm_timing(True)
+        if trainer.reducer is not None:
+            trainer.reducer.use_layer_gates(None)
+        for _ in range(args.steps):
+            trainer._eager_body(batch)
+        torch.cuda.synchronize()
+        Fn.set_gemm_timing(False)
+        gemm = ctypes_read_timing()
+        _lib.check(_lib.load().b2p_timing_enable(_lib.TIMING_GEMM, 0), "timing_disable")
+    if world > 1:
+        t = torch.tensor([dt], device=device)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = t.item()
+    res = dict(cfg=cfg, dt=dt, losses=loss_host[:, 0].tolist(),
+               wers=loss_host[:, 1].tolist() if args.evaluator else None, gemm=gemm,
+               step_mode=("hip-graph replay" if replayed == args.steps else
+                          "eager" if replayed == 0 else f"mixed ({replayed}/{args.steps} replayed)"))
+    trainer.release_graphs()
+    del trainer, model, batch
+    free_device()
+    return res
+
+
+def roofline_record(gemm, kind):
+    gemm_ms, gemm_n, gemm_flops = gemm
+    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
+    return {"bound": "mfma", "kernel": "b2p_gemm (all GEMM launches of the step)",
+            "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
+            "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": gemm_traffic(kind),
+            "launches": gemm_n, "avg_launch_us": round(gemm_ms * 1e3 / max(gemm_n, 1), 2),
+            "algorithmic_flop_per_launch": round(gemm_flops / max(gemm_n, 1), 1)}
+
+
+WORKLOAD_TEXT = {
+    "base": "b2p2t_gru+w2v wav2vec2-base (12L/768), GRU H256x2 bidir, train mode, unfreeze=brain_encoder, Adam",
+    "conformer": "b2p2t_gru+w2v_conformer rope-large (24L/1024, k31), GRU H512x3 bidir, fc [256], train mode, "
+                 "unfreeze=brain_encoder, Adam",
+    "large": "b2p2t_gru+w2v wav2vec2-large-960h (24L/1024, post-LN), GRU H256x2 bidir, train mode, "
+             "unfreeze=brain_encoder, Adam",
+}
+ARCH_TEXT = {"base": "wav2vec2-base", "conformer": "wav2vec2-conformer-rope-large", "large": "wav2vec2-large-960h"}
 
 
 def main():
@@ -200,12 +308,14 @@ def main():
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--no-roofline", action="store_true",
                     help="skip the eager GEMM-timing pass after the timed region (profiling runs)")
+    ap.add_argument("--no-conformer", action="store_true",
+                    help="N=1 base runs: skip the nested Conformer-large (configs[2], the north-star target) record")
     ap.add_argument("--evaluator", action="store_true",
                     help="include the train evaluator's greedy CTC decode + WER (on the device) in every step")
     ap.add_argument("--graph", type=int, default=None,
-                    help="1/0: replay the step as a captured HIP graph (default 1)")
-    ap.add_argument("--config", choices=["base", "conformer"], default="base",
-                    help="base = BASELINE configs[1] (headline); conformer = configs[2]")
+                    help="1/0: Trainer steps replayed as captured HIP graphs (default 1) / eager")
+    ap.add_argument("--config", choices=["base", "conformer", "large"], default="base",
+                    help="base = BASELINE configs[1] (headline); conformer = configs[2]; large = configs[3] per GPU")
     args = ap.parse_args()
     # the committed tree carries sources only: build the library before the first HIP call
     from wav2vec2forbrain_amd import build_lib
@@ -227,141 +337,24 @@ def main():
             dist.init_process_group(backend)
     device = f"cuda:{local}"
     torch.cuda.set_device(local)
-    torch.manual_seed(1234 + rank)
-
-    from wav2vec2forbrain_amd import functional as Fn, _lib
-    from wav2vec2forbrain_amd.optim import HipAdam
-    from wav2vec2forbrain_amd.train.ddp import GradBucketReducer, unused_param_names
-
+    # model weights are deterministic (util/init.py) and equal on every rank; dropout / LayerDrop
+    # masks differ per rank
+    torch.manual_seed(1234)
+    from wav2vec2forbrain_amd import functional as Fn
+    Fn.SEEDS.reseed(1234 * 65537 + rank)
     Fn.set_precision("bf16")
-    cfg = make_config(args.bs, args.seq, args.config)
-    model = build(cfg, device)
-    model.train()
-    if os.environ.get("B2P_DIAG_LAYERDROP"):   # diagnostic only: override the encoder's LayerDrop
-        enc = model.w2v_encoder
-        enc = enc.wav2vec2_conformer.encoder if hasattr(enc, "wav2vec2_conformer") else enc.wav2vec2.encoder
-        enc.config.layerdrop = float(os.environ["B2P_DIAG_LAYERDROP"])
-    skip = unused_param_names(model)
-    brain_params = [p for n, p in model.named_parameters() if n.startswith("brain_encoder.") and n not in skip]
-    opt = HipAdam(model.brain_encoder.parameters(), lr=1e-3)
     use_graph = True if args.graph is None else bool(args.graph)
-    # graph mode: backward is captured, so the bucket all-reduce runs after each replay instead of
-    # from the backward hooks
-    reducer = GradBucketReducer(brain_params, overlap=not use_graph) if world > 1 else None
-    if world > 1 and use_graph and hasattr(model, "sync_batchnorm"):
-        # no collective is captured into the replayed step: the Conformer's BatchNorm uses per-rank
-        # statistics there (DDP's default); eager steps (--graph 0) synchronise them
-        model.sync_batchnorm = False
-    # the frozen w2v's weight gradients (computed, as the reference does) run beside the GRU backward
-    if os.environ.get("B2P_DIAG_NO_FROZEN_GRAD") == "1":   # diagnostic only (not the reference's work)
-        for n, p in model.named_parameters():
-            if not n.startswith("brain_encoder."):
-                p.requires_grad_(False)
-    if os.environ.get("B2P_DEFER_WGRAD", "1") != "0":
-        Fn.set_deferred_wgrad([p for n, p in model.named_parameters() if not n.startswith("brain_encoder.")])
-    batch = batch_on(cfg, device)
 
-    # the reference reads ctc_loss.item() inside forward (w2v_custom_feat_extractor.py:94): a host
-    # sync per step that lets the GPU drain and idle while the host enqueues the backward. The bench
-    # keeps the loss on the device and reads every step's value after the timed region instead.
-    for m in model.modules():
-        if hasattr(m, "sync_metrics"):
-            m.sync_metrics = False
-
-    def metrics(out):
-        # the loss, plus (--evaluator) the train evaluator's greedy-decode WER computed on the device
-        # (SURVEY 8(d1) "with the evaluator"; the reference does it on the host every step)
-        if not args.evaluator:
-            return out.metrics["ctc_loss"].reshape(1)
-        wer = Fn.ctc_greedy_wer(out.logits.detach(), batch.target)[0]
-        return torch.stack([out.metrics["ctc_loss"].reshape(()), wer])
-
-    def zero_grad():
-        # N>1: the trainable gradients live in the reducer's bucket buffers (bound as p.grad views)
-        reducer.zero_grad() if reducer is not None else opt.zero_grad()
-
-    def step():
-        zero_grad()
-        out = model(batch)
-        out.loss.backward()
-        Fn.join_wgrad()
-        if reducer is not None:
-            reducer.finish()
-        opt.step()
-        return metrics(out)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    # The step is captured once as a HIP graph and replayed (train/step_graph.py): one host call per
-    # step instead of ~650 Python-issued launches. N=1: forward, CTC, backward, side-stream frozen-
-    # weight gradients and Adam are all in the graph. N>1: the graph holds forward + backward; after
-    # each replay the gradient buckets are all-reduced over RCCL and Adam runs (no collective is
-    # captured). --graph 0: eager steps (RCCL bucket hooks inside backward).
-    sg = None
-    if use_graph:
-        from wav2vec2forbrain_amd.train.step_graph import StepGraph
-        if world == 1:
-            sg = StepGraph(step, opt)
-            run = sg.replay
-        else:
-            def fwd_bwd():
-                zero_grad()
-                out = model(batch)
-                out.loss.backward()
-                Fn.join_wgrad()
-                return metrics(out)
-            sg = StepGraph(fwd_bwd, None)
-
-            def run():
-                loss = sg.replay()
-                reducer.finish()
-                opt.step()
-                return loss
-        sg.capture()
-    else:
-        run = step
-    if world > 1:
-        dist.barrier()
-    # every step reads its loss back to the host: an async copy into pinned memory,
-    # stream-ordered after the step, instead of the reference's blocking .item()
-    loss_host = torch.zeros(args.steps, 2 if args.evaluator else 1, dtype=torch.float32).pin_memory()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        loss_host[i].copy_(run(), non_blocking=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    dt = time.perf_counter() - t0
-    losses = loss_host[:, 0].tolist()
-    wers = loss_host[:, 1].tolist() if args.evaluator else None
-    # GEMM roofline: HIP events around every GEMM launch of the same number of steps, run eagerly
-    # right after the timed region (a captured graph cannot carry the per-launch events); the
-    # kernels and their durations are the ones the graph replays.
-    ms = (0.0, 0, 0.0)
-    if not args.no_roofline:
-        _lib.check(_lib.load().b2p_timing_enable(_lib.TIMING_GEMM, 100000), "timing_enable")
-        Fn.set_gemm_timing(True)
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
-        Fn.set_gemm_timing(False)
-        ms = ctypes_read_timing()
-        _lib.check(_lib.load().b2p_timing_enable(_lib.TIMING_GEMM, 0), "timing_disable")
-    if world > 1:
-        t = torch.tensor([dt], device=device)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
+    r = timed_run(args.config, args, world, rank, device, use_graph)
     if rank != 0:
         dist.destroy_process_group() if world > 1 else None
         return
+    dt = r["dt"]
     # whole-job throughput: the units all ranks processed / time. A unit is one training step of one
     # rank over its own bs-sample batch (weak scaling: N ranks process N batches per global step).
     steps_per_s = world * args.steps / dt
-    gemm_ms, gemm_n, gemm_flops = ms
-    achieved = gemm_flops / (gemm_ms * 1e-3) / 1e12 if gemm_ms > 0 else 0.0
     step_tflop = STEP_TFLOP[args.config] * args.bs / 32 * args.seq / 1024
+    log(f"timed {args.steps} steps: {dt / args.steps * 1e3:.3f} ms/step ({r['step_mode']})")
     res = {
         "metric": "train steps/sec + CTC loss, b2p2t_gru+w2v bs=32 seq=1024",
         "value": round(steps_per_s, 4),
@@ -375,47 +368,63 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16",
-        "data": "synthetic (x~N(0,1) 256-ch windows, random-init weights of the "
-                + ("wav2vec2-base" if args.config == "base" else "wav2vec2-conformer-rope-large") + " architecture)",
-        "config": {"workload": ("b2p2t_gru+w2v wav2vec2-base (12L/768), GRU H256x2 bidir, train mode, "
-                                "unfreeze=brain_encoder, Adam") if args.config == "base" else
-                               ("b2p2t_gru+w2v_conformer rope-large (24L/1024, k31), GRU H512x3 bidir, fc [256], "
-                                "train mode, unfreeze=brain_encoder, Adam"), "global_batch": args.bs * world,
+        "data": f"synthetic (x~N(0,1) 256-ch windows, random-init weights of the {ARCH_TEXT[args.config]} architecture)",
+        "config": {"workload": WORKLOAD_TEXT[args.config], "global_batch": args.bs * world,
                    "per_gpu_batch": args.bs, "seq_len": args.seq, "parallelism": f"dp{world}"},
-        "ctc_loss": round(losses[-1], 5),
-        "train_evaluator": ({"on_device": True, "word_error_rate": round(wers[-1], 4)} if args.evaluator else None),
-        "step_mode": "hip-graph replay" if use_graph else "eager",
+        "ctc_loss": round(r["losses"][-1], 5),
+        "train_evaluator": ({"on_device": True, "word_error_rate": round(r["wers"][-1], 4)} if args.evaluator
+                            else None),
+        "step_mode": r["step_mode"] + " of Trainer.train_step (train/train_loop.py, the step run.py runs)",
         "samples_per_s": round(steps_per_s * args.bs, 2),
         "step_mfma_frac": round(step_tflop * steps_per_s / world / BF16_DENSE_PEAK_TFLOPS, 4),
-        "roofline": {"bound": "mfma", "kernel": "b2p_gemm (all GEMM launches of the step)",
-                     "achieved": round(achieved, 2), "peak": BF16_DENSE_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / BF16_DENSE_PEAK_TFLOPS, 4), "traffic": gemm_traffic(args.config),
-                     "launches": gemm_n, "avg_launch_us": round(gemm_ms * 1e3 / max(gemm_n, 1), 2),
-                     "algorithmic_flop_per_launch": round(gemm_flops / max(gemm_n, 1), 1)},
+        "roofline": roofline_record(r["gemm"], args.config),
     }
-    if args.config != "base":
+    if args.config == "conformer":
         res["metric"] = "train steps/sec + CTC loss, b2p2t_gru+w2v_conformer bs=32 seq=1024"
-    def log(msg):
-        print(f"bench: {msg}", file=sys.stderr, flush=True)
-
-    log(f"timed {args.steps} steps: {dt / args.steps * 1e3:.3f} ms/step")
+    elif args.config == "large":
+        res["metric"] = "train steps/sec + CTC loss, b2p2t_gru+w2v wav2vec2-large-960h bs=32 seq=1024"
+    cfg = r["cfg"]
     if world == 1 and not args.no_parity:
-        log("parity: deterministic HIP steps vs CPU oracle")
-        res["parity"] = parity_check(cfg, device, args.config, steps=2 if args.config == "base" else 1)
+        log("parity: deterministic HIP Trainer steps vs CPU oracle")
+        res["parity"], _ = parity_check(cfg, device, steps=2)
     if world == 1 and not args.no_cpu_baseline:
         log("cpu_baseline: oracle steps on the host cores")
-        if args.config == "base":
-            res["cpu_baseline"] = cpu_baseline(bs=args.bs, L=args.seq, kind="base", steps=5)
-        else:
-            # Conformer-large: one fp32 CPU step at bs=32 is ~100 s, so the bounded sample is bs=4
-            # (5 timed steps), scaled to the bench batch (the CPU step is linear in batch size)
-            cb = cpu_baseline(bs=4, L=args.seq, kind="conformer", steps=5)
-            cb["value"] = round(cb["value"] * 4 / args.bs, 6)
-            cb["sample"] += f"; scaled x{args.bs / 4:g} to bs={args.bs}"
-            res["cpu_baseline"] = cb
+        res["cpu_baseline"] = cpu_baseline(cfg, steps=5 if args.config == "base" else 3)
+        res["vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
+    if world == 1 and args.config == "base" and not args.no_conformer:
+        res["conformer_large"] = conformer_record(args, device)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def conformer_record(args, device):
+    """The north-star target (BASELINE configs[2], b2p2t_gru+w2v_conformer-large bs=32 seq=1024) on the
+    same GPU in the same run: timed Trainer steps with their GEMM roofline, CTC-loss parity of 3
+    consecutive deterministic steps against the CPU oracle, and the CPU baseline at bs=32 — the
+    oracle's own per-step times of those 3 parity steps (deterministic mode: the CPU skips the dropout
+    / LayerDrop work the timed GPU steps do, so the GPU/CPU ratio is conservative)."""
+    log("conformer_large: timed Trainer steps")
+    r = timed_run("conformer", args, 1, 0, device, True if args.graph is None else bool(args.graph))
+    sps = args.steps / r["dt"]
+    rec = {"metric": "train steps/sec + CTC loss, b2p2t_gru+w2v_conformer bs=32 seq=1024", "value": round(sps, 4),
+           "unit": "steps/s", "ms_per_step": round(r["dt"] / args.steps * 1e3, 3), "steps": args.steps,
+           "warmup": args.warmup, "config": {"workload": WORKLOAD_TEXT["conformer"], "per_gpu_batch": args.bs,
+                                              "seq_len": args.seq, "parallelism": "dp1"},
+           "step_mode": r["step_mode"], "ctc_loss": round(r["losses"][-1], 5),
+           "step_mfma_frac": round(STEP_TFLOP["conformer"] * args.bs / 32 * args.seq / 1024 * sps
+                                   / BF16_DENSE_PEAK_TFLOPS, 4),
+           "roofline": roofline_record(r["gemm"], "conformer")}
+    if not args.no_parity:
+        log("conformer_large: parity (3 deterministic steps) + CPU oracle timing")
+        rec["parity"], (times, threads, n_phys, model_name) = parity_check(r["cfg"], device, steps=3)
+        if not args.no_cpu_baseline:
+            rec["cpu_baseline"] = cpu_record(
+                times, threads, n_phys, model_name,
+                f"oracle fwd+bwd+Adam (fp32, torch-CPU, {threads} threads), bs={args.bs} L={args.seq}, the 3 "
+                "deterministic parity steps (dropout / LayerDrop 0, no extrapolation)")
+            rec["vs_cpu"] = round(rec["value"] / rec["cpu_baseline"]["value"], 1)
+    return rec
 
 
 def gemm_traffic(kind="base"):
@@ -425,7 +434,8 @@ def gemm_traffic(kind="base"):
     config has no measurement."""
     import glob
     fs = glob.glob(os.path.join(ROOT, "profiles", "*_gemm_traffic*.json"))
-    fs = sorted((f for f in fs if f.endswith("_conformer.json") == (kind == "conformer")), key=os.path.basename)
+    fs = sorted((f for f in fs if os.path.basename(f).endswith(f"_gemm_traffic{'' if kind == 'base' else '_' + kind}.json")),
+                key=os.path.basename)
     if not fs:
         return None
     d = json.load(open(fs[-1]))

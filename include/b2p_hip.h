@@ -195,7 +195,8 @@ int b2p_transpose_bf16(const float* x, uint16_t* y, int64_t R, int64_t C, int64_
                        b2p_stream_t stream);
 
 /* Row softmax for attention scores (eager_attention_forward: softmax(QK^T*scale) + dropout).
- * S rows of length n (row stride ld). Writes P (pre-dropout) and Pd (dropped, scaled). */
+ * S rows of length n (row stride ld). Writes P (pre-dropout) and Pd (dropped, scaled); the keep
+ * mask of element (row, c) is b2p_keep(seed, row * (n rounded up to even) + c). */
 int b2p_softmax_fwd(const float* S, float* P, float* Pd, int64_t rows, int64_t n, int64_t ld,
                     float drop_p, uint64_t drop_seed, b2p_stream_t stream);
 /* dS = P * (dPd*mask - rowsum(P * dPd*mask)) */
@@ -348,7 +349,15 @@ int b2p_gru_fwd_mc(const float* gi, const float* whh, const float* bhh, const fl
                    b2p_stream_t stream);
 int b2p_gru_bwd_mc(const float* dout, const float* whh, const float* out, const float* saved,
                    const float* h0, float* dgi, float* dgh, float* dh0, void* workspace, int64_t B,
-                   int64_t T, int64_t H, int ndir, b2p_stream_t stream);
+                   int64_t T, int64_t H, int ndir, b2p_stream_t stream);   /* T + 1 <= 65535 (16-bit tag) */
+/* Stream-ordered after a b2p_gru_fwd_mc / b2p_gru_bwd_mc call on `workspace`: if that launch timed
+ * out, *status = code unless *status is already nonzero (the first failure is kept). status is a
+ * persistent device int32 the caller zeroes once and reads at its next host sync (the Python layer
+ * raises RuntimeError naming the recurrence; functional.check_gru_status). Capturable. */
+int b2p_gru_mc_status(const void* workspace, int32_t* status, int32_t code, b2p_stream_t stream);
+/* test knob: member `member` (0..15) of every recurrence skips its state exchange stores from the
+ * next launch on, so the other members time out (-1: off) */
+int b2p_gru_mc_debug_withhold(int member);
 
 /* ------------------------------------------------------------------ fused attention (bf16 mode)
  * softmax(Q K^T * scale) -> dropout(p) -> @ V per (batch, head), no mask (HF Wav2Vec2Attention,
@@ -356,7 +365,8 @@ int b2p_gru_bwd_mc(const float* dout, const float* whh, const float* out, const 
  * csrc/attn16.hip. Head size 64, T <= 256 (whole K/V of a head in LDS, scores never in HBM).
  * qkv16: bf16 [B*T][3*nh*64] (q | k | v, head-major), O16: bf16 [B*T][nh*64], lse2: f32 [B][nh][T]
  * (row max + log2 sum of the log2e-scaled scores, saved for backward). Dropout keep mask =
- * b2p_keep(seed, ((b*nh + h)*T + q)*T + key), identical to b2p_softmax_fwd's. bwd writes
+ * b2p_keep(seed, ((b*nh + h)*T + q)*TP + key), TP = T rounded up to even (B*nh*T*TP < 2^32),
+ * identical to b2p_softmax_fwd's. fwd runs one workgroup per (batch, head, 128 queries). bwd writes
  * [dQ | dK | dV] into dqkv (f32, may be NULL) and/or dqkv16 (bf16, may be NULL), same layout as qkv;
  * delta_ws: B*nh*T floats of workspace (row constants sum_key P_d dP_d). mask (optional, drop_p > 0):
  * uint32 [B][nh][T][8], written by fwd as the keep bits of each row (key k = bit k%32 of word k/32)
@@ -402,6 +412,16 @@ int b2p_adam_multi_dev(const int64_t* table, int ntensors, int64_t max_numel, co
 int b2p_adam_recs(const int64_t* recs, int ntensors, float lr, double beta1, double beta2, float eps,
                   float weight_decay, float bias_c1, float bias_c2_sqrt, const float* lr_dev, double* step_dev,
                   float* hyper_dev, b2p_stream_t stream);
+/* Per-tensor device step counters and gates (HipAdam's device form, used in captured and in data-
+ * parallel steps). torch.optim.Adam skips a parameter whose .grad is None: no moment update, no
+ * weight decay, no step increment (src/experiments/experiment.py:25-28); under LayerDrop the
+ * reference's skipped encoder layers are such parameters. Records of 7 x int64 read from HOST memory
+ * (32 per launch pair, capturable): {param, grad, exp_avg, exp_avg_sq, numel, step (double*, that
+ * tensor's counter), gate (int32*: 0 = skip this tensor; NULL = always update)}. lr from lr_dev[0];
+ * the bias corrections are formed per tensor in double from its own step. hyper_dev: float[2 *
+ * ntensors] scratch. */
+int b2p_adam_gated_recs(const int64_t* recs, int ntensors, const float* lr_dev, double beta1, double beta2,
+                        float eps, float weight_decay, float* hyper_dev, b2p_stream_t stream);
 
 /* dst += src (fp32) for ntensors records {dst, src, numel} read from HOST memory and passed in the
  * kernel arguments (96 per launch; capturable): the per-step accumulation of the small gradients of

@@ -1,8 +1,6 @@
 """Fixture configurations shared by make_golden.py (reference side) and the tests (build side)."""
 from __future__ import annotations
 
-import torch
-
 CONFIGS = [
     # tiny: every code path, full gradients stored
     dict(name="tiny_a", seed=42, B=3, L=96, in_lens=[96, 80, 64], tgt_range=(2, 8), hidden_size=64, layers=2,
@@ -42,29 +40,25 @@ CONFIGS = [
          hidden_size=1024, layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512, gru_layers=3,
          bidirectional=True, fc_hidden=[256], learnable_h0=False, full_grad_max=0, infeasible=False, conformer=True,
          dw_kernel=31, big=True),
+    # BASELINE configs[3] per GPU: wav2vec2-large-960h architecture (post-LN forced by the reference,
+    # w2v_custom_feat_extractor.py:18-19,36-41: 1024/24L/16H/4096), GRU H256x2, fc [] (the 512 -> 1024
+    # projection), 32 samples x 1024 bins; plus 2 Adam steps over the brain encoder (frozen w2v)
+    dict(name="large960_bs32", seed=48, B=32, L=1024, in_lens=[1024] * 32, tgt_range=(60, 120), hidden_size=1024,
+         layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2, bidirectional=True,
+         fc_hidden=[], learnable_h0=False, full_grad_max=0, infeasible=False, big=True,
+         adam=dict(steps=2, lr=1e-3, w2v_lr=None, wd=0.0)),
+    # BASELINE configs[4] per GPU (primary reading: global 64 = 8/GPU): Conformer-large with
+    # unfreeze_strategy=brain_encoder+w2v (b2t_gru_w2v_conformer_experiment.py:87-123: two param groups,
+    # w2v_learning_rate for the encoder), 3 Adam steps with L2 weight decay over all 618 M parameters
+    dict(name="conformer_large_ft_bs8", seed=49, B=8, L=1024, in_lens=[1024] * 6 + [896, 768], tgt_range=(60, 120),
+         hidden_size=1024, layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512, gru_layers=3,
+         bidirectional=True, fc_hidden=[256], learnable_h0=False, full_grad_max=0, infeasible=False, conformer=True,
+         dw_kernel=31, big=True, adam=dict(steps=3, lr=1e-3, w2v_lr=1e-4, wd=1e-5)),
 ]
 
 
 def make_batch(cfg):
-    """Synthetic inputs (SURVEY 8(d2)): x ~ N(0,1) (B,L,256); day ~ U{0..23}; targets ~ U{4..31}
-    padded with 0; data seed 0."""
-    g = torch.Generator().manual_seed(0)
-    B, L = cfg["B"], cfg["L"]
-    x = torch.randn(B, L, 256, generator=g)
-    for b, il in enumerate(cfg["in_lens"]):
-        x[b, il:] = 0.0   # zero-padded tail like the collate function
-    day = torch.randint(0, 24, (B,), generator=g)
-    lo, hi = cfg["tgt_range"]
-    tl = torch.randint(lo, hi + 1, (B,), generator=g)
-    S = int(tl.max())
-    tgt = torch.zeros(B, S, dtype=torch.int64)
-    for b in range(B):
-        tgt[b, :tl[b]] = torch.randint(4, 32, (int(tl[b]),), generator=g)
-    if cfg.get("infeasible"):
-        # sample 0: more labels (all equal -> needs 2 frames each) than logit frames
-        T = (cfg["in_lens"][0] - 32) // 4
-        n = min(S, T // 2 + 2)
-        tgt[0, :n] = 7
-        tl[0] = n
-    in_lens = torch.tensor(cfg["in_lens"], dtype=torch.int64)
-    return x, day, in_lens, tgt, tl.to(torch.int64)
+    """Synthetic inputs; the generator lives in the package (workloads.make_batch) so
+    bench.py and the fixtures draw identical batches."""
+    from wav2vec2forbrain_amd.workloads import make_batch as _mb
+    return _mb(cfg)

@@ -95,6 +95,38 @@ def build_reference_conformer(cfg, bfe, base_args):
     return model
 
 
+def adam_trajectory(model, batch, a, loss1):
+    """`a["steps"]` updates of the reference's optimizer (torch.optim.Adam with L2 weight decay,
+    src/experiments/experiment.py:25-28) over the param groups create_optimizer builds
+    (b2t_gru_w2v_experiment.py:109-145 / b2t_gru_w2v_conformer_experiment.py:87-123): the brain
+    encoder, plus the w2v encoder at w2v_learning_rate under unfreeze_strategy=brain_encoder+w2v.
+    The gradients of the first update are the ones just recorded. Stores the loss before every update
+    and, after the last one, the parameter change at the sampled gradient indices."""
+    groups = [{"params": list(model.brain_encoder.parameters())}]
+    if a["w2v_lr"] is not None:
+        groups.append({"params": list(model.w2v_encoder.parameters()), "lr": a["w2v_lr"]})
+    opt = torch.optim.Adam(groups, lr=a["lr"], weight_decay=a["wd"], eps=1e-8)
+    p0 = {n: p.detach().clone() for n, p in model.named_parameters()}
+    losses = [loss1]
+    for k in range(a["steps"]):
+        if k:
+            opt.zero_grad()
+            out = model.forward(batch)
+            out.loss.backward()
+            losses.append(out.loss.item())
+        opt.step()
+    res = {"adam_losses": np.array(losses, dtype=np.float64)}
+    gen = torch.Generator().manual_seed(8)
+    for n, p in model.named_parameters():
+        flat = (p.detach() - p0[n]).reshape(-1)
+        idx = torch.randint(0, flat.numel(), (256,), generator=gen)
+        res["didx/" + n] = idx.numpy()
+        res["dval/" + n] = flat[idx].numpy()
+        res["dnorm/" + n] = np.array(flat.double().norm().item())
+    print(f"  adam losses: {losses}")
+    return res
+
+
 def run(cfg, modules):
     tfw, bfe, w2v, base_args = modules
     torch.manual_seed(0)
@@ -145,6 +177,8 @@ def run(cfg, modules):
     for n, bt in model.named_buffers():
         if "running_" in n:
             res["buf/" + n] = bt.numpy()
+    if cfg.get("adam"):
+        res.update(adam_trajectory(model, batch, cfg["adam"], out.loss.item()))
     path = os.path.join(OUT, f"{cfg['name']}.npz")
     np.savez_compressed(path, **res)
     print(f"{path}: loss={out.loss.item():.6f}  ({os.path.getsize(path)/1e6:.2f} MB)")

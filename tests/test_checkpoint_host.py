@@ -127,3 +127,21 @@ def test_model_pt_round_trip_strict(tmp_path, name):
     c.brain_encoder.load_state_dict(torch.load(fb, map_location="cpu", weights_only=True), strict=True)
     assert all(torch.equal(x, y) for x, y in zip(a.brain_encoder.state_dict().values(),
                                                  c.brain_encoder.state_dict().values()))
+
+
+def test_hub_name_without_weights_raises(monkeypatch):
+    """The reference's from_pretrained either loads the pretrained encoder or fails: a hub name that
+    cannot be fetched offline raises instead of silently leaving a random frozen encoder, unless the
+    weights come later (--from_checkpoint) or random-init weights are asked for explicitly."""
+    from wav2vec2forbrain_amd.model import w2v_custom_feat_extractor as w
+    from wav2vec2forbrain_amd.model.w2v_config import W2VConfig
+    monkeypatch.delenv("B2P_RANDOM_W2V_WEIGHTS", raising=False)
+    enc = w.Wav2Vec2WithoutFeatExtrForCTC(W2VConfig(hidden_size=32, num_hidden_layers=1, num_attention_heads=2,
+                                                    intermediate_size=64, num_conv_pos_embeddings=8,
+                                                    num_conv_pos_embedding_groups=2))
+    with pytest.raises(RuntimeError, match="cannot be fetched"):
+        w._load_or_note(enc, "facebook/wav2vec2-base-960h")
+    with w.weights_loaded_later(True):
+        w._load_or_note(enc, "facebook/wav2vec2-base-960h")
+    monkeypatch.setenv("B2P_RANDOM_W2V_WEIGHTS", "1")
+    w._load_or_note(enc, "facebook/wav2vec2-base-960h")

@@ -1,0 +1,93 @@
+"""BASELINE configs[3] and configs[4] on one GPU (their per-GPU workloads), against trajectories the
+reference's own modules and optimizer produced (tests/golden/make_golden.py: adam_trajectory):
+
+  large960_bs32           wav2vec2-large-960h (post-LN 1024/24L/16H/4096), GRU H256x2, fc [] (the
+                          512 -> 1024 projection), 32 x 1024 bins; unfreeze_strategy=brain_encoder,
+                          2 Adam steps (torch.optim.Adam, lr 1e-3).
+  conformer_large_ft_bs8  Conformer-large, unfreeze_strategy=brain_encoder+w2v (two param groups,
+                          b2t_gru_w2v_conformer_experiment.py:87-123: brain lr 1e-3, w2v lr 1e-4, L2
+                          weight decay 1e-5), 8 x 1024 bins (two padded samples), 3 Adam steps over
+                          all 618 M parameters.
+
+The build runs them through Trainer.train_step (train/train_loop.py: the step run.py executes): the
+first step eager, then the step is captured once and replayed, so the later steps are graph replays
+— including the recast of the trained 16-bit weight copies inside the replay. Deterministic mode
+(dropout / LayerDrop 0), bf16 MFMA (the Conformer forward on fp16)."""
+import numpy as np
+import pytest
+import torch
+
+from tests.helpers import CFG, load_fixture, build_model, batch_dict
+
+pytestmark = pytest.mark.gpu
+
+LOSS_RTOL = 1e-3   # BASELINE.json north_star, per step
+
+
+def _trajectory(name):
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    from wav2vec2forbrain_amd.train.train_loop import Trainer
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+    cfg = CFG[name]
+    a = cfg["adam"]
+    model = build_model(cfg)
+    model.train()
+    p0 = {n: p.detach().clone() for n, p in model.named_parameters()}
+    exp = SyntheticStepExperiment(model, unfreeze="brain_encoder+w2v" if a["w2v_lr"] is not None else "brain_encoder",
+                                  lr=a["lr"], w2v_lr=a["w2v_lr"], weight_decay=a["wd"])
+    b = batch_dict(cfg)
+    batch = make_b2t_batch(b["x"], b["target"], b["day_idxs"], b["input_lens"], b["target_lens"]).cuda()
+    with Fn.precision("bf16"):
+        trainer = Trainer(exp)
+        trainer.capture_after = 1
+        losses = [float(trainer.train_step(batch).loss) for _ in range(a["steps"])]
+    torch.cuda.synchronize()
+    assert trainer.eager_steps == 1 and trainer.graph_steps == a["steps"] - 1
+    trainer.release_graphs()
+    Fn.set_deferred_wgrad([])
+    deltas = {n: (p.detach() - p0[n]).reshape(-1) for n, p in model.named_parameters()}
+    return losses, deltas, trainer
+
+
+@pytest.mark.parametrize("name", ["large960_bs32", "conformer_large_ft_bs8"])
+def test_adam_trajectory_matches_reference(name):
+    fx = load_fixture(name)
+    ref = [float(v) for v in fx["adam_losses"]]
+    losses, deltas, trainer = _trajectory(name)
+    rel = [abs(g - r) / abs(r) for g, r in zip(losses, ref)]
+    print(f"{name}: build {losses} reference {ref} rel {rel}")
+    assert max(rel) <= LOSS_RTOL, (losses, ref, rel)
+    # parameter updates: every parameter the reference's Adam moved moved here by about as much, and
+    # every parameter it left alone (unused inpLayer* / hidden_start / conformer pos_conv_embed:
+    # grad None) stayed bit-identical
+    worst = 0.0
+    for n in fx["param_names"]:
+        dref = float(fx["dnorm/" + n])
+        d = deltas[n]
+        if dref == 0.0:
+            assert float(d.abs().max()) == 0.0, n
+            continue
+        got = float(d.double().norm())
+        worst = max(worst, abs(got - dref) / dref)
+        v = d[torch.from_numpy(fx["didx/" + n]).cuda()].cpu().numpy()
+        r = fx["dval/" + n]
+        # Adam's first updates are ~lr * sign(g): entries whose gradient is near zero may flip sign
+        # under bf16 rounding, so the sampled entries are compared by their correlation
+        c = float(np.dot(v, r) / (np.linalg.norm(v) * np.linalg.norm(r) + 1e-30))
+        assert c >= 0.9, (n, c)
+    print(f"{name}: worst relative update-norm error {worst:.3e}")
+    assert worst <= 0.1, worst
+    # the optimizer's per-parameter step counters: one per update for every used parameter
+    opt = trainer.optimizer
+    opt.sync_steps()
+    steps = {float(opt.state[p]["step"]) for g in opt.param_groups for p in g["params"]
+             if len(opt.state[p]) and float(fx["dnorm/" + _name(trainer.model, p)]) > 0}
+    assert steps == {float(CFG[name]["adam"]["steps"])}, steps
+
+
+def _name(model, p):
+    for n, q in model.named_parameters():
+        if q is p:
+            return n
+    raise KeyError

@@ -95,3 +95,61 @@ def test_grad_bucket_reducer_world2_gloo(overlap):
     assert all(nb > 1 for _, _, nb, _ in res)
     # identical collective order on both ranks: bucket index order
     assert all(order == list(range(nb)) for _, _, nb, order in res), res
+
+
+def _gate_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from wav2vec2forbrain_amd.train.ddp import GradBucketReducer
+        torch.manual_seed(0)
+        a, b, c = torch.nn.Linear(4, 4), torch.nn.Linear(4, 4), torch.nn.Linear(4, 4)
+        params = list(a.parameters()) + list(b.parameters()) + list(c.parameters())
+        red = GradBucketReducer(params, bucket_mb=0.001)
+        out = {}
+        # eager step: the backward hooks mark what this rank used; a is used by both ranks, b by rank 0
+        # only, c by neither (every rank's LayerDrop dropped its layer)
+        red.zero_grad()
+        x = torch.randn(2, 4)
+        y = a(x)
+        if rank == 0:
+            y = b(y)
+        y.sum().backward()
+        red.finish()
+        out["eager"] = [int(red.gates[id(p)]) for p in params]
+        # replayed step: no hook fires; the used flags are the layers' device gates of this replay
+        # (rank 0 kept layer b, rank 1 kept layer c; a has no gate: always used)
+        fb = torch.tensor([1 if rank == 0 else 0], dtype=torch.int32)
+        fc = torch.tensor([0 if rank == 0 else 1], dtype=torch.int32)
+        st = red.make_layer_gates({**{id(p): fb for p in b.parameters()}, **{id(p): fc for p in c.parameters()}})
+        red.use_layer_gates(st)
+        red.zero_grad()
+        red.finish()
+        out["replay"] = [int(red.gates[id(p)]) for p in params]
+        fc.fill_(0)   # next replay: nobody kept c
+        red.zero_grad()
+        red.finish()
+        out["replay2"] = [int(red.gates[id(p)]) for p in params]
+        q.put((rank, out))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reducer_used_gates_world2_gloo():
+    """The optimizer gates GradBucketReducer publishes (HipAdam's device form skips a gate-0 tensor,
+    as torch.optim.Adam skips grad=None): "some rank used this parameter in this step", from the
+    backward hooks in eager steps and from the device LayerDrop flags in replayed steps, MAX-reduced."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_gate_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    for r in (0, 1):
+        assert res[r]["eager"] == [1, 1, 1, 1, 0, 0], res
+        assert res[r]["replay"] == [1, 1, 1, 1, 1, 1], res
+        assert res[r]["replay2"] == [1, 1, 1, 1, 0, 0], res

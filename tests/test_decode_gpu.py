@@ -116,6 +116,37 @@ def test_ctc_greedy_cer_matches_host_evaluator(tmp_path):
 
 
 @pytest.mark.gpu
+def test_cer_overflow_row_scored_on_host(tmp_path):
+    """A degenerate decode (early training: 600 alternating <unk> / blank frames = 1,500 characters
+    plus delimiters past the device buffer) is reported by the kernel as char_errs = -1, kept out of
+    the device CER, and the evaluator scores that batch on the host instead of silently lowering it."""
+    from transformers import Wav2Vec2CTCTokenizer
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.model.b2tmodel import ModelOutput
+    from wav2vec2forbrain_amd.train.evaluator import EvaluatorWithW2vLMDecoder, char_error_rate, cut_after_eos_token
+    from wav2vec2forbrain_amd.datasets.batch_types import B2tSampleBatch
+    f = tmp_path / "vocab.json"
+    f.write_text(json.dumps({t: i for i, t in enumerate(VOCAB)}))
+    tok = Wav2Vec2CTCTokenizer(str(f))
+    B, T, C, S = 2, 1400, 32, 40
+    ids = torch.zeros(B, T, dtype=torch.int64)
+    ids[0, 0::2] = 3                                  # <unk> every other frame: > 2048 characters
+    ids[1, :40] = torch.randint(5, C, (40,), generator=torch.Generator().manual_seed(3))
+    logits = torch.full((B, T, C), -4.0)
+    logits.scatter_(2, ids.unsqueeze(-1), 6.0)
+    target = torch.randint(5, C, (B, S), generator=torch.Generator().manual_seed(4))
+    cer, errs, nch = Fn.ctc_greedy_cer(logits.cuda(), target.cuda(), VOCAB)
+    assert int(errs[0]) == -1 and int(errs[1]) >= 0
+    ev = EvaluatorWithW2vLMDecoder(tok, "train")
+    out = ModelOutput(logits.cuda(), {"ctc_loss": 1.0}, loss=torch.tensor(1.0, device="cuda"))
+    ev.track_batch(out, B2tSampleBatch(torch.zeros(B, 1, 1).cuda(), target.cuda()))
+    pred = [cut_after_eos_token(x) for x in tok.batch_decode(ids.numpy(), group_tokens=True)]
+    ref = char_error_rate(pred, tok.batch_decode(target.numpy(), group_tokens=False))
+    got = out.metrics["char_error_rate"]
+    assert abs(got - ref) < 1e-9, (got, ref)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("beam,tmin,prune", [(16, -5.0, -10.0), (48, -1e30, -1e30), (1, -5.0, -10.0)])
 def test_ctc_prefix_beam_matches_oracle(beam, tmin, prune):
     """Device prefix beam search (csrc/beam.hip) == its CPU restatement (oracle/ctc_beam_oracle.py):

@@ -117,3 +117,72 @@ def test_dp_step_equals_global_batch_step(name, tmp_path):
     # the ranks hold identical gradients after the exchange
     for n in grads:
         assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n
+
+
+def _trainer_steps(model, batches, graphs):
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.train.train_loop import Trainer
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+    with Fn.precision("fp32"):
+        trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+        trainer.use_graphs = graphs
+        trainer.capture_after = 1
+        losses = [float(trainer.train_step(b).loss) for b in batches]
+    torch.cuda.synchronize()
+    counts = (trainer.eager_steps, trainer.graph_steps)
+    trainer.release_graphs()
+    Fn.set_deferred_wgrad([])
+    return losses, counts
+
+
+def _trainer_worker(rank, name, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        cfg = _cfg(name)
+        model = build_model(cfg)
+        model.train()
+        model.sync_metrics = False
+        per = cfg["B"] // WORLD
+        b = _batch(cfg, (rank * per, (rank + 1) * per))
+        losses, counts = _trainer_steps(model, [b] * 3, graphs=True)
+        torch.save({"losses": losses, "counts": counts,
+                    "params": {n: p.detach().cpu() for n, p in _trainable(model)}},
+                   os.path.join(out_dir, f"trainer_rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_replayed_trainer_steps_equal_global_batch_steps(tmp_path):
+    """Data-parallel Trainer steps with replays (train/train_loop.py: step 1 eager, then forward +
+    backward captured and replayed; after each replay the bucket all-reduce, the used-by-some-rank
+    gates and the device-form Adam run): three steps of two ranks on half batches give the parameters
+    of three single-process Trainer steps on the whole batch (fp32 MFMA, deterministic mode)."""
+    import torch.multiprocessing as mp
+    name = "tiny_a"
+    cfg = _cfg(name)
+    ref = build_model(cfg)
+    ref.train()
+    ref_losses, _ = _trainer_steps(ref, [_batch(cfg, (0, cfg["B"]))] * 3, graphs=False)
+    params = {n: p.detach().cpu() for n, p in _trainable(ref)}
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, name, port, str(tmp_path))) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [torch.load(tmp_path / f"trainer_rank{r}.pt", weights_only=True) for r in range(WORLD)]
+    for r in res:
+        assert tuple(r["counts"]) == (1, 2), r["counts"]
+    for k in range(3):   # the global-batch loss is the mean of the rank means
+        glob = (res[0]["losses"][k] + res[1]["losses"][k]) / 2
+        assert abs(glob - ref_losses[k]) <= 2e-5 * abs(ref_losses[k]), (k, glob, ref_losses[k])
+    for n, p in params.items():
+        for r in res:
+            d = float((r["params"][n] - p).norm())
+            assert d <= 1e-4 * float(p.norm()) + 1e-6, (n, d)
+        assert torch.equal(res[0]["params"][n], res[1]["params"][n]), n

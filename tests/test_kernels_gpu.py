@@ -691,6 +691,38 @@ def test_gru_mc_direct_and_graph_replay():
             assert torch.equal(a, b)
 
 
+def test_gru_mc_timeout_raises():
+    """A multi-CU GRU launch whose member never publishes its state (test knob: member 1 withholds
+    its exchange stores) times out instead of hanging, and the failure is not silent: the launch's
+    timeout flag is folded into the persistent status word (b2p_gru_mc_status) and the next loss
+    readback (functional.loss_item, the reference's per-step .item()) raises RuntimeError naming the
+    recurrence. Healthy launches afterwards leave the word at 0."""
+    Fn = _fn()
+    from wav2vec2forbrain_amd import _lib
+    torch.manual_seed(6)
+    B, T, H, IN = 16, 6, 512, 64
+    dev = "cuda"
+    x = torch.randn(B, T, IN, device=dev, requires_grad=True)
+    w = [torch.randn(3 * H, IN, device=dev) / 8, torch.randn(3 * H, H, device=dev) / math.sqrt(H),
+         torch.zeros(3 * H, device=dev), torch.zeros(3 * H, device=dev)]
+    Fn.check_gru_status()   # start clean
+    with Fn.precision("bf16"):
+        _lib.call("b2p_gru_mc_debug_withhold", 1)
+        try:
+            out = Fn.gru_layer(x, H, 1, w)
+            loss = out.square().mean()
+            torch.cuda.synchronize()
+        finally:
+            _lib.call("b2p_gru_mc_debug_withhold", -1)
+        with pytest.raises(RuntimeError, match="multi-CU GRU recurrence timed out \\(forward of GRU layer"):
+            Fn.loss_item(loss)
+        assert Fn.gru_status_value() == 0   # cleared by the raise
+        out = Fn.gru_layer(x, H, 1, w)
+        out.square().mean().backward()
+        Fn.loss_item(out.square().mean())   # healthy: no raise
+    assert Fn.gru_status_value() == 0
+
+
 @pytest.mark.gpu
 def test_conformer_16bit_producers():
     """The Conformer's 16-bit operand producers against torch fp32: LayerNorm with its fp16/bf16 copy,

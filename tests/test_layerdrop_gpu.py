@@ -118,3 +118,75 @@ def test_captured_layerdrop_redraws_per_replay(name):
     for n, b in bufs_g.items():   # BatchNorm running statistics: updated only by kept layers
         e = dict(ref.named_buffers())[n]
         assert float((b - e).norm()) <= 1e-5 * float(e.norm()) + 1e-7, n
+
+
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_conf"])
+def test_captured_layerdrop_adam_leaves_dropped_layers(name):
+    """Full fine-tuning under LayerDrop (config 5, unfreeze=brain_encoder+w2v): replayed steps with
+    HipAdam over all parameters (device form: per-parameter step counters, the layer's LayerDrop gate
+    on every tensor) vs eager steps with the same skip pattern, where a dropped layer's parameters
+    have grad None and the update leaves them alone — value, both moments, L2 weight decay and the
+    step count — as torch.optim.Adam does in the reference (src/experiments/experiment.py:25-28)."""
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.optim import HipAdam
+    from wav2vec2forbrain_amd.train.step_graph import StepGraph
+    cfg = CFG[name]
+    Fn.SEEDS.reseed(4321)
+    model = _model(name)
+    batch = _batch(cfg)
+    opt = HipAdam(model.parameters(), lr=1e-2, weight_decay=1e-2)
+
+    def step():
+        opt.zero_grad()
+        out = model(batch)
+        out.loss.backward()
+        opt.step()
+        return out.metrics["ctc_loss"]
+
+    Fn.LAYERDROP_LOG = []
+    with Fn.precision("bf16"):
+        sg = StepGraph(step, opt, warmup=0, warm_replays=0)
+        sg.capture()
+        seeds = list(Fn.LAYERDROP_LOG)
+        Fn.LAYERDROP_LOG = None
+        losses, patterns = [], []
+        for _ in range(REPLAYS):
+            losses.append(float(sg.replay()))
+            ep = int(sg.epoch.item())
+            patterns.append(tuple(Fn.layerdrop_keep(P_LD, s, ep) for s in seeds))
+        sg.release()
+    torch.cuda.synchronize()
+    opt.sync_steps()
+    assert any(not all(p) for p in patterns), patterns     # some layer was dropped in some replay
+    got = {n: (p.detach().clone(), opt.state[p]["exp_avg"].clone(), float(opt.state[p]["step"]))
+           for n, p in model.named_parameters() if len(opt.state[p])}
+
+    ref = _model(name)
+    ropt = HipAdam(ref.parameters(), lr=1e-2, weight_decay=1e-2)
+    losses_e = []
+    with Fn.precision("bf16"):
+        for pat in patterns:
+            ropt.zero_grad()
+            forced = _ForcedRand(pat)
+            torch.rand = forced
+            try:
+                out = ref(batch)
+            finally:
+                torch.rand = forced.orig
+            out.loss.backward()
+            ropt.step()
+            losses_e.append(out.metrics["ctc_loss"])
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(losses, losses_e, rtol=1e-5, atol=0)
+    used_layers = [sum(p[k] for p in patterns) for k in range(cfg["layers"])]
+    for n, p in ref.named_parameters():
+        st = ropt.state[p]
+        e_step = float(st["step"]) if len(st) else 0.0
+        g_p, g_m, g_step = got[n] if n in got else (p.detach(), None, 0.0)
+        assert g_step == e_step, (n, g_step, e_step)
+        assert float((g_p - p.detach()).norm()) <= 1e-5 * float(p.detach().norm()) + 1e-7, n
+        if len(st):
+            assert float((g_m - st["exp_avg"]).norm()) <= 1e-5 * float(st["exp_avg"].norm()) + 1e-9, n
+        if ".layers." in n:   # an encoder layer's tensors stepped once per replay that kept the layer
+            k = int(n.split(".layers.")[1].split(".")[0])
+            assert e_step == used_layers[k], (n, e_step, used_layers[k])

@@ -11,7 +11,7 @@ from tests.helpers import CFG, load_fixture, oracle_cfg, oracle_state, batch_dic
 
 
 @pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
-                                  "base_bs32", "conformer_large_bs32"])
+                                  "base_bs32", "conformer_large_bs32", "large960_bs32", "conformer_large_ft_bs8"])
 def test_state_dict_keys_match_reference(name):
     fx = load_fixture(name)
     model = build_model(CFG[name], device="cpu")
@@ -25,7 +25,9 @@ _SLOW = pytest.mark.skipif(os.environ.get("B2P_SLOW_ORACLE") != "1", reason="set
 
 
 @pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
-                                  "base_bs32", pytest.param("conformer_large_bs32", marks=_SLOW)])
+                                  "base_bs32", pytest.param("conformer_large_bs32", marks=_SLOW),
+                                  pytest.param("large960_bs32", marks=_SLOW),
+                                  pytest.param("conformer_large_ft_bs8", marks=_SLOW)])
 def test_oracle_matches_reference_golden(name):
     cfg = CFG[name]
     fx = load_fixture(name)
@@ -68,3 +70,36 @@ def test_oracle_logits_match_reference():
     loss, aux = forward_loss(sd, batch_dict(cfg), oracle_cfg(cfg), return_all=True)
     np.testing.assert_allclose(aux["logits"].detach().numpy(), fx["logits"], rtol=1e-4, atol=1e-5)
     np.testing.assert_array_equal(aux["logit_lens"].numpy(), fx["logit_lens"])
+
+
+@_SLOW
+@pytest.mark.parametrize("name", ["large960_bs32", "conformer_large_ft_bs8"])
+def test_oracle_adam_trajectory_matches_reference(name):
+    """The oracle's Adam restatement (adam_step, torch.optim.Adam with L2 weight decay) over the
+    experiments' param groups reproduces the reference's own multi-step trajectory (adam_losses)."""
+    cfg = CFG[name]
+    a = cfg["adam"]
+    fx = load_fixture(name)
+    torch.set_num_threads(8)
+    from oracle.b2p2t_oracle import loss_and_grads, conformer_loss_and_grads, adam_step
+    sd = oracle_state(cfg)
+    b = batch_dict(cfg)
+    trained = [k for k in fx["param_names"] if k.startswith("brain_encoder.") or a["w2v_lr"] is not None]
+    lr = {k: (a["lr"] if k.startswith("brain_encoder.") else a["w2v_lr"]) for k in trained}
+    state = {k: (torch.zeros_like(sd[k]), torch.zeros_like(sd[k]), 0) for k in trained}
+    losses = []
+    for _ in range(a["steps"]):
+        if cfg.get("conformer"):
+            loss, grads, bn = conformer_loss_and_grads(sd, b, oracle_cfg(cfg))
+            sd.update(bn)
+        else:
+            loss, grads = loss_and_grads(sd, b, oracle_cfg(cfg))
+        losses.append(float(loss))
+        for k in trained:
+            if float(grads[k].abs().max()) == 0.0 and (".inpLayer" in k or k.endswith("hidden_start")
+                                                       or "pos_conv_embed" in k):
+                continue   # never used on the path: grad None in the reference, Adam skips it
+            m, v, t = state[k]
+            sd[k], m, v = adam_step(sd[k], grads[k], m, v, t + 1, lr[k], wd=a["wd"])
+            state[k] = (m, v, t + 1)
+    np.testing.assert_allclose(losses, fx["adam_losses"], rtol=2e-5)

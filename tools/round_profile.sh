@@ -7,11 +7,11 @@ T=$1
 O=gpurun_out/$T
 mkdir -p $O
 stop() { echo "STOP after $1 (rc=$2)"; exit $2; }
-timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_fetch.log 2>&1 || stop fetch $?
-timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > $O/pmc_write.log 2>&1 || stop write $?
+timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --no-conformer > $O/pmc_fetch.log 2>&1 || stop fetch $?
+timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --no-conformer > $O/pmc_write.log 2>&1 || stop write $?
 python tools/traffic.py $(find $O/pmc_fetch -name "*.db" | head -1) $(find $O/pmc_write -name "*.db" | head -1) $O/gemm_traffic.json || stop traffic $?
 cp $O/gemm_traffic.json profiles/${T}_gemm_traffic.json
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline > $O/prof.log 2>&1 || stop prof $?
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 4 --warmup 2 --no-cpu-baseline --no-parity --no-conformer > $O/prof.log 2>&1 || stop prof $?
 python tools/prof_summary.py $O/prof 6 40 > $O/prof_summary.txt 2>&1
 timeout -k 10 600 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || stop bench $?
 tail -1 $O/bench.json

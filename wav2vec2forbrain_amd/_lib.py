@@ -100,6 +100,8 @@ _SIGS = {
     "b2p_gru_mc_workspace": (c_i64, [c_i64, c_i64, c_i32]),
     "b2p_gru_fwd_mc": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_gru_bwd_mc": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
+    "b2p_gru_mc_status": (c_i32, [c_p, c_p, c_i32, c_p]),
+    "b2p_gru_mc_debug_withhold": (c_i32, [c_i32]),
     "b2p_gru_hprev": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_attn16_fwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p, c_p]),
     "b2p_attn16_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p,
@@ -111,6 +113,7 @@ _SIGS = {
     "b2p_cast16_2d": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_p]),
     "b2p_accum_recs": (c_i32, [c_p, c_i32, c_p]),
     "b2p_adam_recs": (c_i32, [c_p, c_i32, c_f32, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_p, c_p]),
+    "b2p_adam_gated_recs": (c_i32, [c_p, c_i32, c_p, c_f64, c_f64, c_f32, c_f32, c_p, c_p]),
     "b2p_set_seed_epoch": (c_i32, [c_p]),
     "b2p_ctc_greedy_wer": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_i32, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "b2p_ctc_beam_workspace": (c_i64, [c_i64, c_i64, c_i64]),

@@ -90,6 +90,59 @@ __global__ void __launch_bounds__(NTH) adam_rec_k(const AdamRecs recs, float lr,
   }
 }
 
+// Per-tensor step counters and gates (the device form HipAdam uses for captured and DP steps).
+// torch.optim.Adam leaves a parameter whose .grad is None untouched: no moment update, no weight
+// decay, no step increment (src/experiments/experiment.py:25-28). Under LayerDrop the reference's
+// skipped layers are exactly such parameters; a captured step runs every layer and marks a skipped
+// one with its gate flag, so a closed gate here reproduces the None-grad skip.
+constexpr int GADAM_MAXR = 32;
+struct GatedAdamRecs {
+  int64_t r[GADAM_MAXR][7];   // param, grad, exp_avg, exp_avg_sq, numel, step (double*), gate (int32*)
+};
+// one thread per record: advance the step of an open tensor and form its bias corrections in double
+// (as the host does for torch.optim.Adam); a closed tensor gets the skip marker bc2s = 0
+__global__ void adam_gate_steps_k(const GatedAdamRecs recs, int nrec, const float* __restrict__ lr_dev, double b1,
+                                  double b2, float2* __restrict__ hyper) {
+  const int i = threadIdx.x;
+  if (i >= nrec) return;
+  const int64_t* rec = recs.r[i];
+  const int32_t* gate = reinterpret_cast<const int32_t*>(rec[6]);
+  if (gate != nullptr && *gate == 0) {
+    hyper[i] = make_float2(0.f, 0.f);
+    return;
+  }
+  double* st = reinterpret_cast<double*>(rec[5]);
+  const double t = st[0] + 1.0;
+  st[0] = t;
+  hyper[i] = make_float2((float)((double)lr_dev[0] / (1.0 - pow(b1, t))), (float)sqrt(1.0 - pow(b2, t)));
+}
+__global__ void __launch_bounds__(NTH) adam_gated_k(const GatedAdamRecs recs, float b1, float b2, float eps,
+                                                    float wd, const float2* __restrict__ hyper) {
+  const float2 h = hyper[blockIdx.y];
+  if (h.y == 0.f) return;   // gate closed: parameter, moments and step stay as they are
+  const int64_t* rec = recs.r[blockIdx.y];
+  float* __restrict__ p = reinterpret_cast<float*>(rec[0]);
+  const float* __restrict__ g = reinterpret_cast<const float*>(rec[1]);
+  float* __restrict__ m = reinterpret_cast<float*>(rec[2]);
+  float* __restrict__ v = reinterpret_cast<float*>(rec[3]);
+  const int64_t n = rec[4];
+  const float step = h.x, bc2s = h.y;
+  const int64_t stride = (int64_t)gridDim.x * NTH;
+  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += stride) {
+    float gi = g[i];
+    const float pi = p[i];
+    if (wd != 0.f) gi += wd * pi;
+    float mi = m[i];
+    mi = mi + (1.f - b1) * (gi - mi);
+    float vi = v[i];
+    vi = b2 * vi + (1.f - b2) * gi * gi;
+    m[i] = mi;
+    v[i] = vi;
+    const float denom = sqrtf(vi) / bc2s + eps;
+    p[i] = pi - step * (mi / denom);
+  }
+}
+
 // gradient accumulation dst[i] += src[i] over many small tensors in one launch (records by value:
 // capturable, nothing uploaded). blockIdx.y = record, blockIdx.x strides its elements.
 constexpr int ACC_MAXR = 96;
@@ -137,6 +190,37 @@ extern "C" int b2p_adam_recs(const int64_t* recs, int ntensors, float lr, double
     if (bx > 4096) bx = 4096;
     hipLaunchKernelGGL(adam_rec_k, dim3((unsigned)bx, (unsigned)nc), dim3(NTH), 0, st, a, lr, b1f, b2f, eps,
                        weight_decay, bias_c1, bias_c2_sqrt, dev ? (const float*)hyper_dev : nullptr);
+  }
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_adam_gated_recs(const int64_t* recs, int ntensors, const float* lr_dev, double beta1,
+                                   double beta2, float eps, float weight_decay, float* hyper_dev,
+                                   b2p_stream_t stream) {
+  B2P_CHECK_ARG(recs != nullptr || ntensors == 0, "adam_gated_recs: NULL records");
+  B2P_CHECK_ARG(ntensors >= 0, "adam_gated_recs: bad tensor count");
+  B2P_CHECK_ARG(ntensors == 0 || (lr_dev && hyper_dev), "adam_gated_recs: NULL lr_dev / hyper_dev");
+  hipStream_t st = (hipStream_t)stream;
+  const float b1f = (float)beta1, b2f = (float)beta2;
+  for (int c0 = 0; c0 < ntensors; c0 += GADAM_MAXR) {
+    const int nc = ntensors - c0 < GADAM_MAXR ? ntensors - c0 : GADAM_MAXR;
+    GatedAdamRecs a;
+    int64_t maxn = 0;
+    for (int i = 0; i < nc; ++i) {
+      for (int k = 0; k < 7; ++k) a.r[i][k] = recs[7 * (c0 + i) + k];
+      B2P_CHECK_ARG(a.r[i][5] != 0, "adam_gated_recs: NULL step counter in a record");
+      B2P_CHECK_ARG(a.r[i][4] <= 0 || (a.r[i][0] && a.r[i][1] && a.r[i][2] && a.r[i][3]),
+                    "adam_gated_recs: NULL tensor in a record");
+      maxn = a.r[i][4] > maxn ? a.r[i][4] : maxn;
+    }
+    float2* hy = reinterpret_cast<float2*>(hyper_dev) + c0;
+    hipLaunchKernelGGL(adam_gate_steps_k, dim3(1), dim3(64), 0, st, a, nc, lr_dev, beta1, beta2, hy);
+    if (maxn <= 0) continue;
+    int64_t bx = (maxn + (int64_t)NTH * PER_THREAD - 1) / ((int64_t)NTH * PER_THREAD);
+    if (bx > 4096) bx = 4096;
+    hipLaunchKernelGGL(adam_gated_k, dim3((unsigned)bx, (unsigned)nc), dim3(NTH), 0, st, a, b1f, b2f, eps,
+                       weight_decay, (const float2*)hy);
   }
   B2P_CHECK_LAUNCH();
   return 0;

@@ -5,16 +5,17 @@
 // T' (= 249 frames at the 1024-bin windows) <= 256 and head size 64, so one (batch, head)'s whole
 // K and V fit in 64 KB of LDS: no online softmax is needed. Scores never touch HBM (the unfused
 // path writes and re-reads a (B, heads, T', T') fp32 tensor ~6 times per layer).
-//   fwd   (b, h, 64-query block): S^T = K Q^T (keys in registers, query on the lane), in-register
+//   fwd   (b, h, 128-query block): S^T = K Q^T (keys in registers, query on the lane), in-register
 //         softmax (2 cross-lane shuffles per reduction), O^T = V^T P^T with P^T taken straight
 //         from the accumulators as the B operand and V^T read by ds_read_b64_tr_b16.
 //         Saves lse2[b][h][q] = max + log2(sum) in the log2 domain.
-//   dQ    (b, h, 64-query block, launched first): S^T, dP^T recomputed from lse2 (no stored
+//   dQ    (b, h, 128-query block, launched first): S^T, dP^T recomputed from lse2 (no stored
 //         probabilities); delta = sum_key P_d dP_d; dQ^T += K^T dS^T.
-//   dK/dV (b, h, 64-key block): S, dP = dO V^T with the key on the lane; dV^T += dO^T P_d and
+//   dK/dV (b, h, 128-key block): S, dP = dO V^T with the key on the lane; dV^T += dO^T P_d and
 //         dK^T += Q^T dS with the dQ pass's delta.
-// Dropout: keep(b, h, q, key) = b2p_keep(seed, ((b*nh + h)*T + q)*T + key) — the same mask the
-// unfused softmax kernel draws, so both paths agree element for element.
+// Dropout: keep(b, h, q, key) = b2p_keep(seed, ((b*nh + h)*T + q)*TP + key), TP = T rounded up to
+// even (a hash serves an aligned pair of keys) — the same mask the unfused softmax kernel draws
+// (b2p_softmax_fwd), so both paths agree element for element.
 #include "common.h"
 #include <type_traits>
 #include "../../include/b2p_hip.h"
@@ -74,20 +75,6 @@ __device__ __forceinline__ void store_out(float* o32, uint16_t* o16, int64_t off
   if (o16) *reinterpret_cast<uint2*>(o16 + off) = b2p_pack_bf16x4(f);
 }
 
-// XCD-aware block mapping: the hardware deals consecutive workgroups round-robin over the 8 XCDs
-// (private L2 each); remap so the blocks of one (batch, head) — which all stage the same K/V (or
-// Q/dO) — run on ONE XCD and hit its L2 instead of the Infinity Cache. Needs the block count to be
-// a multiple of 8 (else identity).
-__device__ __forceinline__ void block_coords(int& xb, int& h, int& b) {
-  const int nx = gridDim.x, ny = gridDim.y;
-  const int total = nx * ny * gridDim.z;
-  int L = blockIdx.x + nx * (blockIdx.y + ny * blockIdx.z);
-  if ((total & 7) == 0) L = (L & 7) * (total >> 3) + (L >> 3);
-  xb = L % nx;
-  h = (L / nx) % ny;
-  b = L / (nx * ny);
-}
-
 struct DropCfg {
   uint64_t seed;
   uint32_t thr;
@@ -115,108 +102,143 @@ __device__ __forceinline__ float keep_scale(const DropCfg& dc, uint64_t idx) {
 
 // ------------------------------------------------------------------------------------------ forward
 // qkv16 [B*T][3*D] bf16 (q | k | v, head-major inside each); O16 [B*T][D] bf16; lse2 [B][nh][T]
-template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: keep bits in memory
-__global__ void __launch_bounds__(256) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
-                                                    float* __restrict__ lse2, int T, int nh, float scale, DropCfg dc,
-                                                    uint32_t* __restrict__ maskw) {
+// One workgroup per (batch, head, 128-query half): 4 waves stage K and V once (64 KB of LDS) and then
+// each wave runs query tiles w and w + 4 of its half (16 queries each). K/V cross L2 -> LDS once per
+// 128 queries (half the traffic of 64-query blocks), and 2 x B x heads workgroups (768 at the base
+// workload) spread evenly over 256 CUs at two resident workgroups per CU.
+// Dropout keep bits come two per hash (b2p_hash of idx >> 1, 16-bit halves) with the row stride TP
+// = T rounded up to even, so a lane's 4 consecutive keys need exactly 2 hashes.
+constexpr int FWD_NT = 256;
+constexpr int FWD_QB = 128;   // queries per workgroup
+// the 4 keep bits of keys key0 .. key0+3 (key0 % 4 == 0) of mask row `row` (32-bit element index:
+// b2p_hash with idx >> 32 == 0, checked on the host)
+__device__ __forceinline__ uint32_t keep4_bits(uint32_t key_lo, uint32_t k32, uint32_t thr16) {
+  const uint32_t h0 = b2p_mix32(b2p_mix32((key_lo >> 1) ^ k32) + k32);
+  const uint32_t h1 = b2p_mix32(b2p_mix32(((key_lo >> 1) + 1) ^ k32) + k32);
+  return ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) | ((h0 >> 16) >= thr16 ? 2u : 0u) |
+         ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
+}
+
+template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward
+__global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
+                                                       float* __restrict__ lse2, int T, int nh, float scale,
+                                                       DropCfg dc, uint32_t* __restrict__ maskw) {
   constexpr bool DROP = DM != 0;
   if (b2p_gated_off(dc.gate)) return;   // LayerDrop: this replay skips the layer (outputs unused)
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Kimg = smem;
-  char* Vimg = smem + TMAX * 128;
-  int qb, h, b;
-  block_coords(qb, h, b);
+  const int nqh = (T + FWD_QB - 1) / FWD_QB;
+  const int bh = blockIdx.x / nqh, qh = blockIdx.x - bh * nqh;
+  const int b = bh / nh, h = bh - b * nh;
   const int D = nh * DH;
   const int64_t ld = 3 * (int64_t)D;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
   const int64_t row0 = (int64_t)b * T;
-  load_image(Kimg, qkv, row0, T, ld, D + h * DH, tid);
-  load_image(Vimg, qkv, row0, T, ld, 2 * D + h * DH, tid);
-  const int q = qb * 64 + w * 16 + lr;
-  const bool qok = q < T;
+  const int TP = T + (T & 1);
+  // this wave's first query tile: its Q fragments are in flight while K / V are staged
   bf16x8 qf[2];
+  const int qt0 = qh * (FWD_QB / 16) + w;
+  {
+    const int q = qt0 * 16 + lr;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    qf[ks] = bf16x8{};
-    if (qok) qf[ks] = gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g);
+    for (int ks = 0; ks < 2; ++ks) qf[ks] = q < T ? gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g) : bf16x8{};
   }
+  load_image(smem, qkv, row0, T, ld, D + h * DH, tid);
+  load_image(smem + TMAX * 128, qkv, row0, T, ld, 2 * D + h * DH, tid);
   __syncthreads();
-
-  // S^T: tile kt = keys kt*16 + 4g + i (registers) x query q (lane)
-  f32x4 s[16];
   const float c2 = scale * LOG2E;
+  const uint32_t k32 = (uint32_t)dc.seed ^ b2p_mix32((uint32_t)(dc.seed >> 32) + 0x9E3779B9u);   // b2p_hash key
+  const uint32_t thr16 = b2p_thr16(dc.thr);
+  for (int qt = qt0; qt < qt0 + FWD_QB / 16 && qt * 16 < T; qt += 4) {
+    // opaque per-iteration image bases: keeps the compiler from hoisting the ~100 per-lane LDS
+    // fragment addresses of the unrolled body out of the loop (they would not fit beside s[16])
+    uint32_t obase = 0;
+    asm volatile("" : "+v"(obase));
+    const char* Kimg = smem + obase;
+    const char* Vimg = smem + TMAX * 128 + obase;
+    const int q = qt * 16 + lr;
+    const bool qok = q < T;
+    if (qt != qt0) {
 #pragma unroll
-  for (int kt = 0; kt < 16; ++kt) {
-    s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks) s[kt] = mfma(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], s[kt]);
-  }
-  float m = -INFINITY;
-#pragma unroll
-  for (int kt = 0; kt < 16; ++kt)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = kt * 16 + 4 * g + i;
-      const float v = key < T ? s[kt][i] * c2 : -INFINITY;
-      s[kt][i] = v;
-      m = fmaxf(m, v);
+      for (int ks = 0; ks < 2; ++ks) qf[ks] = qok ? gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g) : bf16x8{};
     }
-  m = fmaxf(m, __shfl_xor(m, 16, 64));
-  m = fmaxf(m, __shfl_xor(m, 32, 64));
-  float sum = 0.f;
+    // S^T: tile kt = keys kt*16 + 4g + i (registers) x query q (lane)
+    f32x4 s[16];
 #pragma unroll
-  for (int kt = 0; kt < 16; ++kt)
+    for (int kt = 0; kt < 16; ++kt) {
+      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const float e = exp2_fast(s[kt][i] - m);
-      s[kt][i] = e;
-      sum += e;
+      for (int ks = 0; ks < 2; ++ks) s[kt] = mfma(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], s[kt]);
     }
-  sum += __shfl_xor(sum, 16, 64);
-  sum += __shfl_xor(sum, 32, 64);
-  const float inv = 1.f / sum;
-  const uint64_t rowidx = (((uint64_t)b * nh + h) * T + (qok ? q : 0)) * (uint64_t)T;
-  // O^T (d x q) = V^T (d x keys) . P_d^T (keys x q), 32 keys per k-step: normalisation and dropout
-  // of a k-step's probabilities are interleaved with its MFMAs (keeps the mask math off the
-  // register peak)
-  f32x4 o[4];
+    float m = -INFINITY;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    uint32_t word = 0;   // keep bits of keys 32c .. 32c+31 (this lane's 8 of them)
-#pragma unroll
-    for (int half = 0; half < 2; ++half)
+    for (int kt = 0; kt < 16; ++kt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int key = (2 * c + half) * 16 + 4 * g + i;
-        const float ks = key < T ? keep_scale<DROP>(dc, rowidx + key) : 0.f;
-        if (DROP) word |= (ks != 0.f ? 1u : 0u) << (half * 16 + 4 * g + i);
-        s[2 * c + half][i] *= inv * ks;
+        const int key = kt * 16 + 4 * g + i;
+        const float v = key < T ? s[kt][i] * c2 : -INFINITY;
+        s[kt][i] = v;
+        m = fmaxf(m, v);
       }
-    if (DM == 2) {
-      // the mask as bits for the backward kernels ([b][h][q][8] words): OR over the 4 lanes of a query
-      word |= (uint32_t)__shfl_xor((int)word, 16, 64);
-      word |= (uint32_t)__shfl_xor((int)word, 32, 64);
-      if (qok && g == 0) maskw[(((int64_t)b * nh + h) * T + q) * 8 + c] = word;
+    m = fmaxf(m, __shfl_xor(m, 16, 64));
+    m = fmaxf(m, __shfl_xor(m, 32, 64));
+    float sum = 0.f;
+#pragma unroll
+    for (int kt = 0; kt < 16; ++kt)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float e = exp2_fast(s[kt][i] - m);
+        s[kt][i] = e;
+        sum += e;
+      }
+    sum += __shfl_xor(sum, 16, 64);
+    sum += __shfl_xor(sum, 32, 64);
+    const float inv = 1.f / sum;
+    const uint32_t rowlo = (uint32_t)((((uint32_t)b * (uint32_t)nh + (uint32_t)h) * (uint32_t)T + (uint32_t)(qok ? q : 0)) *
+                                      (uint32_t)TP);
+    // O^T (d x q) = V^T (d x keys) . P_d^T (keys x q), 32 keys per k-step
+    f32x4 o[4];
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      uint32_t word = 0;   // keep bits of keys 32c .. 32c+31 (this lane's 8 of them)
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int key0 = (2 * c + half) * 16 + 4 * g;
+        const uint32_t kb = DROP ? keep4_bits(rowlo + (uint32_t)key0, k32, thr16) : 0xFu;
+        if (DROP) word |= kb << (half * 16 + 4 * g);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float ks = (key0 + i < T && ((kb >> i) & 1u)) ? (DROP ? dc.scale : 1.f) : 0.f;
+          s[2 * c + half][i] *= inv * ks;
+        }
+      }
+      if (DM == 2) {
+        // the mask as bits for the backward kernels ([b][h][q][8] words): OR over the 4 lanes of a query
+        word |= (uint32_t)__shfl_xor((int)word, 16, 64);
+        word |= (uint32_t)__shfl_xor((int)word, 32, 64);
+        if (qok && g == 0) maskw[(((int64_t)b * nh + h) * T + q) * 8 + c] = word;
+      }
+      const bf16x8 bp = pack_acc(s[2 * c], s[2 * c + 1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        o[dt] = mfma(tr_frag(Vimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, o[dt]);
     }
-    const bf16x8 bp = pack_acc(s[2 * c], s[2 * c + 1]);
+    const int64_t orow = (row0 + q) * D + h * DH;
+    if (qok) {
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-      o[dt] = mfma(tr_frag(Vimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, o[dt]);
+      for (int dt = 0; dt < 4; ++dt) store_out(nullptr, O16, orow + dt * 16 + 4 * g, o[dt], 1.f);
+    }
+    if (qok && g == 0) lse2[((int64_t)b * nh + h) * T + q] = m + __log2f(sum);
   }
-  const int64_t orow = (row0 + q) * D + h * DH;
-  if (qok) {
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) store_out(nullptr, O16, orow + dt * 16 + 4 * g, o[dt], 1.f);
-  }
-  if (qok && g == 0) lse2[((int64_t)b * nh + h) * T + q] = m + __log2f(sum);
 }
 
 // ------------------------------------------------------------------------------------ backward dK dV
 // dO16 [B*T][D] bf16; delta [B][nh][T] from the dQ kernel; writes dK, dV into dqkv (fp32 and/or
-// bf16) columns [D + h*64, ...) and [2D + h*64, ...).
+// bf16) columns [D + h*64, ...) and [2D + h*64, ...). One workgroup per (batch, head, 128 keys): Q and
+// dO are staged once for 128 keys (4 waves x key tiles w and w + 4).
+constexpr int BWD_KB = 128;
 template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: keep bits in memory
 __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restrict__ qkv, const float* __restrict__ delta,
                                                         const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
@@ -226,97 +248,107 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
   constexpr bool DROP = DM != 0;
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Qimg = smem;
-  char* dOimg = smem + TMAX * 128;
   float* lse_s = reinterpret_cast<float*>(smem + 2 * TMAX * 128);
   float* del_s = lse_s + TMAX;
-  uint32_t* msk_s = reinterpret_cast<uint32_t*>(del_s + TMAX);   // [q][2]: this block's 64 keys' bits
-  int kb, h, b;
-  block_coords(kb, h, b);
+  uint32_t* msk_s = reinterpret_cast<uint32_t*>(del_s + TMAX);   // [q][4]: this block's 128 keys' bits
+  const int nkb = (T + BWD_KB - 1) / BWD_KB;
+  const int bhi = blockIdx.x / nkb, kb = blockIdx.x - bhi * nkb;
+  const int b = bhi / nh, h = bhi - b * nh;
   const int D = nh * DH;
   const int64_t ld = 3 * (int64_t)D;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
   const int64_t row0 = (int64_t)b * T;
   if (b2p_gated_off(dc.gate)) {   // LayerDrop: zero dK, dV (the bias reduction reads them)
-    zero_block(dqkv, dqkv16, row0, kb * 64, T, ld, D + h * DH, tid);
-    zero_block(dqkv, dqkv16, row0, kb * 64, T, ld, 2 * D + h * DH, tid);
+    for (int half = 0; half < 2; ++half) {
+      zero_block(dqkv, dqkv16, row0, kb * BWD_KB + 64 * half, T, ld, D + h * DH, tid);
+      zero_block(dqkv, dqkv16, row0, kb * BWD_KB + 64 * half, T, ld, 2 * D + h * DH, tid);
+    }
     return;
   }
-  load_image(Qimg, qkv, row0, T, ld, h * DH, tid);
-  load_image(dOimg, dO16, row0, T, D, h * DH, tid);
+  load_image(smem, qkv, row0, T, ld, h * DH, tid);
+  load_image(smem + TMAX * 128, dO16, row0, T, D, h * DH, tid);
   {
     const int qq = tid;   // one thread per query row: row constants lse2 and delta (from the dQ pass)
     const int64_t o = ((int64_t)b * nh + h) * T + qq;
     del_s[qq] = qq < T ? delta[o] : 0.f;
     lse_s[qq] = qq < T ? lse2[o] : 0.f;
-    if (DM == 2) {   // the keep bits of keys 64kb .. 64kb+63 for every query row
-      const uint2 wv = qq < T ? *reinterpret_cast<const uint2*>(maskw + o * 8 + 2 * kb) : make_uint2(0, 0);
-      msk_s[2 * qq] = wv.x;
-      msk_s[2 * qq + 1] = wv.y;
-    }
-  }
-  const int key = kb * 64 + w * 16 + lr;
-  const bool kok = key < T;
-  bf16x8 kf[2], vf[2];
+    if (DM == 2) {   // the keep bits of keys 128kb .. 128kb+127 for every query row
+      const int wbase = (BWD_KB / 32) * kb;
 #pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    kf[ks] = vf[ks] = bf16x8{};
-    if (kok) {
-      kf[ks] = gload8(qkv + (row0 + key) * ld + D + h * DH + 32 * ks + 8 * g);
-      vf[ks] = gload8(qkv + (row0 + key) * ld + 2 * D + h * DH + 32 * ks + 8 * g);
+      for (int j = 0; j < BWD_KB / 32; ++j) msk_s[4 * qq + j] = (qq < T && wbase + j < 8) ? maskw[o * 8 + wbase + j] : 0u;
     }
   }
   __syncthreads();
   const float c2 = scale * LOG2E;
   const uint64_t bh = (uint64_t)b * nh + h;
-  f32x4 dv[4], dk[4];
+  const int TP = T + (T & 1);
+  const int kt0 = kb * (BWD_KB / 16) + w;
+  for (int kt = kt0; kt < kt0 + BWD_KB / 16 && kt * 16 < T; kt += 4) {
+    uint32_t obase = 0;   // opaque image bases: no hoisting of the unrolled body's LDS addresses
+    asm volatile("" : "+v"(obase));
+    const char* Qimg = smem + obase;
+    const char* dOimg = smem + TMAX * 128 + obase;
+    const int key = kt * 16 + lr;
+    const bool kok = key < T;
+    const int kw = (key >> 5) & 3;   // this key's word among the block's 4
+    bf16x8 kf[2], vf[2];
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dv[dt] = dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int nchunk = (T + 31) >> 5;
-  for (int c = 0; c < nchunk; ++c) {
-    f32x4 pd[2], ds[2];
-    uint32_t mw[2][4];   // keep-bit words (from the forward, staged in LDS) of this chunk's queries
-    if (DM == 2) {
-#pragma unroll
-      for (int half = 0; half < 2; ++half)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) mw[half][i] = msk_s[2 * ((2 * c + half) * 16 + 4 * g + i) + ((key >> 5) & 1)];
-    }
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      const int qt = 2 * c + half;
-      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        sv = mfma(row_frag(Qimg, qt * 16 + lr, 32 * ks + 8 * g), kf[ks], sv);
-        dp = mfma(row_frag(dOimg, qt * 16 + lr, 32 * ks + 8 * g), vf[ks], dp);
-      }
-      // rows q = qt*16 + 4g + i, column key
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int qq = qt * 16 + 4 * g + i;
-        const bool ok = kok && qq < T;
-        const float p = ok ? exp2_fast(sv[i] * c2 - lse_s[qq]) : 0.f;
-        const float ksc = !ok ? 0.f
-                          : (DM == 2) ? (((mw[half][i] >> (key & 31)) & 1u) ? dc.scale : 0.f)
-                                            : keep_scale<DROP>(dc, (bh * T + qq) * (uint64_t)T + key);
-        pd[half][i] = p * ksc;
-        ds[half][i] = p * (dp[i] * ksc - del_s[qq]);
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[ks] = vf[ks] = bf16x8{};
+      if (kok) {
+        kf[ks] = gload8(qkv + (row0 + key) * ld + D + h * DH + 32 * ks + 8 * g);
+        vf[ks] = gload8(qkv + (row0 + key) * ld + 2 * D + h * DH + 32 * ks + 8 * g);
       }
     }
-    const bf16x8 bp = pack_acc(pd[0], pd[1]), bs = pack_acc(ds[0], ds[1]);
+    f32x4 dv[4], dk[4];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      dv[dt] = mfma(tr_frag(dOimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, dv[dt]);
-      dk[dt] = mfma(tr_frag(Qimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dk[dt]);
+    for (int dt = 0; dt < 4; ++dt) dv[dt] = dk[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const int nchunk = (T + 31) >> 5;
+    for (int c = 0; c < nchunk; ++c) {
+      f32x4 pd[2], ds[2];
+      uint32_t mw[2][4];   // keep-bit words (from the forward, staged in LDS) of this chunk's queries
+      if (DM == 2) {
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) mw[half][i] = msk_s[4 * ((2 * c + half) * 16 + 4 * g + i) + kw];
+      }
+#pragma unroll
+      for (int half = 0; half < 2; ++half) {
+        const int qt = 2 * c + half;
+        f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          sv = mfma(row_frag(Qimg, qt * 16 + lr, 32 * ks + 8 * g), kf[ks], sv);
+          dp = mfma(row_frag(dOimg, qt * 16 + lr, 32 * ks + 8 * g), vf[ks], dp);
+        }
+        // rows q = qt*16 + 4g + i, column key
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int qq = qt * 16 + 4 * g + i;
+          const bool ok = kok && qq < T;
+          const float p = ok ? exp2_fast(sv[i] * c2 - lse_s[qq]) : 0.f;
+          const float ksc = !ok ? 0.f
+                            : (DM == 2) ? (((mw[half][i] >> (key & 31)) & 1u) ? dc.scale : 0.f)
+                                              : keep_scale<DROP>(dc, (bh * T + qq) * (uint64_t)TP + key);
+          pd[half][i] = p * ksc;
+          ds[half][i] = p * (dp[i] * ksc - del_s[qq]);
+        }
+      }
+      const bf16x8 bp = pack_acc(pd[0], pd[1]), bs = pack_acc(ds[0], ds[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        dv[dt] = mfma(tr_frag(dOimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, dv[dt]);
+        dk[dt] = mfma(tr_frag(Qimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dk[dt]);
+      }
     }
-  }
-  if (kok) {
-    const int64_t r = (row0 + key) * ld + h * DH;
+    if (kok) {
+      const int64_t r = (row0 + key) * ld + h * DH;
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      store_out(dqkv, dqkv16, r + D + dt * 16 + 4 * g, dk[dt], scale);
-      store_out(dqkv, dqkv16, r + 2 * D + dt * 16 + 4 * g, dv[dt], 1.f);
+      for (int dt = 0; dt < 4; ++dt) {
+        store_out(dqkv, dqkv16, r + D + dt * 16 + 4 * g, dk[dt], scale);
+        store_out(dqkv, dqkv16, r + 2 * D + dt * 16 + 4 * g, dv[dt], 1.f);
+      }
     }
   }
 }
@@ -325,7 +357,8 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
 // Runs BEFORE the dK/dV kernel: delta[q] = sum_key P_d dP_d is formed here from the very P and dP
 // the kernel recomputes (not as dO . O from the rounded bf16 O), so sum_key dS = 0 holds to fp32
 // rounding — otherwise the residual feeds a systematic, Q-correlated error into dK. Pass 1 keeps
-// P and dP*keep in registers, pass 2 forms dS and dQ^T += K^T dS^T.
+// P and dP*keep in registers, pass 2 forms dS and dQ^T += K^T dS^T. One workgroup per (batch, head,
+// 128 queries): K and V staged once, 4 waves x query tiles w and w + 4.
 template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: keep bits in memory
 __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restrict__ qkv, float* __restrict__ delta,
                                                        const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
@@ -335,87 +368,94 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
   constexpr bool DROP = DM != 0;
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  char* Kimg = smem;
-  char* Vimg = smem + TMAX * 128;
-  int qb, h, b;
-  block_coords(qb, h, b);
+  const int nqh = (T + FWD_QB - 1) / FWD_QB;
+  const int bhi = blockIdx.x / nqh, qh = blockIdx.x - bhi * nqh;
+  const int b = bhi / nh, h = bhi - b * nh;
   const int D = nh * DH;
   const int64_t ld = 3 * (int64_t)D;
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
   const int64_t row0 = (int64_t)b * T;
   if (b2p_gated_off(dc.gate)) {   // LayerDrop: zero dQ (the bias reduction reads it)
-    zero_block(dqkv, dqkv16, row0, qb * 64, T, ld, h * DH, tid);
+    for (int half = 0; half < 2; ++half) zero_block(dqkv, dqkv16, row0, qh * FWD_QB + 64 * half, T, ld, h * DH, tid);
     return;
   }
-  load_image(Kimg, qkv, row0, T, ld, D + h * DH, tid);
-  load_image(Vimg, qkv, row0, T, ld, 2 * D + h * DH, tid);
-  const int q = qb * 64 + w * 16 + lr;
-  const bool qok = q < T;
-  bf16x8 qf[2], df[2];
-#pragma unroll
-  for (int ks = 0; ks < 2; ++ks) {
-    qf[ks] = df[ks] = bf16x8{};
-    if (qok) {
-      qf[ks] = gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g);
-      df[ks] = gload8(dO16 + (row0 + q) * D + h * DH + 32 * ks + 8 * g);
-    }
-  }
-  const int64_t rowc = ((int64_t)b * nh + h) * T + (qok ? q : 0);
-  const float ls = qok ? lse2[rowc] : 0.f;
+  load_image(smem, qkv, row0, T, ld, D + h * DH, tid);
+  load_image(smem + TMAX * 128, qkv, row0, T, ld, 2 * D + h * DH, tid);
   __syncthreads();
   const float c2 = scale * LOG2E;
-  const uint64_t rowidx = (uint64_t)rowc * (uint64_t)T;
-  uint32_t mw[8];   // this query row's keep bits (from the forward)
-  if (DM == 2) {
-    const uint4* mp = reinterpret_cast<const uint4*>(maskw + (int64_t)rowc * 8);
-    const uint4 m0 = qok ? mp[0] : make_uint4(0, 0, 0, 0), m1 = qok ? mp[1] : make_uint4(0, 0, 0, 0);
-    mw[0] = m0.x; mw[1] = m0.y; mw[2] = m0.z; mw[3] = m0.w; mw[4] = m1.x; mw[5] = m1.y; mw[6] = m1.z; mw[7] = m1.w;
-  }
-  f32x4 P[16], PD[16];
-  float dl = 0.f;
-#pragma unroll
-  for (int kt = 0; kt < 16; ++kt) {
-    f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int TP = T + (T & 1);
+  const int qt0 = qh * (FWD_QB / 16) + w;
+  for (int qt = qt0; qt < qt0 + FWD_QB / 16 && qt * 16 < T; qt += 4) {
+    uint32_t obase = 0;   // opaque image bases: no hoisting of the unrolled body's LDS addresses
+    asm volatile("" : "+v"(obase));
+    const char* Kimg = smem + obase;
+    const char* Vimg = smem + TMAX * 128 + obase;
+    const int q = qt * 16 + lr;
+    const bool qok = q < T;
+    bf16x8 qf[2], df[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      sv = mfma(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], sv);
-      dp = mfma(row_frag(Vimg, kt * 16 + lr, 32 * ks + 8 * g), df[ks], dp);
+      qf[ks] = df[ks] = bf16x8{};
+      if (qok) {
+        qf[ks] = gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g);
+        df[ks] = gload8(dO16 + (row0 + q) * D + h * DH + 32 * ks + 8 * g);
+      }
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = kt * 16 + 4 * g + i;
-      const bool ok = qok && key < T;
-      const float p = ok ? exp2_fast(sv[i] * c2 - ls) : 0.f;
-      const float kp = (DM == 2) ? (((mw[kt >> 1] >> ((kt & 1) * 16 + 4 * g + i)) & 1u) ? dc.scale : 0.f)
-                                       : keep_scale<DROP>(dc, rowidx + key);
-      const float pd = ok ? dp[i] * kp : 0.f;
-      P[kt][i] = p;
-      PD[kt][i] = pd;
-      dl += p * pd;
+    const int64_t rowc = ((int64_t)b * nh + h) * T + (qok ? q : 0);
+    const float ls = qok ? lse2[rowc] : 0.f;
+    const uint64_t rowidx = (uint64_t)rowc * (uint64_t)TP;
+    uint32_t mw[8];   // this query row's keep bits (from the forward)
+    if (DM == 2) {
+      const uint4* mp = reinterpret_cast<const uint4*>(maskw + (int64_t)rowc * 8);
+      const uint4 m0 = qok ? mp[0] : make_uint4(0, 0, 0, 0), m1 = qok ? mp[1] : make_uint4(0, 0, 0, 0);
+      mw[0] = m0.x; mw[1] = m0.y; mw[2] = m0.z; mw[3] = m0.w; mw[4] = m1.x; mw[5] = m1.y; mw[6] = m1.z; mw[7] = m1.w;
     }
-  }
-  dl += __shfl_xor(dl, 16, 64);
-  dl += __shfl_xor(dl, 32, 64);
-  if (qok && g == 0) delta[rowc] = dl;
-  f32x4 dq[4];
+    f32x4 P[16], PD[16];
+    float dl = 0.f;
 #pragma unroll
-  for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int kt = 0; kt < 16; ++kt) {
+      f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int c = 0; c < 8; ++c) {
-    f32x4 ds[2];
+      for (int ks = 0; ks < 2; ++ks) {
+        sv = mfma(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], sv);
+        dp = mfma(row_frag(Vimg, kt * 16 + lr, 32 * ks + 8 * g), df[ks], dp);
+      }
 #pragma unroll
-    for (int half = 0; half < 2; ++half)
+      for (int i = 0; i < 4; ++i) {
+        const int key = kt * 16 + 4 * g + i;
+        const bool ok = qok && key < T;
+        const float p = ok ? exp2_fast(sv[i] * c2 - ls) : 0.f;
+        const float kp = (DM == 2) ? (((mw[kt >> 1] >> ((kt & 1) * 16 + 4 * g + i)) & 1u) ? dc.scale : 0.f)
+                                         : keep_scale<DROP>(dc, rowidx + key);
+        const float pd = ok ? dp[i] * kp : 0.f;
+        P[kt][i] = p;
+        PD[kt][i] = pd;
+        dl += p * pd;
+      }
+    }
+    dl += __shfl_xor(dl, 16, 64);
+    dl += __shfl_xor(dl, 32, 64);
+    if (qok && g == 0) delta[rowc] = dl;
+    f32x4 dq[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) ds[half][i] = P[2 * c + half][i] * (PD[2 * c + half][i] - dl);
-    const bf16x8 bs = pack_acc(ds[0], ds[1]);
+    for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-      dq[dt] = mfma(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dq[dt]);
-  }
-  if (qok) {
-    const int64_t r = (row0 + q) * ld + h * DH;
+    for (int c = 0; c < 8; ++c) {
+      f32x4 ds[2];
 #pragma unroll
-    for (int dt = 0; dt < 4; ++dt) store_out(dqkv, dqkv16, r + dt * 16 + 4 * g, dq[dt], scale);
+      for (int half = 0; half < 2; ++half)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ds[half][i] = P[2 * c + half][i] * (PD[2 * c + half][i] - dl);
+      const bf16x8 bs = pack_acc(ds[0], ds[1]);
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt)
+        dq[dt] = mfma(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dq[dt]);
+    }
+    if (qok) {
+      const int64_t r = (row0 + q) * ld + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) store_out(dqkv, dqkv16, r + dt * 16 + 4 * g, dq[dt], scale);
+    }
   }
 }
 
@@ -429,7 +469,7 @@ DropCfg drop_cfg(float p, uint64_t seed) {
   return d;
 }
 constexpr size_t FWD_LDS = 2 * TMAX * 128;
-constexpr size_t BWD_LDS = 2 * TMAX * 128 + 2 * TMAX * 4 + 2 * TMAX * 4;
+constexpr size_t BWD_LDS = 2 * TMAX * 128 + 2 * TMAX * 4 + 4 * TMAX * 4;
 
 template <typename K>
 int set_lds(K kern, size_t bytes) {
@@ -461,16 +501,18 @@ extern "C" int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t
   B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_fwd: needs head size 64 and T <= 256");
   if (B <= 0) return 0;
   if (init_attrs()) return 2;
-  dim3 grid((unsigned)((T + 63) / 64), (unsigned)nh, (unsigned)B);
+  B2P_CHECK_ARG(B * nh * T * (T + (T & 1)) < (1ll << 32), "attn16_fwd: B * heads * T * T must stay below 2^32 "
+                "(32-bit dropout element index)");
+  dim3 grid((unsigned)(B * nh * ((T + FWD_QB - 1) / FWD_QB)));
   const DropCfg dc = drop_cfg(drop_p, drop_seed);
   if (drop_p > 0.f && mask)
-    hipLaunchKernelGGL(attn16_fwd_k<2>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
+    hipLaunchKernelGGL(attn16_fwd_k<2>, grid, dim3(FWD_NT), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
                        (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, mask);
   else if (drop_p > 0.f)
-    hipLaunchKernelGGL(attn16_fwd_k<1>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
+    hipLaunchKernelGGL(attn16_fwd_k<1>, grid, dim3(FWD_NT), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
                        (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, (uint32_t*)nullptr);
   else
-    hipLaunchKernelGGL(attn16_fwd_k<0>, grid, dim3(256), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
+    hipLaunchKernelGGL(attn16_fwd_k<0>, grid, dim3(FWD_NT), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
                        (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, (uint32_t*)nullptr);
   B2P_CHECK_LAUNCH();
   return 0;
@@ -483,16 +525,17 @@ extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* 
   B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_bwd: needs head size 64 and T <= 256");
   if (B <= 0) return 0;
   if (init_attrs()) return 2;
-  dim3 grid((unsigned)((T + 63) / 64), (unsigned)nh, (unsigned)B);
+  const dim3 grid_q((unsigned)(B * nh * ((T + FWD_QB - 1) / FWD_QB)));
+  const dim3 grid_k((unsigned)(B * nh * ((T + BWD_KB - 1) / BWD_KB)));
   const DropCfg dc = drop_cfg(drop_p, drop_seed);
   hipStream_t st = (hipStream_t)stream;
   const uint16_t *q = (const uint16_t*)qkv16, *d = (const uint16_t*)dO16;
   uint16_t* d16 = (uint16_t*)dqkv16;
   auto run = [&](auto dm) {
     constexpr int DM = decltype(dm)::value;
-    hipLaunchKernelGGL(attn16_bwd_dq_k<DM>, grid, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
+    hipLaunchKernelGGL(attn16_bwd_dq_k<DM>, grid_q, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
                        (int)nh, scale, dc, mask);
-    hipLaunchKernelGGL(attn16_bwd_dkv_k<DM>, grid, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
+    hipLaunchKernelGGL(attn16_bwd_dkv_k<DM>, grid_k, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
                        (int)nh, scale, dc, mask);
   };
   if (drop_p > 0.f && mask) run(std::integral_constant<int, 2>());

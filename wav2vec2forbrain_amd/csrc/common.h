@@ -17,7 +17,10 @@ __device__ __forceinline__ uint2 b2p_pack_bf16x4(float4 v) {
   return make_uint2((uint32_t)b2p_bf16_bits(v.x) | ((uint32_t)b2p_bf16_bits(v.y) << 16),
                     (uint32_t)b2p_bf16_bits(v.z) | ((uint32_t)b2p_bf16_bits(v.w) << 16));
 }
-__device__ __forceinline__ uint16_t b2p_f16_bits(float v) { return __builtin_bit_cast(uint16_t, (_Float16)v); }
+// fp16 with saturation: finite values beyond fp16's range clamp to +-65504 instead of becoming
+// infinities in a GEMM operand (the Conformer's fp16 forward operands, Fn.forward_f16); NaN stays NaN
+__device__ __forceinline__ float b2p_f16_sat(float v) { return fabsf(v) > 65504.f ? copysignf(65504.f, v) : v; }
+__device__ __forceinline__ uint16_t b2p_f16_bits(float v) { return __builtin_bit_cast(uint16_t, (_Float16)b2p_f16_sat(v)); }
 // 16-bit bits of v: fp16 when half, else bf16
 __device__ __forceinline__ uint16_t b2p_16_bits(float v, bool half) { return half ? b2p_f16_bits(v) : b2p_bf16_bits(v); }
 __device__ __forceinline__ uint2 b2p_pack16x4(float4 v, bool half) {

@@ -304,7 +304,8 @@ __global__ void ln_bwd_scatter(const float* __restrict__ red3, int cols, float* 
 }
 
 // ------------------------------------------------------------------ attention softmax
-// one wave per row, row length n <= 64*8
+// one wave per row, row length n <= 64*8; dropout element index row * (n rounded up to even) + c (the
+// fused attention kernels draw the same mask, csrc/attn16.hip)
 constexpr int SM_MAXE = 8;
 __global__ void __launch_bounds__(256) softmax_fwd_k(const float* __restrict__ S, float* __restrict__ P,
                                                      float* __restrict__ Pd, int64_t rows, int n, int64_t ld,
@@ -340,7 +341,7 @@ __global__ void __launch_bounds__(256) softmax_fwd_k(const float* __restrict__ S
     if (c < n) {
       const float p = v[i] * inv;
       pr[c] = p;
-      if (drop_p > 0.f) pdr[c] = b2p_keep(seed, (uint64_t)row * n + c, thr) ? p * dscale : 0.f;
+      if (drop_p > 0.f) pdr[c] = b2p_keep(seed, (uint64_t)row * (n + (n & 1)) + c, thr) ? p * dscale : 0.f;
       else pdr[c] = p;
     } else if (c < ld) {
       pr[c] = 0.f;
@@ -366,7 +367,7 @@ __global__ void __launch_bounds__(256) softmax_bwd_k(const float* __restrict__ P
     const int c = lane + 64 * i;
     p[i] = c < n ? pr[c] : 0.f;
     float gv = c < n ? gr[c] : 0.f;
-    if (drop_p > 0.f && c < n) gv = b2p_keep(seed, (uint64_t)row * n + c, thr) ? gv * dscale : 0.f;
+    if (drop_p > 0.f && c < n) gv = b2p_keep(seed, (uint64_t)row * (n + (n & 1)) + c, thr) ? gv * dscale : 0.f;
     g[i] = gv;
     s += p[i] * gv;
   }
@@ -669,7 +670,7 @@ __global__ void __launch_bounds__(256) cast16_2d_k(const float* __restrict__ x, 
   const float* xs = x + r * ldx + c;
   uint16_t* ys = y + r * ldy + c;
   auto cvt = [](float v) -> uint16_t {
-    if constexpr (H) return __builtin_bit_cast(uint16_t, (_Float16)v);
+    if constexpr (H) return b2p_f16_bits(v);
     else return b2p_bf16_bits(v);
   };
   if (VEC && c + 4 <= C) {

@@ -53,7 +53,7 @@ __device__ __forceinline__ void st4(typename Prec<PREC, KB>::T* dst, float a, fl
     bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
     *reinterpret_cast<bf16x4*>(dst) = v;
   } else if constexpr (PREC == 2) {
-    f16x4 v = {(_Float16)a, (_Float16)b, (_Float16)c, (_Float16)d};
+    f16x4 v = {(_Float16)b2p_f16_sat(a), (_Float16)b2p_f16_sat(b), (_Float16)b2p_f16_sat(c), (_Float16)b2p_f16_sat(d)};
     *reinterpret_cast<f16x4*>(dst) = v;
   } else {
     dst[0] = a; dst[1] = b; dst[2] = c; dst[3] = d;

@@ -263,13 +263,10 @@ struct Cfg {
   static constexpr int LDS = LDS_MAIN > LDS_EPI ? LDS_MAIN : LDS_EPI;
   static constexpr int OCC = LDS > 80 * 1024 ? 1 : 2;           // workgroups per CU
 };
-using CfgSmall = Cfg<128, 128, 32, 3>;   // 4 waves, 2 workgroups/CU (default)
-using CfgSmall64 = Cfg<128, 128, 64, 2>; // 4 waves, 2 workgroups/CU, half the barriers (small grids)
-using CfgN64 = Cfg<128, 64, 32, 3>;     // 2 waves, 128 x 64 tiles: twice the workgroups for N <= 1024 grids
-                                         // (k-contiguous operands only: the mn-contiguous swizzle needs 128)
-using CfgSmall4 = Cfg<128, 128, 32, 4>; // 4 waves, 2 workgroups/CU, 3 k-tiles in flight (B2P_GEMM16_S4=1)
-using CfgBig = Cfg<256, 128, 64, 3>;     // 8 waves, 1 workgroup/CU (measured slower on the step's shapes:
-                                         // lock-stepped waves leave the MFMA pipe idle at every barrier)
+using CfgSmall = Cfg<128, 128, 32, 3>;   // 4 waves, 3 workgroups/CU by LDS (48 KB) and VGPRs (143)
+// Measured and removed (DESIGN.md "rejected"): 128 x 128 x 64 two-stage tiles (no gain inside the step),
+// 128 x 64 tiles for N <= 1024 grids (59.3 -> 57.1 steps/s), 4-stage 128 x 128 x 32 (-10 % at K = 768),
+// 256 x 128 x 64 eight-wave tiles (lock-stepped waves idle the MFMA pipe at every barrier).
 
 // H16: the operands are fp16 (Operand.dtype 2, precision 2) and feed v_mfma_f32_16x16x32_f16; the
 // data movement is the same 16-bit copy either way
@@ -627,20 +624,10 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   }
   const int ks = d.ksplit > 1 ? d.ksplit : 1;
   const int64_t nz = (int64_t)d.nz1 * d.nz2 * ks;
-  // big tile (opt-in, B2P_GEMM16_BIG=1): one unsplit, unbatched, plain (non-conv) operand pair with a
-  // grid that still fills the chip
-  static int big_ok = getenv("B2P_GEMM16_BIG") ? atoi(getenv("B2P_GEMM16_BIG")) : 0;
-  const int64_t tiles_big = ((d.M + 255) / 256) * ((d.N + 127) / 128);
   const bool h16 = d.A.dtype == 2;
   if (h16 && d.A.conv) {
     b2p_set_error("gemm16: fp16 operands support plain (non-conv) views only");
     return 1;
-  }
-  const bool big = !h16 && big_ok && ks == 1 && nz == 1 && !d.A.conv && d.K >= 512 && tiles_big >= 192;
-  if (big) {
-    const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 127) / 128);
-    launch_cfg<CfgBig>(d, ea, st, dim3((unsigned)((int64_t)tm * tn)), tm, tn);
-    return 0;
   }
   // 256 x 256 ping-pong tile (B2P_GEMM16_PP: 0 off, 1 (default) for long-K launches whose grid fills
   // most of the chip, 2 always for plain operands). One workgroup per CU cannot hide its epilogue
@@ -670,28 +657,6 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
     b2p_set_error("gemm16: split-K chunk must be a multiple of 32");
     return 1;
   }
-  // 64-deep K tiles (half the barriers) measured -4..6 % on grids of <= 2 tiles per CU slot in
-  // isolation (N = 768 encoder shapes) and +10 % at N = 2304, but no gain inside the step (graph
-  // replay, side stream beside): B2P_GEMM16_K64 = 0 never (default), 1 always, -1 by grid size.
-  static int k64 = getenv("B2P_GEMM16_K64") ? atoi(getenv("B2P_GEMM16_K64")) : 0;
-  const bool use64 = k64 == 1 || (k64 < 0 && nwg <= 512);
-  // narrow grids (N = 768 / 1024 projections: 378-504 tiles of 128 x 128 for 256 CUs) on 128 x 64 tiles:
-  // B2P_GEMM16_N64 = 1 when the 128 x 128 grid has < 512 tiles (default 0: measured slower, 59.3 -> 57.1
-  // steps/s on the base step; the 2-wave workgroups hide less latency than the 4-wave 128 x 128 ones)
-  static int n64 = getenv("B2P_GEMM16_N64") ? atoi(getenv("B2P_GEMM16_N64")) : 0;
-  if (n64 && d.A.inner_is_k && d.B.inner_is_k && !d.A.conv && nwg < 512 && d.N <= 1024 &&
-      (ks == 1 || d.kchunk % 32 == 0)) {
-    const int tn64 = (int)((d.N + 63) / 64);
-    const dim3 grid((unsigned)((int64_t)tm * tn64 * nz)), block(CfgN64::NT);
-    if (h16) hipLaunchKernelGGL((gemm16_kernel<CfgN64, true, true, false, true>), grid, block, 0, st, d, ea, tm, tn64,
-                                gemm16_group(false));
-    else hipLaunchKernelGGL((gemm16_kernel<CfgN64, true, true, false>), grid, block, 0, st, d, ea, tm, tn64,
-                            gemm16_group(false));
-    return 0;
-  }
-  static int s4 = getenv("B2P_GEMM16_S4") ? atoi(getenv("B2P_GEMM16_S4")) : 0;
-  if (use64 && !h16 && (ks == 1 || d.kchunk % 64 == 0)) launch_cfg<CfgSmall64>(d, ea, st, dim3((unsigned)nwg), tm, tn);
-  else if (s4) launch_cfg<CfgSmall4>(d, ea, st, dim3((unsigned)nwg), tm, tn);
-  else launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
+  launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   return 0;
 }

@@ -69,7 +69,8 @@ __device__ __forceinline__ float4 f4(const f32x4& a) { return make_float4(a[0], 
 
 // Sweep N granules per lane (stride NTH, starting at this lane) until every tag == tag; the values
 // go to u32 LDS words at dst(q). On timeout the kernel records `fail` and stops waiting (the results
-// are then garbage, the launch still terminates).
+// are then garbage, the launch still terminates); the caller folds `fail` into a persistent status
+// word right after the launch (b2p_gru_mc_status), which the host checks at its next sync and raises.
 template <int N, typename Tag, typename Dst>
 __device__ __forceinline__ void sweep(const unsigned long long* slot, Tag tag_ok, Dst dst, int* fail, bool& dead) {
   static_assert(N <= 64, "one 64-bit pending mask per lane");
@@ -159,7 +160,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
                                                     const float* __restrict__ bhh, const float* __restrict__ h0,
                                                     float* __restrict__ out, float* __restrict__ saved,
                                                     unsigned long long* xch, unsigned long long* ids, int* fail, int B,
-                                                    int T, int ndir, int nbg) {
+                                                    int T, int ndir, int nbg, int withhold) {
   constexpr int P = H / UPM;
   constexpr int KS = H / 32;
   constexpr int HPW = H / 2 + 4;              // u32 words per batch row of the h image (16-B stagger)
@@ -274,7 +275,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
     }
     // publish h_s (bf16 pairs) FIRST: the other members wait on it, and a later store or load issued
     // before it would delay it; then this step's outputs and the next step's input projection
-    if (s + 1 < T) {
+    if (s + 1 < T && m != withhold) {   // withhold: test knob (b2p_gru_mc_debug_withhold), -1 = off
       unsigned long long* dst = xg + (s & 1) * P * 512 + m * 512 + lr * 32 + w * 8 + lq * 2;
       put_granule(dst, (unsigned)(s + 1), pack2(hh[0], hh[1]), local);
       put_granule(dst + 1, (unsigned)(s + 1), pack2(hh[2], hh[3]), local);
@@ -303,7 +304,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_bwd(const float* __restrict__ do
                                                     const float* __restrict__ h0, float* __restrict__ dgi,
                                                     float* __restrict__ dgh, float* __restrict__ dh0,
                                                     unsigned long long* xch, unsigned long long* ids, int* fail, int B,
-                                                    int T, int ndir, int nbg) {
+                                                    int T, int ndir, int nbg, int withhold) {
   constexpr int P = H / UPM;
   constexpr int G3 = 3 * H;
   constexpr int KS = G3 / 32;                  // k-steps over all gate rows
@@ -423,7 +424,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_bwd(const float* __restrict__ do
       dhn[i] = bok ? dh : 0.f;
       zn[i] = z4[i];
     }
-    if (s > 0 || dh0) {   // the step before (or dh0) needs this step's dgh
+    if ((s > 0 || dh0) && m != withhold) {   // the step before (or dh0) needs this step's dgh
       unsigned long long* dst = xg + (s & 1) * P * 1024 + m * 1024 + lr * 64 + w * 16 + lq * 4;
       const unsigned tag = (unsigned)(s + 1);
 #pragma unroll
@@ -448,6 +449,9 @@ constexpr size_t bwd_lds() { return (size_t)2 * BG * (3 * H + 8) * 2; }
 
 int grid_blocks(int P, int ngroups) { return ngroups <= 8 ? 8 * P : ngroups * P; }
 
+// test knob (b2p_gru_mc_debug_withhold): this member skips its granule stores, so the others time out
+int g_withhold = -1;
+
 template <int H>
 int launch_fwd(const float* gi, const float* whh, const float* bhh, const float* h0, float* out, float* saved,
                unsigned long long* xch, unsigned long long* ids, int* fail, int B, int T, int ndir, hipStream_t st) {
@@ -459,7 +463,7 @@ int launch_fwd(const float* gi, const float* whh, const float* bhh, const float*
   }
   const int nbg = (B + BG - 1) / BG;
   hipLaunchKernelGGL(grumc_fwd<H>, dim3(grid_blocks(H / UPM, ndir * nbg)), dim3(NTH), fwd_lds<H>(), st, gi, whh, bhh,
-                     h0, out, saved, xch, ids, fail, B, T, ndir, nbg);
+                     h0, out, saved, xch, ids, fail, B, T, ndir, nbg, g_withhold);
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -476,7 +480,7 @@ int launch_bwd(const float* dout, const float* whh, const float* out, const floa
   }
   const int nbg = (B + BG - 1) / BG;
   hipLaunchKernelGGL(grumc_bwd<H>, dim3(grid_blocks(H / UPM, ndir * nbg)), dim3(NTH), bwd_lds<H>(), st, dout, whh,
-                     out, saved, h0, dgi, dgh, dh0, xch, ids, fail, B, T, ndir, nbg);
+                     out, saved, h0, dgi, dgh, dh0, xch, ids, fail, B, T, ndir, nbg, g_withhold);
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -487,9 +491,27 @@ __global__ void zero16_k(uint4* __restrict__ p, int64_t n16) {
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
     p[i] = make_uint4(0u, 0u, 0u, 0u);
 }
+
+__global__ void mc_status_k(const int* __restrict__ fail, int32_t* status, int32_t code) {
+  if (threadIdx.x == 0 && fail[0] != 0) atomicCAS(status, 0, code);
+}
 }  // namespace
 
 extern "C" int b2p_gru_mc_supported(int64_t H) { return mc_supported(H) ? 1 : 0; }
+
+extern "C" int b2p_gru_mc_status(const void* workspace, int32_t* status, int32_t code, b2p_stream_t stream) {
+  B2P_CHECK_ARG(workspace && status, "gru_mc_status: NULL pointer");
+  B2P_CHECK_ARG(code != 0, "gru_mc_status: code must be nonzero");
+  hipLaunchKernelGGL(mc_status_k, dim3(1), dim3(64), 0, (hipStream_t)stream, (const int*)workspace, status, code);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_gru_mc_debug_withhold(int member) {
+  B2P_CHECK_ARG(member >= -1 && member < 16, "gru_mc_debug_withhold: member must be -1 (off) or 0..15");
+  g_withhold = member;
+  return 0;
+}
 
 // exchange buffer (bytes, before the 16-B-aligned fail word block): 2 slots x granules per group
 extern "C" int64_t b2p_gru_mc_workspace(int64_t B, int64_t H, int ndir) {
@@ -546,6 +568,8 @@ extern "C" int b2p_gru_bwd_mc(const float* dout, const float* whh, const float* 
   const int nbg = (int)((B + BG - 1) / BG);
   B2P_CHECK_ARG(grid_blocks((int)(H / UPM), ndir * nbg) <= 256 && ndir * nbg <= MAX_GROUPS,
                 "gru_bwd_mc: more recurrences than CUs");
+  // the backward granule carries a 16-bit step tag (dgh_granule): tags 1..T must stay distinct
+  B2P_CHECK_ARG(T + 1 <= 0xFFFF, "gru_bwd_mc: T = %lld exceeds the 16-bit step tag", (long long)T);
   hipStream_t st = (hipStream_t)stream;
   unsigned long long *xch, *ids;
   int* fail;

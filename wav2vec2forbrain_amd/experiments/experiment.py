@@ -8,7 +8,8 @@ Differences, all offline / platform consequences:
     construction, :87-95) is not loaded: the hub is unreachable and nothing on the training path
     uses it.
   * data-parallel runs (torchrun, one process per GPU): the train loader is sharded with a
-    DistributedSampler, the seed is offset by the rank for data order only, rank 0 writes results.
+    DistributedSampler (reshuffled every epoch by the Trainer's set_epoch), the dropout seed stream
+    is offset by the rank (host torch seed equal on all ranks), rank 0 writes results.
   * the model's training step runs on the HIP kernels (functional.py); the optimizer is the
     multi-tensor HIP Adam (optim.HipAdam) with the reference's arguments (SGD stays torch's).
 """
@@ -53,6 +54,12 @@ class Experiment(metaclass=ABCMeta):
         np.random.seed(self.base_config.seed)
         self.yaml_config = yamlConfig
         self.rank, self.world = rank_world()
+        # the host torch seed stays equal on every rank (identical initial weights, identical host
+        # LayerDrop draws in eager steps); the dropout masks and the device LayerDrop draws of captured
+        # steps come from the functional seed stream, offset by the rank so that the ranks' halves of a
+        # global batch draw independent masks, as one process would over its rows
+        from .. import functional as Fn
+        Fn.SEEDS.reseed(self.base_config.seed * 65537 + self.rank)
 
         self.dataloader_train = self._create_dataloader(split="train")
         self.dataloader_val = self._create_dataloader(split="val")
@@ -70,7 +77,9 @@ class Experiment(metaclass=ABCMeta):
             with open(os.path.join(self.results_dir, "config.json"), "w") as f:
                 json.dump(dict(config, repro_cmd="python " + " ".join(sys.argv)), f, indent=5)
 
-        self.model = self._create_model().cuda()
+        from ..model.w2v_custom_feat_extractor import weights_loaded_later
+        with weights_loaded_later(self.base_config.from_checkpoint is not None):
+            self.model = self._create_model().cuda()
         if self.base_config.from_checkpoint is not None:
             print(f"loading model from checkpoint {self.base_config.from_checkpoint}")
             state = torch.load(self.base_config.from_checkpoint, map_location="cuda", weights_only=True)

@@ -486,7 +486,12 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
                              aconv=int(A.conv), bconv=int(B.conv), ksplit=int(d.ksplit),
                              epi="".join(c for c, f in (("b", bias is not None), ("a", act != 0), ("g", act_bwd != 0),
                                                         ("d", drop_p > 0), ("r", residual is not None),
-                                                        ("h", C16 is not None), ("f", C is not None)) if f)))
+                                                        ("h", C16 is not None), ("f", C is not None)) if f),
+                             # output-side bytes the epilogue must move once (writes + residual / aux / C reads)
+                             out_bytes=M * N * nz1 * nz2 * (4 * (C is not None) + 4 * (pre_out is not None)
+                                                            + 2 * (C16 is not None) + 2 * (pre16 is not None)
+                                                            + 4 * (residual is not None) + 4 * (beta != 0.0)
+                                                            + (2 if aux16 is not None else 4 if aux is not None else 0))))
     _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
 
 
@@ -877,6 +882,70 @@ def _gru_mc_ws(B, H, ndir, dev):
     return torch.empty(int(_lib.load().b2p_gru_mc_workspace(B, H, ndir)), device=dev, dtype=torch.uint8)
 
 
+# Multi-CU GRU timeouts (csrc/grumc.hip): a member that never publishes its state leaves the others
+# to time out with garbage results. Every launch folds its timeout flag into one persistent device
+# word per device (b2p_gru_mc_status: the first failure's code is kept); the host reads it at its
+# next sync (the loss readback of a forward with sync_metrics, the Trainer after a replay) and raises.
+_GRU_STATUS: dict = {}      # device -> int32[1]
+_GRU_LAYERS: dict = {}      # id(W_hh of direction 0) -> layer number (order of first use)
+
+
+def _gru_status_word(dev):
+    st = _GRU_STATUS.get(dev)
+    if st is None:
+        st = _GRU_STATUS[dev] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return st
+
+
+def _gru_mc_code(kind: int, whh0, H: int) -> int:
+    n = _GRU_LAYERS.setdefault(id(whh0), len(_GRU_LAYERS))
+    return kind * 65536 + (n % 4096) * 16 + {256: 1, 384: 2, 512: 3}.get(H, 0)
+
+
+def _gru_mc_fold(ws, kind, whh0, H, dev):
+    _lib.call("b2p_gru_mc_status", _p(ws), _p(_gru_status_word(dev)), _gru_mc_code(kind, whh0, H), _st())
+
+
+def _gru_status_error(code: int) -> RuntimeError:
+    kind = {1: "forward", 2: "backward"}.get(code // 65536, "?")
+    n, h = (code % 65536) // 16, {1: 256, 2: 384, 3: 512}.get(code % 16, "?")
+    return RuntimeError(f"multi-CU GRU recurrence timed out ({kind} of GRU layer {n}, H={h}; recurrence id "
+                        f"{code}): a member workgroup never published its state (not co-resident?), so the "
+                        "layer's outputs / gradients of that step are invalid")
+
+
+def gru_status_value(dev=None) -> int:
+    """Current status word (0 = no multi-CU GRU timeout since the last check); a host sync."""
+    dev = dev if dev is not None else torch.device("cuda", torch.cuda.current_device())
+    st = _GRU_STATUS.get(torch.device(dev))
+    return 0 if st is None else int(st.item())
+
+
+def check_gru_status(dev=None) -> None:
+    """Raises RuntimeError if a multi-CU GRU launch on `dev` (default: every device used) timed out
+    since the last check (then the word is cleared). One host sync per device."""
+    for d, st in list(_GRU_STATUS.items()):
+        if dev is not None and d != torch.device(dev):
+            continue
+        code = int(st.item())
+        if code:
+            st.zero_()
+            raise _gru_status_error(code)
+
+
+def loss_item(loss: torch.Tensor) -> float:
+    """loss.item() (the reference's per-step readback, w2v_custom_feat_extractor.py:94) with the
+    multi-CU GRU status word of the loss's device in the same transfer: raises on a timeout."""
+    st = _GRU_STATUS.get(loss.device)
+    if st is None:
+        return loss.item()
+    v, code = torch.stack([loss.detach().reshape(()).float(), st.reshape(()).float()]).tolist()
+    if code:
+        st.zero_()
+        raise _gru_status_error(int(code))
+    return v
+
+
 def _ln_floats(B, T, H, ndir, R):
     return int(_lib.load().b2p_gru16_lane_floats(B, T, H, ndir, R))
 
@@ -956,14 +1025,17 @@ class _GRULayer(torch.autograd.Function):
             _lib.call("b2p_gru_lane_permute", _p(hL), _p(out), B, T, H, ndir, 1, 1, 0x0, 0, _st())
         elif usemc:
             hL = None
-            _lib.call("b2p_gru_fwd_mc", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved),
-                      _p(_gru_mc_ws(B, H, ndir, dev)), B, T, H, ndir, _st())
+            ws = _gru_mc_ws(B, H, ndir, dev)
+            _lib.call("b2p_gru_fwd_mc", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved), _p(ws), B, T, H,
+                      ndir, _st())
+            _gru_mc_fold(ws, 1, whh[0], H, dev)
         else:
             hL = None
             _lib.call("b2p_gru_fwd", _p(gi), _p(whh_s), _p(bhh_s), _p(h0), _p(out), _p(saved), B, T, H, ndir,
                       _st())
         ctx.save_for_backward(x, out, saved, whh_s, h0, wperm, hL, U16, *wih)
         ctx.meta = (unf_meta, H, ndir, B, T, IN, bih[0] is not None, bhh[0] is not None, use16, usemc)
+        ctx.whh0 = whh[0]
         return out
 
     @staticmethod
@@ -996,6 +1068,7 @@ class _GRULayer(torch.autograd.Function):
             ev.record()
             _lib.call("b2p_gru_bwd_mc", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi), _p(dgh), _p(dh0),
                       _p(ws), B, T, H, ndir, _st())
+            _gru_mc_fold(ws, 2, ctx.whh0, H, dev)
             flush_wgrad(ev)   # frozen-parameter gradient GEMMs beside the (H/64 x 4)-CU recurrence
         else:
             dhbuf = torch.empty(ndir, B, H, device=dev)
@@ -1189,6 +1262,15 @@ def capturing() -> bool:
 # B2P_LAYERDROP_GATE=0: a skipped layer still computes (diagnostic / A-B of the gate)
 LAYERDROP_GATE = os.environ.get("B2P_LAYERDROP_GATE", "1") != "0"
 _GATE_FLAGS: list = []
+# parameter id -> (weak reference, the device gate of its layer in the most recently captured step).
+# HipAdam reads it while capturing: a parameter of a layer this replay dropped is left untouched, as
+# torch.optim.Adam leaves a parameter whose .grad is None (the reference never ran that layer).
+_LD_PARAM_GATE: dict = {}
+
+
+def layerdrop_param_gates() -> dict:
+    """{id(parameter): int32 device flag (1 = its layer ran in this replay)} of the last capture."""
+    return {k: f for k, (r, f) in _LD_PARAM_GATE.items() if r() is not None}
 
 
 def layerdrop_layer(layer, x, p):
@@ -1202,12 +1284,14 @@ def layerdrop_layer(layer, x, p):
     bufs = [b for b in layer.buffers() if b.is_floating_point() and b.numel() % 4 == 0]
     olds = [b.clone() for b in bufs]
     y = None
+    flag = torch.empty(1, dtype=torch.int32, device=x.device)
+    _GATE_FLAGS.append(flag)      # referenced by the captured graph's kernels: kept for its life
+    _lib.call("b2p_layerdrop_flag", _p(flag), float(p), seed, _st())
+    for prm in layer.parameters():
+        _LD_PARAM_GATE[id(prm)] = (weakref.ref(prm), flag)
     if LAYERDROP_GATE:
         # the layer's GEMMs and fused attention (forward, backward, deferred weight gradients) read
         # this replay's draw and do no work when it skips the layer; the select below still routes
-        flag = torch.empty(1, dtype=torch.int32, device=x.device)
-        _GATE_FLAGS.append(flag)      # referenced by the captured graph's kernels: kept for its life
-        _lib.call("b2p_layerdrop_flag", _p(flag), float(p), seed, _st())
         with _gated(flag):
             y = layer(x)
     else:
@@ -1801,7 +1885,10 @@ def token_char_table(vocab, device):
 def ctc_greedy_cer(logits, targets, vocab, blank=0, eos=2, delim=4):
     """Device-side character error rate of the greedy decode (csrc/decode.hip; reference
     EvaluatorWithW2vLMDecoder.calculate_char_error_rate, src/train/evaluator.py:212-214,231-242).
-    Returns (cer 0-d tensor, char_errs (B,) int32, nchars (B,) int32)."""
+    Returns (cer 0-d tensor, char_errs (B,) int32, nchars (B,) int32). A row whose decoded string
+    overflows the kernel's per-row buffer reports char_errs = -1 and nchars = 0; such rows are left
+    out of `cer`, so callers must check char_errs < 0 and score those rows on the host (the
+    evaluator does: train/evaluator.py)."""
     _chk(logits, "ctc_greedy_cer.logits")
     B, T, C = logits.shape
     targets = targets.to(torch.int64).contiguous()
@@ -1814,7 +1901,7 @@ def ctc_greedy_cer(logits, targets, vocab, blank=0, eos=2, delim=4):
     nch = torch.empty(B, device=dev, dtype=torch.int32)
     _lib.call("b2p_ctc_greedy_cer", _p(logits), B, T, C, targets.data_ptr(), S, blank, eos, delim, chars.data_ptr(),
               lens.data_ptr(), errs.data_ptr(), nch.data_ptr(), _st())
-    cer = errs.sum().float() / nch.sum().clamp_min(1).float()
+    cer = errs.clamp_min(0).sum().float() / nch.sum().clamp_min(1).float()
     return cer, errs, nch
 
 

@@ -195,5 +195,5 @@ class W2VConformerBrainEncoderModel(B2TModel):
                     if batch.target_lens is not None and encoded_brain.logit_lens is not None else None)
         metrics = {}
         if ctc_loss is not None:
-            metrics["ctc_loss"] = ctc_loss.item() if self.sync_metrics else ctc_loss.detach()
+            metrics["ctc_loss"] = Fn.loss_item(ctc_loss) if self.sync_metrics else ctc_loss.detach()
         return ModelOutput(w2v_output, metrics, loss=ctc_loss)

@@ -198,18 +198,46 @@ class Wav2Vec2WithoutFeatExtrForCTC(nn.Module):
         return logits, hidden_states
 
 
+# Set while an Experiment builds its model with --from_checkpoint: the whole state dict is loaded
+# right after construction, so a hub name that cannot be fetched offline is not an error then.
+_WEIGHTS_LOADED_LATER = [False]
+
+
+class weights_loaded_later:
+    def __init__(self, on: bool):
+        self.on = bool(on)
+
+    def __enter__(self):
+        self.old = _WEIGHTS_LOADED_LATER[0]
+        _WEIGHTS_LOADED_LATER[0] = self.on or self.old
+
+    def __exit__(self, *exc):
+        _WEIGHTS_LOADED_LATER[0] = self.old
+
+
 def _load_or_note(w2v_encoder, wav2vec_checkpoint: str) -> None:
-    """Reference from_pretrained weight load (:43-51) from a local HF checkpoint directory; hub names
-    are unreachable offline (weights then come from load_state_dict / --from_checkpoint)."""
+    """Reference from_pretrained weight load (:43-51) from a local HF checkpoint directory. The
+    reference either loads the pretrained weights or fails; so does this: a hub name (unreachable
+    offline) raises, unless the weights come afterwards (--from_checkpoint, weights_loaded_later) or
+    the run opts into random-init encoder weights explicitly (B2P_RANDOM_W2V_WEIGHTS=1: synthetic
+    benchmarks and tests), instead of silently training against a random frozen encoder."""
     import os
     if os.path.isdir(wav2vec_checkpoint):
         from ..util.hf_weights import load_pretrained_w2v
         rep = load_pretrained_w2v(w2v_encoder, wav2vec_checkpoint)
         print(f"loaded {rep['loaded']} tensors from {wav2vec_checkpoint} (dropped {len(rep['dropped'])}; "
               f"positional-conv weight norm: {rep['pos_conv']})")
+    elif _WEIGHTS_LOADED_LATER[0]:
+        print(f"Note: {wav2vec_checkpoint} is not a local checkpoint directory; the encoder weights come from "
+              "the checkpoint loaded after construction")
+    elif os.environ.get("B2P_RANDOM_W2V_WEIGHTS") == "1":
+        print(f"Note: B2P_RANDOM_W2V_WEIGHTS=1: the {wav2vec_checkpoint} encoder keeps random-init weights")
     else:
-        print(f"Note: pretrained weights for {wav2vec_checkpoint} are not downloadable offline; "
-              "load them with load_state_dict / --from_checkpoint or pass a local checkpoint directory")
+        raise RuntimeError(
+            f"pretrained weights for {wav2vec_checkpoint!r} cannot be fetched (no network): pass a local HF "
+            "checkpoint directory as --wav2vec_checkpoint, load a full model with --from_checkpoint, set "
+            "--w2v_skip_loading_weights true (b2p2t_gru+w2v), or set B2P_RANDOM_W2V_WEIGHTS=1 to train "
+            "against random-init encoder weights on purpose")
 
 
 class W2VBrainEncoderModel(B2TModel):
@@ -248,6 +276,6 @@ class W2VBrainEncoderModel(B2TModel):
             if batch.target_lens is not None and encoded_brain.logit_lens is not None else None)
         metrics = {}
         if ctc_loss is not None:
-            metrics["ctc_loss"] = ctc_loss.item() if self.sync_metrics else ctc_loss.detach()
+            metrics["ctc_loss"] = Fn.loss_item(ctc_loss) if self.sync_metrics else ctc_loss.detach()
         return ModelOutput(w2v_output, metrics, loss=ctc_loss, logit_lens=encoded_brain.logit_lens,
                            hidden_states=hidden_states)

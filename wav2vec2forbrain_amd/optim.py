@@ -1,8 +1,21 @@
-"""HipAdam: torch.optim.Adam-compatible optimizer whose update runs in the multi-tensor HIP kernel
-(b2p_adam_multi). Same hyper-parameters, param-group semantics, state names (step, exp_avg,
+"""HipAdam: torch.optim.Adam-compatible optimizer whose update runs in the multi-tensor HIP kernels
+(csrc/adam.hip). Same hyper-parameters, param-group semantics, state names (step, exp_avg,
 exp_avg_sq) and numerics as torch.optim.Adam (amsgrad=False, maximize=False) — the optimizer the
 reference builds in src/experiments/experiment.py:25-28 / b2t_gru_w2v_experiment.py:138-145,
-so LR schedulers (StepLR, LambdaLR warmup) and state_dict round-trips work unchanged."""
+so LR schedulers (StepLR, LambdaLR warmup) and state_dict round-trips work unchanged.
+
+Two forms:
+  * host form (default): lr and the bias corrections are formed on the host per step, like
+    torch.optim.Adam; a parameter whose .grad is None is skipped.
+  * device form (make_capturable: captured / graph-replayed and data-parallel steps): every
+    parameter owns a device step counter, lr lives on the device, and each tensor may carry a device
+    gate (int32, 0 = leave the parameter untouched this step). torch.optim.Adam skips a parameter
+    whose .grad is None — no moment update, no weight decay, no step increment. Under LayerDrop the
+    reference never runs a dropped layer, so its parameters are such None-grad parameters; a captured
+    step runs every layer and hands the layer's gate (functional.layerdrop_param_gates) to the
+    update instead, and a data-parallel step hands the gate "some rank used it"
+    (train.ddp.GradBucketReducer.gates), so both leave exactly the reference's parameters alone.
+"""
 from __future__ import annotations
 
 import ctypes
@@ -20,37 +33,116 @@ class HipAdam(torch.optim.Optimizer):
             raise NotImplementedError("amsgrad is not used by the reference")
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.capturable = False
-        self._dev = []       # per param group: (lr float32[1], step float64[1], hyper float32[3]) on device
+        # device form, per param group: lr float32[1], per-parameter step counters float64[n],
+        # hyper scratch float32[2n], {id(p): index}
+        self._dev = []
+        # optional {id(p): int32 device tensor}: the caller's per-parameter gates (data-parallel
+        # steps: 0 = no rank used the parameter this step); device form only
+        self.gates = None
 
+    # ------------------------------------------------------------------ device form
     def make_capturable(self, device) -> None:
-        """Switch to the graph-replayable update (b2p_adam_multi_dev: lr and the step counter live on
-        the device, the bias corrections are formed there). Call before capturing a step; then call
-        prepare_replay() before and after_replay() after every replay."""
+        """Switch to the device form (graph-replayable update with per-parameter device step counters
+        and gates). Call before capturing a step; then call prepare_replay() before and
+        after_replay() after every replay. State is created here for every trainable parameter (zero
+        moments, step 0: what torch.optim.Adam creates at a parameter's first gradient), so nothing
+        is allocated inside a captured step. Idempotent: captured steps hold pointers to the device
+        counters, so a second call (another capture) keeps them."""
+        if self.capturable:
+            return
         self._dev = []
         for group in self.param_groups:
-            steps = [float(self.state[p]["step"]) for p in group["params"] if len(self.state[p])]
-            t = steps[0] if steps else 0.0
-            self._dev.append((torch.full((1,), float(group["lr"]), device=device, dtype=torch.float32),
-                              torch.full((1,), t, device=device, dtype=torch.float64),
-                              torch.zeros(3, device=device, dtype=torch.float32)))
+            ps = group["params"]
+            for p in ps:
+                st = self.state[p]
+                if len(st) == 0 and p.requires_grad:
+                    st["step"] = torch.tensor(0.0)
+                    st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                    st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
+            steps = [float(self.state[p]["step"]) if len(self.state[p]) else 0.0 for p in ps]
+            self._dev.append(dict(
+                lr=torch.full((1,), float(group["lr"]), device=device, dtype=torch.float32),
+                steps=torch.tensor(steps, device=device, dtype=torch.float64),
+                hyper=torch.zeros(2 * max(len(ps), 1), device=device, dtype=torch.float32),
+                index={id(p): i for i, p in enumerate(ps)}))
         self.capturable = True
 
-    def prepare_replay(self) -> None:
-        """Stream-ordered refresh of each group's device lr (LR schedulers change it on the host)."""
-        for group, (lr, _, _) in zip(self.param_groups, self._dev):
-            lr.fill_(float(group["lr"]))
-
-    def after_replay(self) -> None:
-        """Host-side step counters (state_dict) advance with every replayed update, and cached bf16
-        copies of the updated parameters are invalidated."""
-        for group in self.param_groups:
-            ps = []
+    def sync_steps(self) -> None:
+        """Copies the device step counters into the host state (state_dict, inspection)."""
+        if not self.capturable:
+            return
+        for group, d in zip(self.param_groups, self._dev):
+            host = d["steps"].cpu().tolist()
             for p in group["params"]:
                 st = self.state[p]
                 if len(st):
-                    st["step"] += 1
-                    ps.append(p)
+                    st["step"] = torch.tensor(float(host[d["index"][id(p)]]))
+
+    def state_dict(self):
+        self.sync_steps()
+        return super().state_dict()
+
+    def load_state_dict(self, state_dict) -> None:
+        """In the device form the loaded step counts go into the existing device counters; the
+        moment tensors are replaced, so steps captured before the load must be captured again."""
+        super().load_state_dict(state_dict)
+        if self.capturable:
+            for group, d in zip(self.param_groups, self._dev):
+                steps = [float(self.state[p]["step"]) if len(self.state[p]) else 0.0 for p in group["params"]]
+                d["steps"].copy_(torch.tensor(steps, dtype=torch.float64))
+
+    def prepare_replay(self) -> None:
+        """Stream-ordered refresh of each group's device lr (LR schedulers change it on the host)."""
+        for group, d in zip(self.param_groups, self._dev):
+            d["lr"].fill_(float(group["lr"]))
+
+    def after_replay(self) -> None:
+        """Cached 16-bit copies of the updated parameters are invalidated (the device step counters
+        advanced inside the replay; sync_steps() brings them to the host state)."""
+        for group in self.param_groups:
+            Fn.bump_param_epoch([p for p in group["params"] if len(self.state[p])])
+
+    def _gate_of(self, p, ld_gates):
+        if self.gates is not None and id(p) in self.gates:
+            return self.gates[id(p)].data_ptr()
+        f = ld_gates.get(id(p))
+        return f.data_ptr() if f is not None else 0
+
+    def _step_device(self, lib, stream):
+        capturing = Fn.capturing()
+        ld_gates = Fn.layerdrop_param_gates() if capturing else {}
+        for group, d in zip(self.param_groups, self._dev):
+            b1, b2 = group["betas"]
+            if not capturing:   # inside a capture prepare_replay() refreshes lr before every replay
+                d["lr"].fill_(float(group["lr"]))
+            recs, ps = [], []
+            base = d["steps"].data_ptr()
+            for p in group["params"]:
+                if p.grad is None:
+                    continue
+                self._check(p)
+                st = self.state[p]
+                if len(st) == 0:
+                    raise RuntimeError("HipAdam (device form): a parameter without optimizer state got a "
+                                       "gradient; call make_capturable() after adding parameters")
+                recs += [p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
+                         p.numel(), base + 8 * d["index"][id(p)], self._gate_of(p, ld_gates)]
+                ps.append(p)
+            if not ps:
+                continue
+            arr = (ctypes.c_int64 * len(recs))(*recs)
+            _lib.check(lib.b2p_adam_gated_recs(arr, len(ps), d["lr"].data_ptr(), float(b1), float(b2),
+                                               float(group["eps"]), float(group["weight_decay"]),
+                                               d["hyper"].data_ptr(), stream), "b2p_adam_gated_recs")
             Fn.bump_param_epoch(ps)
+
+    @staticmethod
+    def _check(p):
+        if p.grad.is_sparse:
+            raise RuntimeError("HipAdam does not support sparse gradients")
+        if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.is_contiguous()
+                and p.grad.dtype == torch.float32):
+            raise RuntimeError("HipAdam expects contiguous fp32 device parameters and gradients")
 
     @torch.no_grad()
     def step(self, closure=None):
@@ -61,6 +153,9 @@ class HipAdam(torch.optim.Optimizer):
         Fn.join_wgrad()    # deferred frozen-parameter gradient work is ordered before the update
         lib = _lib.load()
         stream = _lib.stream_ptr()
+        if self.capturable:
+            self._step_device(lib, stream)
+            return loss
         for group in self.param_groups:
             b1, b2 = group["betas"]
             # bucket by step count (identical for all params of a group in practice)
@@ -68,11 +163,7 @@ class HipAdam(torch.optim.Optimizer):
             for p in group["params"]:
                 if p.grad is None:
                     continue
-                if p.grad.is_sparse:
-                    raise RuntimeError("HipAdam does not support sparse gradients")
-                if not (p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() and p.grad.is_contiguous()
-                        and p.grad.dtype == torch.float32):
-                    raise RuntimeError("HipAdam expects contiguous fp32 device parameters and gradients")
+                self._check(p)
                 st = self.state[p]
                 if len(st) == 0:
                     st["step"] = torch.tensor(0.0)
@@ -82,25 +173,15 @@ class HipAdam(torch.optim.Optimizer):
                 buckets.setdefault(int(st["step"].item()), []).append(p)
             for step, ps in buckets.items():
                 recs = []
-                maxn = 0
                 for p in ps:
                     st = self.state[p]
                     recs += [p.data_ptr(), p.grad.data_ptr(), st["exp_avg"].data_ptr(), st["exp_avg_sq"].data_ptr(),
                              p.numel()]
-                    maxn = max(maxn, p.numel())
                 arr = (ctypes.c_int64 * len(recs))(*recs)
-                if self.capturable:
-                    if len(buckets) != 1:
-                        raise RuntimeError("HipAdam(capturable): a param group's tensors must share one step count")
-                    lr_d, step_d, hyp_d = self._dev[self.param_groups.index(group)]
-                    _lib.check(lib.b2p_adam_recs(arr, len(ps), 0.0, float(b1), float(b2), float(group["eps"]),
-                                                 float(group["weight_decay"]), 1.0, 1.0, lr_d.data_ptr(),
-                                                 step_d.data_ptr(), hyp_d.data_ptr(), stream), "b2p_adam_recs")
-                else:
-                    bc1 = 1.0 - b1 ** step
-                    bc2s = math.sqrt(1.0 - b2 ** step)
-                    _lib.check(lib.b2p_adam_recs(arr, len(ps), float(group["lr"]), float(b1), float(b2),
-                                                 float(group["eps"]), float(group["weight_decay"]), float(bc1),
-                                                 float(bc2s), None, None, None, stream), "b2p_adam_recs")
+                bc1 = 1.0 - b1 ** step
+                bc2s = math.sqrt(1.0 - b2 ** step)
+                _lib.check(lib.b2p_adam_recs(arr, len(ps), float(group["lr"]), float(b1), float(b2),
+                                             float(group["eps"]), float(group["weight_decay"]), float(bc1),
+                                             float(bc2s), None, None, None, stream), "b2p_adam_recs")
                 Fn.bump_param_epoch(ps)   # in-place writes invisible to torch: drop bf16 weight copies
         return loss

@@ -68,6 +68,15 @@ class GradBucketReducer:
                 off += p.numel()
             self.flat.append(flat)
         self.launch_log: list[int] = []     # bucket indices in the order their collectives were issued
+        # "used by some rank this step" per parameter (int32, MAX-reduced in finish()): the gates
+        # HipAdam's device form reads (opt.gates = reducer.gates), so a parameter no rank used —
+        # every rank's LayerDrop dropped its layer — is left untouched, as torch.optim.Adam leaves a
+        # grad=None parameter of the reference's single process
+        dev = self.params[0].device if self.params else torch.device("cpu")
+        self.used = torch.ones(max(len(self.params), 1), dtype=torch.int32, device=dev)
+        self.gates = {id(p): self.used[k] for k, p in enumerate(self.params)}
+        self._layer_gates = None   # graph-replayed steps: the device LayerDrop flags (make_layer_gates)
+        self._seen: set = set()
         self._reset()
         if self.world > 1:
             for p in self.params:
@@ -75,10 +84,52 @@ class GradBucketReducer:
         if grad_views:
             self.zero_grad()
 
+    def make_layer_gates(self, param_flags: dict):
+        """Graph-replayed steps (backward captured: no hook fires on a replay): the local "used" flag
+        of each parameter is its layer's device LayerDrop flag of the captured step
+        ({id(p): int32 flag}, functional.layerdrop_param_gates()); other parameters are always used.
+        Returns the state to pass to use_layer_gates() before each replay's finish()."""
+        flags, src = [], []
+        for p in self.params:
+            f = param_flags.get(id(p))
+            if f is None:
+                src.append(-1)
+            else:
+                for j, g in enumerate(flags):
+                    if g is f:
+                        src.append(j)
+                        break
+                else:
+                    flags.append(f)
+                    src.append(len(flags) - 1)
+        if not flags:
+            return None
+        one = torch.ones(1, dtype=torch.int32, device=self.used.device)
+        idx = torch.tensor([len(flags) if s < 0 else s for s in src], dtype=torch.int64, device=self.used.device)
+        return (flags + [one], idx)
+
+    def use_layer_gates(self, state) -> None:
+        """None: the local used flags come from the backward hooks (eager steps)."""
+        self._layer_gates = state
+
     def _reset(self):
         self.pending = [len(b) for b in self.buckets]
         self.next_launch = 0
         self.works = [None] * len(self.buckets)
+        self._seen = set()
+
+    def _exchange_used(self):
+        """Local used flags -> MAX over ranks into self.used (the optimizer's gates)."""
+        if not self.params:
+            return
+        if self._layer_gates is not None:
+            flags, idx = self._layer_gates
+            torch.index_select(torch.cat([f.reshape(1) for f in flags]), 0, idx, out=self.used)
+        else:
+            loc = torch.tensor([1 if id(p) in self._seen else 0 for p in self.params], dtype=torch.int32)
+            self.used.copy_(loc, non_blocking=False)
+        if self.world > 1:
+            dist.all_reduce(self.used, op=dist.ReduceOp.MAX, group=self.pg)
 
     def zero_grad(self) -> None:
         """Zeroes the buckets and binds every p.grad to its bucket slice (use instead of the
@@ -107,6 +158,7 @@ class GradBucketReducer:
             self.next_launch += 1
 
     def _hook(self, p):
+        self._seen.add(id(p))
         if not self.overlap:
             return
         bi = self.bucket_of.get(p)
@@ -123,6 +175,7 @@ class GradBucketReducer:
         while self.next_launch < len(self.buckets):
             self._launch(self.next_launch)
             self.next_launch += 1
+        self._exchange_used()
         for bi, w in enumerate(self.works):
             w.wait()
             if self.average and not self.avg_op:

@@ -119,9 +119,10 @@ class DefaultEvaluator(Evaluator):
         wer, _, nw, _, _ = Fn.ctc_greedy_wer(logits, sample.target, blank=blank, eos=eos, delim=delim)
         out = [torch.where(nw.sum() > 0, wer, torch.full_like(wer, nan))]
         if self.with_cer:
-            cer, _, nch = Fn.ctc_greedy_cer(logits, sample.target, vocab_of(self.tokenizer), blank=blank, eos=eos,
-                                            delim=delim)
+            cer, errs, nch = Fn.ctc_greedy_cer(logits, sample.target, vocab_of(self.tokenizer), blank=blank, eos=eos,
+                                               delim=delim)
             out.append(torch.where(nch.sum() > 0, cer, torch.full_like(cer, nan)))
+            out.append((errs < 0).sum())   # rows the device decode could not hold: scored on the host
         return out
 
     def _track_batch(self, predictions: ModelOutput, sample) -> float:
@@ -135,6 +136,9 @@ class DefaultEvaluator(Evaluator):
             extra["word_error_rate"] = vals[1]
             if self.with_cer:
                 extra["char_error_rate"] = vals[2]
+                if vals[3] > 0:   # a decoded string overflowed the device buffer: the host path
+                    pred, labels = self.decode_predictions(predictions, sample)
+                    extra["char_error_rate"] = char_error_rate([cut_after_eos_token(x) for x in pred], labels)
         else:
             loss = float(loss_t)
             pred, labels = self.decode_predictions(predictions, sample)

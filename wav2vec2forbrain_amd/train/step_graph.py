@@ -28,23 +28,26 @@ from .. import functional as Fn
 
 
 class StepGraph:
-    def __init__(self, step_fn, optimizer=None, warmup: int = 2, warm_replays: int = 2):
+    def __init__(self, step_fn, optimizer=None, warmup: int = 2, warm_replays: int = 2, epoch=None):
         """step_fn() runs one step on the current stream and returns the loss tensor (no host
         syncs inside: model.sync_metrics must be False). Pass the optimizer when step_fn includes
         its update (captured); without it the update runs eagerly after each replay (the data-
-        parallel step: replay, gradient all-reduce, update)."""
+        parallel step: replay, gradient all-reduce, update). epoch: a shared int64 device step
+        counter (several graphs of one training run, e.g. one per batch shape, draw from one
+        dropout-seed sequence); a new one by default."""
         self.step_fn = step_fn
         self.opt = optimizer
         self.warmup = warmup
         self.warm_replays = warm_replays
         self.graph = None
         self.loss = None
-        self.epoch = None
+        self.epoch = epoch
 
     def capture(self) -> None:
         dev = torch.device("cuda", torch.cuda.current_device())
         lib = _lib.load()
-        self.epoch = torch.zeros(1, dtype=torch.int64, device=dev)
+        if self.epoch is None:
+            self.epoch = torch.zeros(1, dtype=torch.int64, device=dev)
         _lib.check(lib.b2p_set_seed_epoch(ctypes.c_void_p(self.epoch.data_ptr())), "b2p_set_seed_epoch")
         if self.opt is not None:
             self.opt.make_capturable(dev)

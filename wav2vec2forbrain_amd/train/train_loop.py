@@ -4,6 +4,7 @@ torch.distributed is initialised: gradients of the optimised parameters are all-
 train.ddp.GradBucketReducer overlapped with backward."""
 from __future__ import annotations
 
+import dataclasses
 import os
 import uuid
 from typing import Literal, cast
@@ -37,6 +38,11 @@ class Trainer:
             skip = unused_param_names(self.model)
             params = [p for n, p in self.model.named_parameters() if id(p) in opt_ids and n not in skip]
             self.reducer = GradBucketReducer(params)
+            if hasattr(self.optimizer, "make_capturable"):
+                # device-form update gated per parameter by "some rank used it" (LayerDrop: a
+                # parameter no rank used keeps its value and moments, as with grad=None)
+                self.optimizer.make_capturable(params[0].device)
+                self.optimizer.gates = self.reducer.gates
             if self.config.gradient_clipping is not None:
                 # clip_grad_norm_ runs over model.parameters() (reference :72-75), frozen gradients
                 # included; averaging those too keeps every rank's clip coefficient equal to the
@@ -45,14 +51,133 @@ class Trainer:
                 self.frozen_reducer = GradBucketReducer(frozen, overlap=False, grad_views=False)
         # frozen parameters (not optimised): their gradient GEMMs run deferred beside the GRU backward
         Fn.set_deferred_wgrad(frozen)
+        # replayed steps (see train_step): a cache of captured steps keyed by the batch shape
+        self.use_graphs = (os.environ.get("B2P_TRAINER_GRAPH", "1") != "0" and torch.cuda.is_available()
+                           and hasattr(self.optimizer, "make_capturable"))
+        self.graph_cache_size = int(os.environ.get("B2P_TRAINER_GRAPHS", "4"))
+        self.capture_after = int(os.environ.get("B2P_TRAINER_CAPTURE_AFTER", "1"))
+        self._graphs: dict = {}
+        self._shape_seen: dict = {}
+        self._epoch_counter = None
+        self.graph_steps = 0
+        self.eager_steps = 0
 
     def _log_intermediate(self, batch: int, n_batches: int, evaluator):
         print(f"Batch {batch + 1}/{n_batches} loss: {evaluator.get_latest_loss():.2f} "
               f"running: {evaluator.get_running_loss():.2f}\r", end="")
 
+    # ------------------------------------------------------------------ replayed steps
+    @staticmethod
+    def _shape_key(batch):
+        t = batch.target
+        return (tuple(batch.input.shape), None if t is None else tuple(t.shape), str(batch.input.device))
+
+    def _graphable(self, batch) -> bool:
+        return (self.use_graphs and self.model.training and batch.input.is_cuda and batch.target is not None
+                and getattr(batch, "target_lens", None) is not None and not Fn.capturing())
+
+    def _capture(self, batch):
+        """Captures one whole step for this batch shape (train/step_graph.py) on static copies of the
+        batch tensors; the captured step reads them, train_step copies each new batch into them."""
+        from .step_graph import StepGraph
+        static = batch.copy_and_change(**{f: getattr(batch, f).clone() for f in batch._fields
+                                          if isinstance(getattr(batch, f), torch.Tensor)})
+        for a in ("day_idxs", "input_lens", "target_lens"):
+            v = getattr(batch, a, None)
+            if isinstance(v, torch.Tensor):
+                setattr(static, a, v.clone())
+        mods = [m for m in self.model.modules() if hasattr(m, "sync_metrics")]
+        olds = [m.sync_metrics for m in mods]
+        for m in mods:   # no host sync inside the captured step: the loss stays a device tensor
+            m.sync_metrics = False
+        box = {}
+        dp = self.reducer is not None
+
+        def step():
+            out = self._eager_body(static, in_graph=True)
+            box["out"] = out
+            return out.loss.detach().reshape(1)
+
+        if self._epoch_counter is None:
+            self._epoch_counter = torch.zeros(1, dtype=torch.int64, device=batch.input.device)
+        if dp:
+            self.reducer.overlap = False   # no collective inside the capture: exchanged after each replay
+        try:
+            sg = StepGraph(step, None if dp else self.optimizer, warmup=0, warm_replays=0,
+                           epoch=self._epoch_counter)
+            sg.capture()
+        finally:
+            if dp:
+                self.reducer.overlap = True
+                self.reducer._reset()
+            for m, o in zip(mods, olds):
+                m.sync_metrics = o
+        gates = self.reducer.make_layer_gates(Fn.layerdrop_param_gates()) if dp else None
+        return dict(graph=sg, batch=static, out=box["out"], gates=gates, sync=any(olds))
+
+    def _replay(self, g, batch):
+        st = g["batch"]
+        for f in batch._fields:
+            v = getattr(batch, f)
+            if isinstance(v, torch.Tensor):
+                getattr(st, f).copy_(v, non_blocking=True)
+        for a in ("day_idxs", "input_lens", "target_lens"):
+            v = getattr(batch, a, None)
+            if isinstance(v, torch.Tensor):
+                getattr(st, a).copy_(v, non_blocking=True)
+        g["graph"].replay()
+        if self.reducer is not None:
+            self.reducer.use_layer_gates(g["gates"])
+            self._dp_tail()
+        # the captured output's tensors are overwritten by the next replay
+        out = dataclasses.replace(g["out"], metrics=dict(g["out"].metrics))
+        if g["sync"] and "ctc_loss" in out.metrics:
+            # the reference reads ctc_loss.item() every step (w2v_custom_feat_extractor.py:94); the
+            # same transfer carries the multi-CU GRU status word (raises on a recurrence timeout)
+            out.metrics["ctc_loss"] = Fn.loss_item(out.loss)
+        return out
+
+    def _dp_tail(self):
+        """After a replayed forward + backward: bucket exchange, clip, update (eager)."""
+        self.reducer.finish()
+        if self.frozen_reducer is not None:
+            self.frozen_reducer.finish()
+        if self.config.gradient_clipping is not None:
+            torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.gradient_clipping)
+        self.optimizer.step()
+        self.reducer.use_layer_gates(None)
+
+    def release_graphs(self) -> None:
+        for g in self._graphs.values():
+            g["graph"].release()
+        self._graphs.clear()
+
     def train_step(self, batch: SampleBatch):
+        """One training step. The first `capture_after` steps of a batch shape run eagerly; then the
+        whole step is captured once as a HIP graph and replayed for every later batch of that shape
+        (at most graph_cache_size shapes; other shapes keep running eagerly). Replayed and eager steps
+        compute the same update (tests/test_trainer_gpu.py); the replay issues it with one host call
+        instead of ~650 Python-issued launches."""
+        if self._graphable(batch):
+            key = self._shape_key(batch)
+            g = self._graphs.get(key)
+            if g is None:
+                n = self._shape_seen.get(key, 0)
+                self._shape_seen[key] = n + 1
+                if n >= self.capture_after and len(self._graphs) < self.graph_cache_size:
+                    g = self._graphs[key] = self._capture(batch)
+            if g is not None:
+                self.graph_steps += 1
+                return self._replay(g, batch)
+        self.eager_steps += 1
+        if self.reducer is not None:
+            self.reducer.use_layer_gates(None)
+        return self._eager_body(batch)
+
+    def _eager_body(self, batch: SampleBatch, in_graph: bool = False):
         """One step of the reference loop body (:42-79): zero_grad, (no-op noise), forward,
-        backward, [DP all-reduce], optional clip, optimizer step."""
+        backward, [DP all-reduce], optional clip, optimizer step. in_graph (captured data-parallel
+        step): stops after the backward; the exchange and update run after each replay."""
         if self.reducer is not None:
             self.reducer.zero_grad()    # trainable gradients live in the all-reduce buckets
         else:
@@ -67,6 +192,8 @@ class Trainer:
         loss = cast(torch.Tensor, outputs.loss)
         loss.backward()
         Fn.join_wgrad()
+        if in_graph and self.reducer is not None:
+            return outputs
         if self.reducer is not None:
             self.reducer.finish()
         if self.frozen_reducer is not None:
@@ -76,8 +203,13 @@ class Trainer:
         self.optimizer.step()
         return outputs
 
-    def _train_epoch(self, data_loader):
+    def _train_epoch(self, data_loader, epoch: int = 0):
         self.model.train()
+        sampler = getattr(data_loader, "sampler", None)
+        if hasattr(sampler, "set_epoch"):
+            # DistributedSampler: a new permutation (and per-rank shard) every epoch, as the
+            # reference's single-process DataLoader(shuffle=True) reshuffles every epoch
+            sampler.set_epoch(epoch)
         evaluator = self.experiment.create_evaluator("train")
         for i, batch in enumerate(data_loader):
             batch = cast(SampleBatch, batch).cuda()
@@ -117,7 +249,7 @@ class Trainer:
         saved = False
         for epoch in range(self.config.epochs):
             print(f"\nEpoch {epoch + 1}/{self.config.epochs}")
-            train_losses = self._train_epoch(self.dataloader_train)
+            train_losses = self._train_epoch(self.dataloader_train, epoch)
             val_losses = self._evaluate_epoch("val")
             self.scheduler.step()
             print(f"\n\n{'=' * 20}\nFinished Epoch {epoch + 1}/{self.config.epochs} "
@@ -149,7 +281,7 @@ class Trainer:
             print("Loaded model with best validation loss of this experiment from disk")
         if getattr(self.config, "train_on_val_once", False):   # reference :211-213
             print("Training one epoch on val set")
-            self._train_epoch(self.dataloader_val)
+            self._train_epoch(self.dataloader_val, self.config.epochs)
         test_losses = self._evaluate_epoch("test")
         print(f"\nTest loss ({self.config.loss_function}): {test_losses.get_average().loss}")
         return self.model, TrainHistory(history, test_losses)
