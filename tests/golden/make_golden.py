@@ -176,7 +176,9 @@ def run(cfg, modules):
         res["logit_lens"] = out.logit_lens.numpy()
     for n, bt in model.named_buffers():
         if "running_" in n:
-            res["buf/" + n] = bt.numpy()
+            # a copy: numpy() shares the buffer's memory, and the Adam trajectory's forwards below
+            # update the running statistics in place
+            res["buf/" + n] = bt.detach().clone().numpy()
     if cfg.get("adam"):
         res.update(adam_trajectory(model, batch, cfg["adam"], out.loss.item()))
     path = os.path.join(OUT, f"{cfg['name']}.npz")

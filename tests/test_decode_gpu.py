@@ -117,9 +117,10 @@ def test_ctc_greedy_cer_matches_host_evaluator(tmp_path):
 
 @pytest.mark.gpu
 def test_cer_overflow_row_scored_on_host(tmp_path):
-    """A degenerate decode (early training: 600 alternating <unk> / blank frames = 1,500 characters
-    plus delimiters past the device buffer) is reported by the kernel as char_errs = -1, kept out of
-    the device CER, and the evaluator scores that batch on the host instead of silently lowering it."""
+    """A degenerate decode (early training: 512 alternating <unk> / blank frames over the kernel's
+    1024-frame maximum = 2,560 characters, past the 2,048-character device buffer) is reported by the
+    kernel as char_errs = -1, kept out of the device CER, and the evaluator scores that batch on the
+    host instead of silently lowering it."""
     from transformers import Wav2Vec2CTCTokenizer
     from wav2vec2forbrain_amd import functional as Fn
     from wav2vec2forbrain_amd.model.b2tmodel import ModelOutput
@@ -128,7 +129,7 @@ def test_cer_overflow_row_scored_on_host(tmp_path):
     f = tmp_path / "vocab.json"
     f.write_text(json.dumps({t: i for i, t in enumerate(VOCAB)}))
     tok = Wav2Vec2CTCTokenizer(str(f))
-    B, T, C, S = 2, 1400, 32, 40
+    B, T, C, S = 2, 1024, 32, 40
     ids = torch.zeros(B, T, dtype=torch.int64)
     ids[0, 0::2] = 3                                  # <unk> every other frame: > 2048 characters
     ids[1, :40] = torch.randint(5, C, (40,), generator=torch.Generator().manual_seed(3))

@@ -175,7 +175,7 @@ def test_captured_layerdrop_adam_leaves_dropped_layers(name):
                 torch.rand = forced.orig
             out.loss.backward()
             ropt.step()
-            losses_e.append(out.metrics["ctc_loss"])
+            losses_e.append(float(out.metrics["ctc_loss"]))
     torch.cuda.synchronize()
     np.testing.assert_allclose(losses, losses_e, rtol=1e-5, atol=0)
     used_layers = [sum(p[k] for p in patterns) for k in range(cfg["layers"])]

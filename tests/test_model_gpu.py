@@ -222,6 +222,7 @@ def test_step_graph_replay_matches_eager(adam_in_graph, train_w2v):
             else:
                 losses = [step() for _ in range(5)][2:]
         torch.cuda.synchronize()
+        opt.sync_steps()   # device-form step counters (captured Adam) -> host state
         res.append((torch.stack(losses).float().cpu(),
                     {n: p.detach().clone() for n, p in model.named_parameters()},
                     {n: p.grad.detach().clone() for n, p in model.named_parameters()

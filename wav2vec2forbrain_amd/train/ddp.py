@@ -102,8 +102,8 @@ class GradBucketReducer:
                 else:
                     flags.append(f)
                     src.append(len(flags) - 1)
-        if not flags:
-            return None
+        # no LayerDrop flag at all (deterministic mode / no dropped layers): every parameter is
+        # used — a replay fires no backward hook, so the hook-based flags would all read "unused"
         one = torch.ones(1, dtype=torch.int32, device=self.used.device)
         idx = torch.tensor([len(flags) if s < 0 else s for s in src], dtype=torch.int64, device=self.used.device)
         return (flags + [one], idx)
