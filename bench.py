@@ -211,6 +211,11 @@ def timed_run(kind, args, world, rank, device, use_graph):
     cfg = make_config(args.bs, args.seq, kind)
     model = build(cfg, device)
     model.train()
+    if world > 1 and hasattr(model, "sync_batchnorm"):
+        # the Conformer under DP: per-rank BatchNorm statistics (torch DDP's default semantics) so the
+        # step replays as a graph; SyncBN (the statistics all-reduce inside the forward) keeps a DP
+        # step eager (Trainer._sync_bn)
+        model.sync_batchnorm = False
     # the reference reads ctc_loss.item() inside forward (w2v_custom_feat_extractor.py:94): a host sync
     # per step. The bench keeps the loss on the device and reads every step's value into pinned host
     # memory (stream-ordered) instead, and reads them all after the timed region.

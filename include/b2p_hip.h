@@ -374,6 +374,13 @@ int b2p_gru_mc_debug_withhold(int member);
 int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
                    int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
                    b2p_stream_t stream);
+/* fp16-operand forward (the bf16 precision mode's attention operands: 11 significant bits for Q, K, V and
+ * the probabilities instead of bf16's 8; same rate): qkv16h and O16h hold fp16 bits, Ob16 (may be NULL)
+ * receives a bf16 copy of O for the out-projection's weight gradient. The backward reads a bf16 copy
+ * of qkv (b2p_attn16_bwd). */
+int b2p_attn16_fwd_f16(const void* qkv16h, void* O16h, void* Ob16, float* lse2, int64_t B, int64_t T,
+                       int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
+                       b2p_stream_t stream);
 int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws,
                    float* dqkv, void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh,
                    float scale, float drop_p, uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream);
@@ -418,8 +425,9 @@ int b2p_adam_recs(const int64_t* recs, int ntensors, float lr, double beta1, dou
  * reference's skipped encoder layers are such parameters. Records of 7 x int64 read from HOST memory
  * (32 per launch pair, capturable): {param, grad, exp_avg, exp_avg_sq, numel, step (double*, that
  * tensor's counter), gate (int32*: 0 = skip this tensor; NULL = always update)}. lr from lr_dev[0];
- * the bias corrections are formed per tensor in double from its own step. hyper_dev: float[2 *
- * ntensors] scratch. */
+ * the bias corrections are formed per tensor in double from its own step and rounded to float, as
+ * the host form (b2p_adam_recs) receives them, and the element update is the same code: both forms
+ * are bit-identical for equal inputs. hyper_dev: float[4 * ntensors] scratch (16-B aligned). */
 int b2p_adam_gated_recs(const int64_t* recs, int ntensors, const float* lr_dev, double beta1, double beta2,
                         float eps, float weight_decay, float* hyper_dev, b2p_stream_t stream);
 

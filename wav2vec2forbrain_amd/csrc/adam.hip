@@ -11,20 +11,11 @@ namespace {
 constexpr int NTH = 256;
 constexpr int PER_THREAD = 4;
 
-__global__ void __launch_bounds__(NTH) adam_k(const int64_t* __restrict__ table, float lr, float b1, float b2,
-                                              float eps, float wd, float bc1, float bc2s,
-                                              const float* __restrict__ hyper) {
-  if (hyper) {   // graph-replayable form: lr and the bias corrections live on the device
-    lr = hyper[0];
-    bc1 = hyper[1];
-    bc2s = hyper[2];
-  }
-  const int64_t* rec = table + 5 * (int64_t)blockIdx.y;
-  float* __restrict__ p = reinterpret_cast<float*>(rec[0]);
-  const float* __restrict__ g = reinterpret_cast<const float*>(rec[1]);
-  float* __restrict__ m = reinterpret_cast<float*>(rec[2]);
-  float* __restrict__ v = reinterpret_cast<float*>(rec[3]);
-  const int64_t n = rec[4];
+// the update of one tensor's elements (grid-strided over blockIdx.x); every form of the kernel runs
+// this same code, so host-form, device-form and gated updates are bit-identical for equal inputs
+__device__ __forceinline__ void adam_range(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ m,
+                                           float* __restrict__ v, int64_t n, float lr, float b1, float b2, float eps,
+                                           float wd, float bc1, float bc2s) {
   const float step = lr / bc1;
   const int64_t stride = (int64_t)gridDim.x * NTH;
   for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += stride) {
@@ -40,6 +31,19 @@ __global__ void __launch_bounds__(NTH) adam_k(const int64_t* __restrict__ table,
     const float denom = sqrtf(vi) / bc2s + eps;
     p[i] = pi - step * (mi / denom);
   }
+}
+
+__global__ void __launch_bounds__(NTH) adam_k(const int64_t* __restrict__ table, float lr, float b1, float b2,
+                                              float eps, float wd, float bc1, float bc2s,
+                                              const float* __restrict__ hyper) {
+  if (hyper) {   // graph-replayable form: lr and the bias corrections live on the device
+    lr = hyper[0];
+    bc1 = hyper[1];
+    bc2s = hyper[2];
+  }
+  const int64_t* rec = table + 5 * (int64_t)blockIdx.y;
+  adam_range(reinterpret_cast<float*>(rec[0]), reinterpret_cast<const float*>(rec[1]), reinterpret_cast<float*>(rec[2]),
+             reinterpret_cast<float*>(rec[3]), rec[4], lr, b1, b2, eps, wd, bc1, bc2s);
 }
 // one thread: the step counter of a parameter group and its bias corrections (double, as the host
 // computes them for torch.optim.Adam), for a step captured in a graph
@@ -68,26 +72,8 @@ __global__ void __launch_bounds__(NTH) adam_rec_k(const AdamRecs recs, float lr,
     bc2s = hyper[2];
   }
   const int64_t* rec = recs.r[blockIdx.y];
-  float* __restrict__ p = reinterpret_cast<float*>(rec[0]);
-  const float* __restrict__ g = reinterpret_cast<const float*>(rec[1]);
-  float* __restrict__ m = reinterpret_cast<float*>(rec[2]);
-  float* __restrict__ v = reinterpret_cast<float*>(rec[3]);
-  const int64_t n = rec[4];
-  const float step = lr / bc1;
-  const int64_t stride = (int64_t)gridDim.x * NTH;
-  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += stride) {
-    float gi = g[i];
-    const float pi = p[i];
-    if (wd != 0.f) gi += wd * pi;
-    float mi = m[i];
-    mi = mi + (1.f - b1) * (gi - mi);
-    float vi = v[i];
-    vi = b2 * vi + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    p[i] = pi - step * (mi / denom);
-  }
+  adam_range(reinterpret_cast<float*>(rec[0]), reinterpret_cast<const float*>(rec[1]), reinterpret_cast<float*>(rec[2]),
+             reinterpret_cast<float*>(rec[3]), rec[4], lr, b1, b2, eps, wd, bc1, bc2s);
 }
 
 // Per-tensor step counters and gates (the device form HipAdam uses for captured and DP steps).
@@ -99,48 +85,31 @@ constexpr int GADAM_MAXR = 32;
 struct GatedAdamRecs {
   int64_t r[GADAM_MAXR][7];   // param, grad, exp_avg, exp_avg_sq, numel, step (double*), gate (int32*)
 };
-// one thread per record: advance the step of an open tensor and form its bias corrections in double
-// (as the host does for torch.optim.Adam); a closed tensor gets the skip marker bc2s = 0
+// one thread per record: advance the step of an open tensor and form its bias corrections in double,
+// rounded to float as the host form passes them (bit-identical updates in both forms); hyper[i] =
+// {lr, bc1, sqrt(bc2), open}, open = 0 for a closed gate
 __global__ void adam_gate_steps_k(const GatedAdamRecs recs, int nrec, const float* __restrict__ lr_dev, double b1,
-                                  double b2, float2* __restrict__ hyper) {
+                                  double b2, float4* __restrict__ hyper) {
   const int i = threadIdx.x;
   if (i >= nrec) return;
   const int64_t* rec = recs.r[i];
   const int32_t* gate = reinterpret_cast<const int32_t*>(rec[6]);
   if (gate != nullptr && *gate == 0) {
-    hyper[i] = make_float2(0.f, 0.f);
+    hyper[i] = make_float4(0.f, 1.f, 1.f, 0.f);
     return;
   }
   double* st = reinterpret_cast<double*>(rec[5]);
   const double t = st[0] + 1.0;
   st[0] = t;
-  hyper[i] = make_float2((float)((double)lr_dev[0] / (1.0 - pow(b1, t))), (float)sqrt(1.0 - pow(b2, t)));
+  hyper[i] = make_float4(lr_dev[0], (float)(1.0 - pow(b1, t)), (float)sqrt(1.0 - pow(b2, t)), 1.f);
 }
 __global__ void __launch_bounds__(NTH) adam_gated_k(const GatedAdamRecs recs, float b1, float b2, float eps,
-                                                    float wd, const float2* __restrict__ hyper) {
-  const float2 h = hyper[blockIdx.y];
-  if (h.y == 0.f) return;   // gate closed: parameter, moments and step stay as they are
+                                                    float wd, const float4* __restrict__ hyper) {
+  const float4 h = hyper[blockIdx.y];
+  if (h.w == 0.f) return;   // gate closed: parameter, moments and step stay as they are
   const int64_t* rec = recs.r[blockIdx.y];
-  float* __restrict__ p = reinterpret_cast<float*>(rec[0]);
-  const float* __restrict__ g = reinterpret_cast<const float*>(rec[1]);
-  float* __restrict__ m = reinterpret_cast<float*>(rec[2]);
-  float* __restrict__ v = reinterpret_cast<float*>(rec[3]);
-  const int64_t n = rec[4];
-  const float step = h.x, bc2s = h.y;
-  const int64_t stride = (int64_t)gridDim.x * NTH;
-  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += stride) {
-    float gi = g[i];
-    const float pi = p[i];
-    if (wd != 0.f) gi += wd * pi;
-    float mi = m[i];
-    mi = mi + (1.f - b1) * (gi - mi);
-    float vi = v[i];
-    vi = b2 * vi + (1.f - b2) * gi * gi;
-    m[i] = mi;
-    v[i] = vi;
-    const float denom = sqrtf(vi) / bc2s + eps;
-    p[i] = pi - step * (mi / denom);
-  }
+  adam_range(reinterpret_cast<float*>(rec[0]), reinterpret_cast<const float*>(rec[1]), reinterpret_cast<float*>(rec[2]),
+             reinterpret_cast<float*>(rec[3]), rec[4], h.x, b1, b2, eps, wd, h.y, h.z);
 }
 
 // gradient accumulation dst[i] += src[i] over many small tensors in one launch (records by value:
@@ -214,13 +183,13 @@ extern "C" int b2p_adam_gated_recs(const int64_t* recs, int ntensors, const floa
                     "adam_gated_recs: NULL tensor in a record");
       maxn = a.r[i][4] > maxn ? a.r[i][4] : maxn;
     }
-    float2* hy = reinterpret_cast<float2*>(hyper_dev) + c0;
+    float4* hy = reinterpret_cast<float4*>(hyper_dev) + c0;
     hipLaunchKernelGGL(adam_gate_steps_k, dim3(1), dim3(64), 0, st, a, nc, lr_dev, beta1, beta2, hy);
     if (maxn <= 0) continue;
     int64_t bx = (maxn + (int64_t)NTH * PER_THREAD - 1) / ((int64_t)NTH * PER_THREAD);
     if (bx > 4096) bx = 4096;
     hipLaunchKernelGGL(adam_gated_k, dim3((unsigned)bx, (unsigned)nc), dim3(NTH), 0, st, a, b1f, b2f, eps,
-                       weight_decay, (const float2*)hy);
+                       weight_decay, (const float4*)hy);
   }
   B2P_CHECK_LAUNCH();
   return 0;

@@ -53,6 +53,26 @@ __device__ __forceinline__ bf16x8 pack_acc(const f32x4& a, const f32x4& b) {
 __device__ __forceinline__ f32x4 mfma(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+// H: the 16-bit containers hold fp16 bits (v_mfma_f32_16x16x32_f16), else bf16
+typedef _Float16 f16x8a __attribute__((ext_vector_type(8)));
+template <bool H>
+__device__ __forceinline__ f32x4 mfma_t(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  if constexpr (H)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8a, a), __builtin_bit_cast(f16x8a, b), c, 0,
+                                                  0, 0);
+  else
+    return mfma(a, b, c);
+}
+template <bool H>
+__device__ __forceinline__ bf16x8 pack_acc_t(const f32x4& a, const f32x4& b) {
+  if constexpr (H) {
+    f16x8a r = {(_Float16)a[0], (_Float16)a[1], (_Float16)a[2], (_Float16)a[3],
+                (_Float16)b[0], (_Float16)b[1], (_Float16)b[2], (_Float16)b[3]};
+    return __builtin_bit_cast(bf16x8, r);
+  } else {
+    return pack_acc(a, b);
+  }
+}
 __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // Load rows [0, 256) of a head slice (64 bf16 at column `col` of a row-major [B*T][ld] bf16
@@ -102,6 +122,9 @@ __device__ __forceinline__ float keep_scale(const DropCfg& dc, uint64_t idx) {
 
 // ------------------------------------------------------------------------------------------ forward
 // qkv16 [B*T][3*D] bf16 (q | k | v, head-major inside each); O16 [B*T][D] bf16; lse2 [B][nh][T]
+// H (b2p_attn16_fwd_f16): qkv16 and O16 hold fp16 and both products run on fp16 MFMA (P in fp16: 11
+// significant bits instead of 8); Ob16, when given, receives a bf16 copy of O (the backward's
+// weight-gradient operand)
 // One workgroup per (batch, head, 128-query half): 4 waves stage K and V once (64 KB of LDS) and then
 // each wave runs query tiles w and w + 4 of its half (16 queries each). K/V cross L2 -> LDS once per
 // 128 queries (half the traffic of 64-query blocks), and 2 x B x heads workgroups (768 at the base
@@ -119,10 +142,10 @@ __device__ __forceinline__ uint32_t keep4_bits(uint32_t key_lo, uint32_t k32, ui
          ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
 }
 
-template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward
+template <int DM, bool H>   // DM 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward
 __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
-                                                       float* __restrict__ lse2, int T, int nh, float scale,
-                                                       DropCfg dc, uint32_t* __restrict__ maskw) {
+                                                       uint16_t* __restrict__ Ob16, float* __restrict__ lse2, int T,
+                                                       int nh, float scale, DropCfg dc, uint32_t* __restrict__ maskw) {
   constexpr bool DROP = DM != 0;
   if (b2p_gated_off(dc.gate)) return;   // LayerDrop: this replay skips the layer (outputs unused)
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
@@ -168,7 +191,7 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     for (int kt = 0; kt < 16; ++kt) {
       s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) s[kt] = mfma(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], s[kt]);
+      for (int ks = 0; ks < 2; ++ks) s[kt] = mfma_t<H>(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], s[kt]);
     }
     float m = -INFINITY;
 #pragma unroll
@@ -220,15 +243,23 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
         word |= (uint32_t)__shfl_xor((int)word, 32, 64);
         if (qok && g == 0) maskw[(((int64_t)b * nh + h) * T + q) * 8 + c] = word;
       }
-      const bf16x8 bp = pack_acc(s[2 * c], s[2 * c + 1]);
+      const bf16x8 bp = pack_acc_t<H>(s[2 * c], s[2 * c + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        o[dt] = mfma(tr_frag(Vimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, o[dt]);
+        o[dt] = mfma_t<H>(tr_frag(Vimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, o[dt]);
     }
     const int64_t orow = (row0 + q) * D + h * DH;
     if (qok) {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) store_out(nullptr, O16, orow + dt * 16 + 4 * g, o[dt], 1.f);
+      for (int dt = 0; dt < 4; ++dt) {
+        const int64_t off = orow + dt * 16 + 4 * g;
+        if constexpr (H) {
+          *reinterpret_cast<uint2*>(O16 + off) = b2p_pack16x4(make_float4(o[dt][0], o[dt][1], o[dt][2], o[dt][3]), true);
+          if (Ob16) store_out(nullptr, Ob16, off, o[dt], 1.f);
+        } else {
+          store_out(nullptr, O16, off, o[dt], 1.f);
+        }
+      }
     }
     if (qok && g == 0) lse2[((int64_t)b * nh + h) * T + q] = m + __log2f(sum);
   }
@@ -480,9 +511,12 @@ int init_attrs() {
   static int done = -1;
   if (done >= 0) return done;
   int rc = 0;
-  rc |= set_lds(attn16_fwd_k<0>, FWD_LDS);
-  rc |= set_lds(attn16_fwd_k<1>, FWD_LDS);
-  rc |= set_lds(attn16_fwd_k<2>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<0, false>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<1, false>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<2, false>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<0, true>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<1, true>, FWD_LDS);
+  rc |= set_lds(attn16_fwd_k<2, true>, FWD_LDS);
   rc |= set_lds(attn16_bwd_dkv_k<0>, BWD_LDS);
   rc |= set_lds(attn16_bwd_dkv_k<1>, BWD_LDS);
   rc |= set_lds(attn16_bwd_dkv_k<2>, BWD_LDS);
@@ -494,9 +528,10 @@ int init_attrs() {
 }
 }  // namespace
 
-extern "C" int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
-                              int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
-                              b2p_stream_t stream) {
+namespace {
+int attn16_fwd_launch(bool half, const void* qkv16, void* O16, void* Ob16, float* lse2, int64_t B, int64_t T,
+                      int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
+                      b2p_stream_t stream) {
   B2P_CHECK_ARG(qkv16 && O16 && lse2, "attn16_fwd: NULL pointer");
   B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_fwd: needs head size 64 and T <= 256");
   if (B <= 0) return 0;
@@ -505,17 +540,38 @@ extern "C" int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t
                 "(32-bit dropout element index)");
   dim3 grid((unsigned)(B * nh * ((T + FWD_QB - 1) / FWD_QB)));
   const DropCfg dc = drop_cfg(drop_p, drop_seed);
-  if (drop_p > 0.f && mask)
-    hipLaunchKernelGGL(attn16_fwd_k<2>, grid, dim3(FWD_NT), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
-                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, mask);
-  else if (drop_p > 0.f)
-    hipLaunchKernelGGL(attn16_fwd_k<1>, grid, dim3(FWD_NT), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
-                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, (uint32_t*)nullptr);
-  else
-    hipLaunchKernelGGL(attn16_fwd_k<0>, grid, dim3(FWD_NT), FWD_LDS, (hipStream_t)stream, (const uint16_t*)qkv16,
-                       (uint16_t*)O16, lse2, (int)T, (int)nh, scale, dc, (uint32_t*)nullptr);
+  const int dm = drop_p > 0.f ? (mask ? 2 : 1) : 0;
+  auto run = [&](auto dmc, auto hc) {
+    hipLaunchKernelGGL((attn16_fwd_k<decltype(dmc)::value, decltype(hc)::value>), grid, dim3(FWD_NT), FWD_LDS,
+                       (hipStream_t)stream, (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T,
+                       (int)nh, scale, dc, dm == 2 ? mask : (uint32_t*)nullptr);
+  };
+  using F = std::false_type;
+  using Tr = std::true_type;
+  if (half) {
+    if (dm == 2) run(std::integral_constant<int, 2>(), Tr());
+    else if (dm == 1) run(std::integral_constant<int, 1>(), Tr());
+    else run(std::integral_constant<int, 0>(), Tr());
+  } else {
+    if (dm == 2) run(std::integral_constant<int, 2>(), F());
+    else if (dm == 1) run(std::integral_constant<int, 1>(), F());
+    else run(std::integral_constant<int, 0>(), F());
+  }
   B2P_CHECK_LAUNCH();
   return 0;
+}
+}  // namespace
+
+extern "C" int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
+                              int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
+                              b2p_stream_t stream) {
+  return attn16_fwd_launch(false, qkv16, O16, nullptr, lse2, B, T, nh, dh, scale, drop_p, drop_seed, mask, stream);
+}
+
+extern "C" int b2p_attn16_fwd_f16(const void* qkv16h, void* O16h, void* Ob16, float* lse2, int64_t B, int64_t T,
+                                  int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed,
+                                  uint32_t* mask, b2p_stream_t stream) {
+  return attn16_fwd_launch(true, qkv16h, O16h, Ob16, lse2, B, T, nh, dh, scale, drop_p, drop_seed, mask, stream);
 }
 
 extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws, float* dqkv,

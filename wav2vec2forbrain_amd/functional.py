@@ -1499,6 +1499,27 @@ def _attn16_fwd(qkv16, B, T, nh, dh, p_attn, seed, want_mask=False):
     return (O16, lse2, mask) if want_mask else (O16, lse2)
 
 
+# bf16 precision mode: the fused attention's forward operands (Q, K, V, the probabilities, O) in fp16
+# (csrc/attn16.hip b2p_attn16_fwd_f16). bf16's 8-bit mantissa on the scores / probabilities biased the
+# 24-layer models' CTC loss by ~1e-3 relative (tools/fixture_err.py: with the attention alone in exact
+# fp32 the Conformer-large error fell from 1.0e-3 to 8e-5). The QKV projection writes the fp16 operand
+# and a bf16 copy for the backward kernels; B2P_ATTN_F16=0 keeps the bf16 forward (A/B).
+ATTN_F16 = os.environ.get("B2P_ATTN_F16", "1") != "0"
+
+
+def _attn16_fwd_f16(qkvh, B, T, nh, dh, p_attn, seed):
+    """qkvh (B*T, 3D) fp16 -> Oh (B*T, D) fp16 (the out-projection's operand), Ob (B*T, D) bf16 (its
+    weight-gradient operand), lse2 (B, nh, T) f32, the dropout keep bits (None without dropout)."""
+    dev = qkvh.device
+    Oh = torch.empty(B * T, nh * dh, device=dev, dtype=torch.float16)
+    Ob = torch.empty(B * T, nh * dh, device=dev, dtype=BF16)
+    lse2 = torch.empty(B, nh, T, device=dev)
+    mask = torch.empty(B, nh, T, 8, device=dev, dtype=torch.int32) if p_attn > 0 else None
+    _lib.call("b2p_attn16_fwd_f16", _p(qkvh), _p(Oh), _p(Ob), _p(lse2), B, T, nh, dh, float(dh ** -0.5),
+              float(p_attn), seed, None if mask is None else mask.data_ptr(), _st())
+    return Oh, Ob, lse2, mask
+
+
 def _attn16_bwd(qkv16, dO16, lse2, B, T, nh, dh, p_attn, seed, want32=True, mask=None):
     """-> dqkv (B*T, 3D) f32 (or None) and its bf16 copy (mask: the forward's keep bits, or None to
     re-hash)."""
@@ -1633,21 +1654,30 @@ class _EncoderLayer16(torch.autograd.Function):
         wqkv16 = weight16(wq, wk, wv)
         bqkv = bias_cat(bq, bk, bv) if any(b is not None for b in (bq, bk, bv)) else None
         fused = attn16_ok(T, dh)
+        Oh = None
         if fused:
             qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16)     # bf16 only: attention operand
-            gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), None, 3 * D, bias=bqkv, C16=qkv)
-            # P slot: lse2, Pd slot: the dropout keep bits for the backward
-            O16, P, Pd = _attn16_fwd(qkv, B, T, nh, dh, p_attn, seeds[0], want_mask=True)
+            if ATTN_F16:   # fp16 forward operand + the backward's bf16 copy from one epilogue
+                qkvh = torch.empty(NT, 3 * D, device=dev, dtype=torch.float16)
+                gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), None, 3 * D, bias=bqkv, C16=qkvh,
+                     c16_fp16=True, pre16=qkv)
+                Oh, O16, P, Pd = _attn16_fwd_f16(qkvh, B, T, nh, dh, p_attn, seeds[0])
+                del qkvh
+            else:
+                gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), None, 3 * D, bias=bqkv, C16=qkv)
+                # P slot: lse2, Pd slot: the dropout keep bits for the backward
+                O16, P, Pd = _attn16_fwd(qkv, B, T, nh, dh, p_attn, seeds[0], want_mask=True)
         else:
             qkv = torch.empty(NT, 3 * D, device=dev)
             gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), qkv, 3 * D, bias=bqkv)
             P, Pd, _O, O16 = _attn_core_fwd(qkv, B, T, nh, dh, p_attn, seeds[0], want16=True)
             del _O
-        # y1 = x + dropout(O Wo^T + bo)
-        wo16 = weight16(wo)
+        # y1 = x + dropout(O Wo^T + bo)   (fp16 O: the fp16 weight copy)
+        wo16, wo_op = _w_op16(wo, Oh is not None)
         y1 = torch.empty(NT, D, device=dev)
-        gemm(NT, D, D, op(O16, 0, D, True), op(wo16, 0, D, True), y1, D, bias=bo, drop_p=p_hid, seed=seeds[1],
-             residual=x2)
+        gemm(NT, D, D, op(O16 if Oh is None else Oh, 0, D, True), wo_op, y1, D, bias=bo, drop_p=p_hid,
+             seed=seeds[1], residual=x2)
+        del Oh, wo16
         x1, x1_16, m1, r1 = _ln_fwd16(y1, g1, be1, eps)
         # FFN: f = dropout(gelu(x1 W1^T + b1)) (bf16 only: it is a GEMM operand and nothing else)
         w1_16, w2_16 = weight16(w1), weight16(w2)
@@ -2152,6 +2182,8 @@ class _ConformerAttnBlock(torch.autograd.Function):
         # keep bits / O16
         ctx.fused = bf16_mode() and attn16_ok(T, hd)
         qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16 if ctx.fused else torch.float32)
+        # fused, ATTN_F16: the projections write the fp16 attention operand and the backward's bf16 copy
+        qkvh = torch.empty(NT, 3 * D, device=dev, dtype=torch.float16) if (ctx.fused and ATTN_F16) else None
         if bf16_mode():
             # the Q/K/V operands come straight from their producers as 16-bit copies (LayerNorm, rotary):
             # fp16 under forward_f16, else bf16; the fp32 rotated copy is never stored
@@ -2165,7 +2197,10 @@ class _ConformerAttnBlock(torch.autograd.Function):
             hr = None
             for i, (w, bb, src) in enumerate(((wq, bq, hr16), (wk, bk, hr16), (wv, bv, h16))):
                 wbuf, wop = _w_op16(w, half)
-                if ctx.fused:
+                if qkvh is not None:
+                    gemm(NT, D, D, op(src, 0, D, True), wop, None, 3 * D, c_off=i * D, bias=bb, C16=qkvh,
+                         c16_fp16=True, pre16=qkv)
+                elif ctx.fused:
                     gemm(NT, D, D, op(src, 0, D, True), wop, None, 3 * D, c_off=i * D, bias=bb, C16=qkv)
                 else:
                     gemm(NT, D, D, op(src, 0, D, True), wop, qkv, 3 * D, c_off=i * D, bias=bb)
@@ -2182,7 +2217,13 @@ class _ConformerAttnBlock(torch.autograd.Function):
             for i, (w, bb, src) in enumerate(((wq, bq, hr), (wk, bk, hr), (wv, bv, h))):
                 gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=bb)
         y = torch.empty(NT, D, device=dev)
-        if ctx.fused:
+        if qkvh is not None:
+            Oh, O, P, Pd = _attn16_fwd_f16(qkvh, B, T, nh, hd, p_attn, seeds[0])
+            del qkvh
+            wbuf, wop = _w_op16(wo, True)
+            gemm(NT, D, D, op(Oh, 0, D, True), wop, y, D, bias=bo, drop_p=p_out, seed=seeds[1], residual=x2)
+            del Oh, wbuf
+        elif ctx.fused:
             O, P, Pd = _attn16_fwd(qkv, B, T, nh, hd, p_attn, seeds[0], want_mask=True)
             gemm(NT, D, D, op(O, 0, D, True), op(weight16(wo), 0, D, True), y, D, bias=bo, drop_p=p_out,
                  seed=seeds[1], residual=x2)

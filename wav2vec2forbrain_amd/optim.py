@@ -34,7 +34,7 @@ class HipAdam(torch.optim.Optimizer):
         super().__init__(params, dict(lr=lr, betas=betas, eps=eps, weight_decay=weight_decay))
         self.capturable = False
         # device form, per param group: lr float32[1], per-parameter step counters float64[n],
-        # hyper scratch float32[2n], {id(p): index}
+        # hyper scratch float32[4n], {id(p): index}
         self._dev = []
         # optional {id(p): int32 device tensor}: the caller's per-parameter gates (data-parallel
         # steps: 0 = no rank used the parameter this step); device form only
@@ -63,7 +63,7 @@ class HipAdam(torch.optim.Optimizer):
             self._dev.append(dict(
                 lr=torch.full((1,), float(group["lr"]), device=device, dtype=torch.float32),
                 steps=torch.tensor(steps, device=device, dtype=torch.float64),
-                hyper=torch.zeros(2 * max(len(ps), 1), device=device, dtype=torch.float32),
+                hyper=torch.zeros(4 * max(len(ps), 1), device=device, dtype=torch.float32),
                 index={id(p): i for i, p in enumerate(ps)}))
         self.capturable = True
 
@@ -80,7 +80,12 @@ class HipAdam(torch.optim.Optimizer):
 
     def state_dict(self):
         self.sync_steps()
-        return super().state_dict()
+        sd = super().state_dict()
+        if self.capturable:
+            # the device form creates state for every trainable parameter up front; torch.optim.Adam
+            # has none for a parameter that never received a gradient (unused inpLayer* etc.)
+            sd["state"] = {k: v for k, v in sd["state"].items() if float(v["step"]) > 0}
+        return sd
 
     def load_state_dict(self, state_dict) -> None:
         """In the device form the loaded step counts go into the existing device counters; the

@@ -20,6 +20,16 @@ from .ddp import GradBucketReducer, unused_param_names
 from .history import EpochLosses, SingleEpochHistory, TrainHistory
 
 
+def _detached(out):
+    """The step's ModelOutput with its tensors detached. After backward the caller only reads values
+    (evaluator: loss, logits); a returned output that still referenced the autograd graph would keep
+    the parameters' AccumulateGrad nodes alive, bound to the stream they were created on, and the next
+    step's capture on the capture stream would then accumulate through them (an illegal cross-stream
+    dependency inside the capture: the HIP runtime crashed in hipStreamEndCapture)."""
+    return dataclasses.replace(out, **{f.name: getattr(out, f.name).detach() for f in dataclasses.fields(out)
+                                       if isinstance(getattr(out, f.name), torch.Tensor)})
+
+
 class Trainer:
     def __init__(self, experiment):
         self.experiment = experiment
@@ -72,9 +82,16 @@ class Trainer:
         t = batch.target
         return (tuple(batch.input.shape), None if t is None else tuple(t.shape), str(batch.input.device))
 
+    def _sync_bn(self) -> bool:
+        """Data-parallel with synchronised BatchNorm statistics (the Conformer's sync_batchnorm): the
+        statistics all-reduce runs inside the forward, which a captured step cannot hold (no collective
+        is captured), so such steps stay eager. With sync_batchnorm off each rank normalises over its
+        own micro-batch (torch DDP's default semantics) in eager and replayed steps alike."""
+        return self.reducer is not None and any(getattr(m, "sync_batchnorm", False) for m in self.model.modules())
+
     def _graphable(self, batch) -> bool:
         return (self.use_graphs and self.model.training and batch.input.is_cuda and batch.target is not None
-                and getattr(batch, "target_lens", None) is not None and not Fn.capturing())
+                and getattr(batch, "target_lens", None) is not None and not Fn.capturing() and not self._sync_bn())
 
     def _capture(self, batch):
         """Captures one whole step for this batch shape (train/step_graph.py) on static copies of the
@@ -193,7 +210,7 @@ class Trainer:
         loss.backward()
         Fn.join_wgrad()
         if in_graph and self.reducer is not None:
-            return outputs
+            return _detached(outputs)
         if self.reducer is not None:
             self.reducer.finish()
         if self.frozen_reducer is not None:
@@ -201,7 +218,7 @@ class Trainer:
         if self.config.gradient_clipping is not None:
             torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.gradient_clipping)
         self.optimizer.step()
-        return outputs
+        return _detached(outputs)
 
     def _train_epoch(self, data_loader, epoch: int = 0):
         self.model.train()
