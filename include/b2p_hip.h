@@ -376,14 +376,21 @@ int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t
                    b2p_stream_t stream);
 /* fp16-operand forward (the bf16 precision mode's attention operands: 11 significant bits for Q, K, V and
  * the probabilities instead of bf16's 8; same rate): qkv16h and O16h hold fp16 bits, Ob16 (may be NULL)
- * receives a bf16 copy of O for the out-projection's weight gradient. The backward reads a bf16 copy
- * of qkv (b2p_attn16_bwd). */
+ * receives a bf16 copy of O for the out-projection's weight gradient. The backward of such a forward is
+ * b2p_attn16_bwd_f16. */
 int b2p_attn16_fwd_f16(const void* qkv16h, void* O16h, void* Ob16, float* lse2, int64_t B, int64_t T,
                        int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
                        b2p_stream_t stream);
 int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws,
                    float* dqkv, void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh,
                    float scale, float drop_p, uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream);
+/* backward of b2p_attn16_fwd_f16: qkv16h fp16. The scores are recomputed on fp16 MFMA from the same
+ * operands as the forward (consistent with its lse2, so saturated softmax rows give ~0 dS as in fp32);
+ * the products with the bf16 gradients (dP = dO V^T, dQ = dS K, dK = dS^T Q) take bf16 conversions of
+ * V, K, Q made in registers / while staging LDS. Same outputs and workspace as b2p_attn16_bwd. */
+int b2p_attn16_bwd_f16(const void* qkv16h, const void* dO16, const float* lse2, float* delta_ws,
+                       float* dqkv, void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh,
+                       float scale, float drop_p, uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream);
 
 /* ------------------------------------------------------------------ CTC
  * log_softmax + nn.CTCLoss(blank=0, reduction="mean", zero_infinity=True)

@@ -206,14 +206,16 @@ def _keep_mask_ref(seed, p, B, nh, T):
 
 @pytest.mark.parametrize("B,T,nh,p", [(2, 249, 12, 0.0), (2, 249, 12, 0.1), (3, 100, 4, 0.1), (1, 17, 2, 0.0),
                                        (2, 256, 3, 0.1)])
-@pytest.mark.parametrize("variant", ["hash", "mask", "epoch"])
+@pytest.mark.parametrize("variant", ["hash", "mask", "epoch", "f16"])
 def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
     """csrc/attn16.hip (bf16 MFMA, scores on-chip) vs the unfused fp32 attention core (GEMM ->
     softmax/dropout kernel -> GEMM) on the same bf16-rounded q/k/v and the SAME dropout mask
     (both hash ((b*nh+h)*T+q)*T+key). Tolerance: relative L2 1e-2 on O, 2e-2 on dQ/dK/dV.
     variant: hash = backward re-hashes the mask; mask = backward reads the forward's keep bits
     (must equal the re-hashed result bit for bit); epoch = both paths under a graph-replay seed
-    counter (the fused forward, fused backward and unfused kernels must offset the seed alike)."""
+    counter (the fused forward, fused backward and unfused kernels must offset the seed alike);
+    f16 = the bf16 precision mode's default: fp16 forward operands (b2p_attn16_fwd_f16, O in fp16 plus
+    its bf16 copy) and the backward recomputing the scores from them (b2p_attn16_bwd_f16)."""
     import ctypes
     Fn = _fn()
     torch.manual_seed(7)
@@ -230,10 +232,15 @@ def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
         with Fn.precision("fp32"):
             P, Pd, O = Fn._attn_core_fwd(qkv, B, T, nh, dh, p, seed)
             dref = Fn._attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p, seed)
-        q16 = qkv.to(torch.bfloat16)
-        O16, lse2, mask = Fn._attn16_fwd(q16, B, T, nh, dh, p, seed, want_mask=True)
+        if variant == "f16":
+            q16 = qkv.to(torch.float16)
+            Oh, O16, lse2, mask = Fn._attn16_fwd_f16(q16, B, T, nh, dh, p, seed)
+            assert float((Oh.float() - O16.float()).norm()) <= 1e-2 * float(Oh.float().norm())
+        else:
+            q16 = qkv.to(torch.bfloat16)
+            O16, lse2, mask = Fn._attn16_fwd(q16, B, T, nh, dh, p, seed, want_mask=True)
         dq32, dq16 = Fn._attn16_bwd(q16, dO.to(torch.bfloat16), lse2, B, T, nh, dh, p, seed,
-                                    mask=mask if variant == "mask" else None)
+                                    mask=mask if variant in ("mask", "f16") else None)
         if variant == "mask" and p > 0:
             h32, _ = Fn._attn16_bwd(q16, dO.to(torch.bfloat16), lse2, B, T, nh, dh, p, seed)
             # the keep bits the forward stored are the hash mask, bit for bit (integer check against

@@ -107,6 +107,8 @@ _SIGS = {
     "b2p_attn16_fwd_f16": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p, c_p]),
     "b2p_attn16_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p,
                                c_p]),
+    "b2p_attn16_bwd_f16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p,
+                               c_p]),
     "b2p_ctc_workspace": (c_i64, [c_i64, c_i64, c_i64, c_i64]),
     "b2p_ctc_fwd_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_p, c_p, c_p, c_p]),
     "b2p_adam_multi": (c_i32, [c_p, c_i32, c_i64, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_f32, c_p]),

@@ -89,6 +89,31 @@ __device__ __forceinline__ void load_image(char* img, const uint16_t* base, int6
   }
 }
 __device__ __forceinline__ bf16x8 gload8(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+// 8 fp16 values (bits in a bf16x8 container) -> bf16 (the backward's products with bf16 gradients)
+__device__ __forceinline__ bf16x8 h2b8(const bf16x8& x) {
+  const f16x8a h = __builtin_bit_cast(f16x8a, x);
+  bf16x8 r = {(__bf16)(float)h[0], (__bf16)(float)h[1], (__bf16)(float)h[2], (__bf16)(float)h[3],
+              (__bf16)(float)h[4], (__bf16)(float)h[5], (__bf16)(float)h[6], (__bf16)(float)h[7]};
+  return r;
+}
+template <bool H>
+__device__ __forceinline__ bf16x8 to_b16(const bf16x8& x) {
+  if constexpr (H) return h2b8(x);
+  else return x;
+}
+// load_image with each 16-B chunk converted fp16 -> bf16 on the way (H), else a plain copy
+template <bool H>
+__device__ __forceinline__ void load_image_b16(char* img, const uint16_t* base, int64_t row0, int T, int64_t ld,
+                                               int col, int tid) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const int idx = tid + 256 * k;
+    const int r = idx >> 3, c = idx & 7;
+    bf16x8 v = bf16x8{};
+    if (r < T) v = to_b16<H>(gload8(base + (row0 + r) * ld + col + 8 * c));
+    *reinterpret_cast<bf16x8*>(img + r * 128 + (((c ^ r) & 7) << 4)) = v;
+  }
+}
 __device__ __forceinline__ void store_out(float* o32, uint16_t* o16, int64_t off, const f32x4& v, float s) {
   const float4 f = make_float4(v[0] * s, v[1] * s, v[2] * s, v[3] * s);
   if (o32) *reinterpret_cast<float4*>(o32 + off) = f;
@@ -193,30 +218,39 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) s[kt] = mfma_t<H>(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], s[kt]);
     }
+    // row max of the raw scores (scale > 0 commutes with max); keys >= T are masked only in the tiles
+    // that hold them (wave-uniform test), the scale is folded into the exponent's FMA
     float m = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 16; ++kt)
+    for (int kt = 0; kt < 16; ++kt) {
+      if (kt * 16 + 16 <= T) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int key = kt * 16 + 4 * g + i;
-        const float v = key < T ? s[kt][i] * c2 : -INFINITY;
-        s[kt][i] = v;
-        m = fmaxf(m, v);
+        for (int i = 0; i < 4; ++i) m = fmaxf(m, s[kt][i]);
+      } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float v = kt * 16 + 4 * g + i < T ? s[kt][i] : -INFINITY;
+          s[kt][i] = v;
+          m = fmaxf(m, v);
+        }
       }
+    }
     m = fmaxf(m, __shfl_xor(m, 16, 64));
     m = fmaxf(m, __shfl_xor(m, 32, 64));
+    const float mc = m * c2;
     float sum = 0.f;
 #pragma unroll
     for (int kt = 0; kt < 16; ++kt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float e = exp2_fast(s[kt][i] - m);
+        const float e = exp2_fast(fmaf(s[kt][i], c2, -mc));
         s[kt][i] = e;
         sum += e;
       }
     sum += __shfl_xor(sum, 16, 64);
     sum += __shfl_xor(sum, 32, 64);
     const float inv = 1.f / sum;
+    const float inv_s = DROP ? inv * dc.scale : inv;   // keys >= T already hold exp2(-inf) = 0
     const uint32_t rowlo = (uint32_t)((((uint32_t)b * (uint32_t)nh + (uint32_t)h) * (uint32_t)T + (uint32_t)(qok ? q : 0)) *
                                       (uint32_t)TP);
     // O^T (d x q) = V^T (d x keys) . P_d^T (keys x q), 32 keys per k-step
@@ -233,8 +267,8 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
         if (DROP) word |= kb << (half * 16 + 4 * g);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
-          const float ks = (key0 + i < T && ((kb >> i) & 1u)) ? (DROP ? dc.scale : 1.f) : 0.f;
-          s[2 * c + half][i] *= inv * ks;
+          const float pv = s[2 * c + half][i] * inv_s;
+          s[2 * c + half][i] = (DROP && !((kb >> i) & 1u)) ? 0.f : pv;
         }
       }
       if (DM == 2) {
@@ -261,7 +295,7 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
         }
       }
     }
-    if (qok && g == 0) lse2[((int64_t)b * nh + h) * T + q] = m + __log2f(sum);
+    if (qok && g == 0) lse2[((int64_t)b * nh + h) * T + q] = mc + __log2f(sum);
   }
 }
 
@@ -270,7 +304,7 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
 // bf16) columns [D + h*64, ...) and [2D + h*64, ...). One workgroup per (batch, head, 128 keys): Q and
 // dO are staged once for 128 keys (4 waves x key tiles w and w + 4).
 constexpr int BWD_KB = 128;
-template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: keep bits in memory
+template <int DM, bool H>   // DM 0: no dropout, 1: hash the keep mask, 2: keep bits in memory; H: fp16 qkv
 __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restrict__ qkv, const float* __restrict__ delta,
                                                         const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                         float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
@@ -328,7 +362,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
       kf[ks] = vf[ks] = bf16x8{};
       if (kok) {
         kf[ks] = gload8(qkv + (row0 + key) * ld + D + h * DH + 32 * ks + 8 * g);
-        vf[ks] = gload8(qkv + (row0 + key) * ld + 2 * D + h * DH + 32 * ks + 8 * g);
+        vf[ks] = to_b16<H>(gload8(qkv + (row0 + key) * ld + 2 * D + h * DH + 32 * ks + 8 * g));
       }
     }
     f32x4 dv[4], dk[4];
@@ -350,7 +384,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
         f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          sv = mfma(row_frag(Qimg, qt * 16 + lr, 32 * ks + 8 * g), kf[ks], sv);
+          sv = mfma_t<H>(row_frag(Qimg, qt * 16 + lr, 32 * ks + 8 * g), kf[ks], sv);
           dp = mfma(row_frag(dOimg, qt * 16 + lr, 32 * ks + 8 * g), vf[ks], dp);
         }
         // rows q = qt*16 + 4g + i, column key
@@ -358,7 +392,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
         for (int i = 0; i < 4; ++i) {
           const int qq = qt * 16 + 4 * g + i;
           const bool ok = kok && qq < T;
-          const float p = ok ? exp2_fast(sv[i] * c2 - lse_s[qq]) : 0.f;
+          const float p = ok ? exp2_fast(fmaf(sv[i], c2, -lse_s[qq])) : 0.f;
           const float ksc = !ok ? 0.f
                             : (DM == 2) ? (((mw[half][i] >> (key & 31)) & 1u) ? dc.scale : 0.f)
                                               : keep_scale<DROP>(dc, (bh * T + qq) * (uint64_t)TP + key);
@@ -370,7 +404,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         dv[dt] = mfma(tr_frag(dOimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, dv[dt]);
-        dk[dt] = mfma(tr_frag(Qimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dk[dt]);
+        dk[dt] = mfma(to_b16<H>(tr_frag(Qimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr)), bs, dk[dt]);
       }
     }
     if (kok) {
@@ -390,7 +424,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
 // rounding — otherwise the residual feeds a systematic, Q-correlated error into dK. Pass 1 keeps
 // P and dP*keep in registers, pass 2 forms dS and dQ^T += K^T dS^T. One workgroup per (batch, head,
 // 128 queries): K and V staged once, 4 waves x query tiles w and w + 4.
-template <int DM>   // 0: no dropout, 1: hash the keep mask, 2: keep bits in memory
+template <int DM, bool H>   // DM 0: no dropout, 1: hash the keep mask, 2: keep bits in memory; H: fp16 qkv
 __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restrict__ qkv, float* __restrict__ delta,
                                                        const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                        float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
@@ -410,8 +444,8 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
     for (int half = 0; half < 2; ++half) zero_block(dqkv, dqkv16, row0, qh * FWD_QB + 64 * half, T, ld, h * DH, tid);
     return;
   }
-  load_image(smem, qkv, row0, T, ld, D + h * DH, tid);
-  load_image(smem + TMAX * 128, qkv, row0, T, ld, 2 * D + h * DH, tid);
+  load_image(smem, qkv, row0, T, ld, D + h * DH, tid);                        // K (as stored: S = Q K^T)
+  load_image_b16<H>(smem + TMAX * 128, qkv, row0, T, ld, 2 * D + h * DH, tid);  // V in bf16 (dP = dO V^T)
   __syncthreads();
   const float c2 = scale * LOG2E;
   const int TP = T + (T & 1);
@@ -448,14 +482,14 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
       f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        sv = mfma(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], sv);
+        sv = mfma_t<H>(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], sv);
         dp = mfma(row_frag(Vimg, kt * 16 + lr, 32 * ks + 8 * g), df[ks], dp);
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int key = kt * 16 + 4 * g + i;
         const bool ok = qok && key < T;
-        const float p = ok ? exp2_fast(sv[i] * c2 - ls) : 0.f;
+        const float p = ok ? exp2_fast(fmaf(sv[i], c2, -ls)) : 0.f;
         const float kp = (DM == 2) ? (((mw[kt >> 1] >> ((kt & 1) * 16 + 4 * g + i)) & 1u) ? dc.scale : 0.f)
                                          : keep_scale<DROP>(dc, rowidx + key);
         const float pd = ok ? dp[i] * kp : 0.f;
@@ -480,7 +514,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
       const bf16x8 bs = pack_acc(ds[0], ds[1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
-        dq[dt] = mfma(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dq[dt]);
+        dq[dt] = mfma(to_b16<H>(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr)), bs, dq[dt]);
     }
     if (qok) {
       const int64_t r = (row0 + q) * ld + h * DH;
@@ -517,12 +551,18 @@ int init_attrs() {
   rc |= set_lds(attn16_fwd_k<0, true>, FWD_LDS);
   rc |= set_lds(attn16_fwd_k<1, true>, FWD_LDS);
   rc |= set_lds(attn16_fwd_k<2, true>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<0>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<1>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<2>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<0>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<1>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<2>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<0, false>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<1, false>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<2, false>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<0, false>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<1, false>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<2, false>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<0, true>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<1, true>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dkv_k<2, true>, BWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<0, true>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<1, true>, FWD_LDS);
+  rc |= set_lds(attn16_bwd_dq_k<2, true>, FWD_LDS);
   done = rc;
   return rc;
 }
@@ -574,9 +614,10 @@ extern "C" int b2p_attn16_fwd_f16(const void* qkv16h, void* O16h, void* Ob16, fl
   return attn16_fwd_launch(true, qkv16h, O16h, Ob16, lse2, B, T, nh, dh, scale, drop_p, drop_seed, mask, stream);
 }
 
-extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws, float* dqkv,
-                              void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh, float scale, float drop_p,
-                              uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream) {
+namespace {
+int attn16_bwd_launch(bool half, const void* qkv16, const void* dO16, const float* lse2, float* delta_ws, float* dqkv,
+                      void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh, float scale, float drop_p,
+                      uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream) {
   B2P_CHECK_ARG(qkv16 && dO16 && lse2 && delta_ws && (dqkv || dqkv16), "attn16_bwd: NULL pointer");
   B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_bwd: needs head size 64 and T <= 256");
   if (B <= 0) return 0;
@@ -587,16 +628,36 @@ extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* 
   hipStream_t st = (hipStream_t)stream;
   const uint16_t *q = (const uint16_t*)qkv16, *d = (const uint16_t*)dO16;
   uint16_t* d16 = (uint16_t*)dqkv16;
-  auto run = [&](auto dm) {
+  auto run = [&](auto dm, auto hc) {
     constexpr int DM = decltype(dm)::value;
-    hipLaunchKernelGGL(attn16_bwd_dq_k<DM>, grid_q, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
-                       (int)nh, scale, dc, mask);
-    hipLaunchKernelGGL(attn16_bwd_dkv_k<DM>, grid_k, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16, (int)T,
-                       (int)nh, scale, dc, mask);
+    constexpr bool HH = decltype(hc)::value;
+    hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH>), grid_q, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16,
+                       (int)T, (int)nh, scale, dc, mask);
+    hipLaunchKernelGGL((attn16_bwd_dkv_k<DM, HH>), grid_k, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16,
+                       (int)T, (int)nh, scale, dc, mask);
   };
-  if (drop_p > 0.f && mask) run(std::integral_constant<int, 2>());
-  else if (drop_p > 0.f) run(std::integral_constant<int, 1>());
-  else run(std::integral_constant<int, 0>());
+  auto by_dm = [&](auto hc) {
+    if (drop_p > 0.f && mask) run(std::integral_constant<int, 2>(), hc);
+    else if (drop_p > 0.f) run(std::integral_constant<int, 1>(), hc);
+    else run(std::integral_constant<int, 0>(), hc);
+  };
+  if (half) by_dm(std::true_type());
+  else by_dm(std::false_type());
   B2P_CHECK_LAUNCH();
   return 0;
+}
+}  // namespace
+
+extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws, float* dqkv,
+                              void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh, float scale, float drop_p,
+                              uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream) {
+  return attn16_bwd_launch(false, qkv16, dO16, lse2, delta_ws, dqkv, dqkv16, B, T, nh, dh, scale, drop_p, drop_seed,
+                           mask, stream);
+}
+
+extern "C" int b2p_attn16_bwd_f16(const void* qkv16h, const void* dO16, const float* lse2, float* delta_ws,
+                                  float* dqkv, void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh, float scale,
+                                  float drop_p, uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream) {
+  return attn16_bwd_launch(true, qkv16h, dO16, lse2, delta_ws, dqkv, dqkv16, B, T, nh, dh, scale, drop_p, drop_seed,
+                           mask, stream);
 }

@@ -23,6 +23,7 @@
 #include "gemm_epi.h"
 #include <stdio.h>
 #include <stdlib.h>
+#include <type_traits>
 
 namespace {
 
@@ -236,8 +237,18 @@ __device__ __forceinline__ void store_colsum(const EpiArgs& ea, float* Cs, int t
 // output tile of linear tile index t: row-major (grp = 0), or grouped (grp > 0): column sweeps over
 // bands of grp row tiles, so the workgroups resident on one XCD at a time share a few A row panels
 // and a few B column panels in that XCD's L2 instead of cycling through all of B
+// grp < 0: column bands of G = (tiles_n <= 8 ? tiles_n : ceil(tiles_n / 8)) output columns, row-major
+// inside a band: the workgroups of one XCD (a contiguous range of this order, see the remap) then hold
+// a G-column slice of B in their L2 while every A row panel they fetch feeds G tiles running side by side
 __device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int grp, int& tm, int& tn) {
-  if (grp > 0) {
+  if (grp < 0) {
+    const int G = tiles_n <= 8 ? tiles_n : (tiles_n + 7) / 8;
+    const int per = G * tiles_m;
+    const int band = t / per, r = t - band * per;
+    const int gs = tiles_n - band * G < G ? tiles_n - band * G : G;
+    tm = r / gs;
+    tn = band * G + (r - tm * gs);
+  } else if (grp > 0) {
     const int per = grp * tiles_n;
     const int g = t / per, first = g * grp;
     const int gs = tiles_m - first < grp ? tiles_m - first : grp;
@@ -250,12 +261,12 @@ __device__ __forceinline__ void tile_of(int t, int tiles_m, int tiles_n, int grp
   }
 }
 
-// Tile configurations: BM x BN output tile, WGM x WGN waves of 64 x 64 each (4 x 4 MFMA tiles),
+// Tile configurations: BM x BN output tile, WGM x WGN waves of WTM x 64 each ((WTM/16) x 4 MFMA tiles),
 // KT-deep k-tiles, S LDS stages (S-1 tiles in flight behind counted vmcnt waits + raw barriers).
-template <int BM_, int BN_, int KT_, int S_>
+template <int BM_, int BN_, int KT_, int S_, int WTM_ = 64>
 struct Cfg {
-  static constexpr int BM = BM_, BN = BN_, KT = KT_, S = S_;
-  static constexpr int WGM = BM / 64, WGN = BN / 64, NW = WGM * WGN, NT = NW * 64;
+  static constexpr int BM = BM_, BN = BN_, KT = KT_, S = S_, WTM = WTM_, MI = WTM_ / 16;
+  static constexpr int WGM = BM / WTM, WGN = BN / 64, NW = WGM * WGN, NT = NW * 64;
   static constexpr int STAGE = (BM + BN) * KT * 2;
   static constexpr int LDS_MAIN = S * STAGE;
   static constexpr int CS_LD = BN + 4;                          // epilogue staging row (floats)
@@ -264,6 +275,10 @@ struct Cfg {
   static constexpr int OCC = LDS > 80 * 1024 ? 1 : 2;           // workgroups per CU
 };
 using CfgSmall = Cfg<128, 128, 32, 3>;   // 4 waves, 3 workgroups/CU by LDS (48 KB) and VGPRs (143)
+// 256 x 128 tiles of 4 waves with 128 x 64 wave tiles (8 x 4 MFMA tiles): a quarter less operand traffic
+// per FLOP than 128 x 128 (1/256 + 1/128 vs 2/128 of K per output) and 12 fragment reads per 32 MFMAs
+// instead of 8 per 16; 72 KB of LDS, 2 workgroups per CU (B2P_GEMM16_TALL)
+using CfgTall = Cfg<256, 128, 32, 3, 128>;
 // Measured and removed (DESIGN.md "rejected"): 128 x 128 x 64 two-stage tiles (no gain inside the step),
 // 128 x 64 tiles for N <= 1024 grids (59.3 -> 57.1 steps/s), 4-stage 128 x 128 x 32 (-10 % at K = 768),
 // 256 x 128 x 64 eight-wave tiles (lock-stepped waves idle the MFMA pipe at every barrier).
@@ -313,9 +328,10 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_
   sa.init(d.A, z1, z2, wave, lane, m0, M, kbeg);
   sb.init(d.B, z1, z2, wave, lane, n0, N, kbeg);
 
-  f32x4 acc[4][4];
+  constexpr int MI = CF::MI;
+  f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
@@ -345,22 +361,29 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_
     const char* Bs = As + A_BYTES;
 #pragma unroll
     for (int kk = 0; kk < KT / 32; ++kk) {
-      bf16x8 af[4], bfr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-        af[i] = AK ? frag_k<KT>(As, wm * 64 + i * 16, kk, lane) : frag_t<BM>(As, wm * 64 + i * 16, kk, lane);
+      bf16x8 bfr[4];
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         bfr[j] = BK ? frag_k<KT>(Bs, wn * 64 + j * 16, kk, lane) : frag_t<BN>(Bs, wn * 64 + j * 16, kk, lane);
+      // A fragments in groups of 4 rows of MFMA tiles: at most 8 fragments live beside the
+      // (MI x 4) accumulators (the 128-row wave tile would otherwise exceed 256 registers)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i0 = 0; i0 < MI; i0 += 4) {
+        bf16x8 af[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-          if constexpr (H16)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8g, af[i]),
-                                                               __builtin_bit_cast(f16x8g, bfr[j]), acc[i][j], 0, 0, 0);
-          else
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < 4; ++i)
+          af[i] = AK ? frag_k<KT>(As, wm * CF::WTM + (i0 + i) * 16, kk, lane)
+                     : frag_t<BM>(As, wm * CF::WTM + (i0 + i) * 16, kk, lane);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if constexpr (H16)
+              acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(
+                  __builtin_bit_cast(f16x8g, af[i]), __builtin_bit_cast(f16x8g, bfr[j]), acc[i0 + i][j], 0, 0, 0);
+            else
+              acc[i0 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i0 + i][j], 0, 0, 0);
+      }
     }
     cur = cur + 1 == S ? 0 : cur + 1;
     nxt = nxt + 1 == S ? 0 : nxt + 1;
@@ -370,18 +393,25 @@ __global__ void __launch_bounds__(CF::NT, CF::OCC) gemm16_kernel(const b2p_gemm_
   float* Cs = reinterpret_cast<float*>(smem);
   float* slab = ks > 1 ? d.workspace + ((int64_t)z * ks + ksl) * (int64_t)M * N : nullptr;
   float4 csum = make_float4(0.f, 0.f, 0.f, 0.f);   // fused bias-gradient column sums (colsum_part)
+  constexpr int HB = CF::WTM / 64;   // 64-row bands per wave row
 #pragma unroll
-  for (int band = 0; band < CF::WGM; ++band) {
+  for (int band = 0; band < BM / 64; ++band) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __syncthreads();
-    if (wm == band) {
+    if (wm == band / HB) {
+      // static accumulator indices on both paths (a runtime index would move acc to scratch)
+      auto stage = [&](auto hbc) {
+        constexpr int hb = decltype(hbc)::value;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+          for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            Cs[(i * 16 + (lane >> 4) * 4 + r) * CS_LD + wn * 64 + j * 16 + (lane & 15)] = acc[i][j][r];
+            for (int r = 0; r < 4; ++r)
+              Cs[(i * 16 + (lane >> 4) * 4 + r) * CS_LD + wn * 64 + j * 16 + (lane & 15)] = acc[hb * 4 + i][j][r];
+      };
+      if (band % HB == 0) stage(std::integral_constant<int, 0>());
+      else if constexpr (HB > 1) stage(std::integral_constant<int, 1>());
     }
     __syncthreads();
     store_band<BN, NT, B2P_EPI_UNROLL_SMALL>(ea, Cs, tid, z, z1, z2, M, N, slab, m0 + band * 64, n0, csum);
@@ -656,6 +686,16 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   if (ks > 1 && d.kchunk % 32 != 0) {
     b2p_set_error("gemm16: split-K chunk must be a multiple of 32");
     return 1;
+  }
+  // 256 x 128 tiles (B2P_GEMM16_TALL: 0 off, 1 when the grid still gives every CU at least `tall_min`
+  // tiles of 256 x 128, default 2): plain or conv operands, any split
+  static int tall = getenv("B2P_GEMM16_TALL") ? atoi(getenv("B2P_GEMM16_TALL")) : 0;
+  static int tall_min = getenv("B2P_GEMM16_TALL_MIN") ? atoi(getenv("B2P_GEMM16_TALL_MIN")) : 512;
+  const int tmt = (int)((d.M + 255) / 256);
+  const int64_t nwg_t = (int64_t)tmt * tn * nz;
+  if (tall && nwg_t >= tall_min) {
+    launch_cfg<CfgTall>(d, ea, st, dim3((unsigned)nwg_t), tmt, tn);
+    return 0;
   }
   launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
   return 0;

@@ -1502,8 +1502,8 @@ def _attn16_fwd(qkv16, B, T, nh, dh, p_attn, seed, want_mask=False):
 # bf16 precision mode: the fused attention's forward operands (Q, K, V, the probabilities, O) in fp16
 # (csrc/attn16.hip b2p_attn16_fwd_f16). bf16's 8-bit mantissa on the scores / probabilities biased the
 # 24-layer models' CTC loss by ~1e-3 relative (tools/fixture_err.py: with the attention alone in exact
-# fp32 the Conformer-large error fell from 1.0e-3 to 8e-5). The QKV projection writes the fp16 operand
-# and a bf16 copy for the backward kernels; B2P_ATTN_F16=0 keeps the bf16 forward (A/B).
+# fp32 the Conformer-large error fell from 1.0e-3 to 8e-5). The QKV projection writes the fp16 operand,
+# the backward recomputes the scores from it (b2p_attn16_bwd_f16); B2P_ATTN_F16=0 keeps bf16 (A/B).
 ATTN_F16 = os.environ.get("B2P_ATTN_F16", "1") != "0"
 
 
@@ -1522,12 +1522,13 @@ def _attn16_fwd_f16(qkvh, B, T, nh, dh, p_attn, seed):
 
 def _attn16_bwd(qkv16, dO16, lse2, B, T, nh, dh, p_attn, seed, want32=True, mask=None):
     """-> dqkv (B*T, 3D) f32 (or None) and its bf16 copy (mask: the forward's keep bits, or None to
-    re-hash)."""
+    re-hash). qkv16 fp16 (the _attn16_fwd_f16 forward) selects b2p_attn16_bwd_f16."""
     dev = qkv16.device
     dqkv = torch.empty(B * T, 3 * nh * dh, device=dev) if want32 else None
     d16 = torch.empty(B * T, 3 * nh * dh, device=dev, dtype=BF16)
     delta = torch.empty(B, nh, T, device=dev)
-    _lib.call("b2p_attn16_bwd", _p(qkv16), _p(dO16), _p(lse2), _p(delta), _p(dqkv), _p(d16), B, T, nh, dh,
+    fn = "b2p_attn16_bwd_f16" if qkv16.dtype == torch.float16 else "b2p_attn16_bwd"
+    _lib.call(fn, _p(qkv16), _p(dO16), _p(lse2), _p(delta), _p(dqkv), _p(d16), B, T, nh, dh,
               float(dh ** -0.5), float(p_attn), seed, None if mask is None else mask.data_ptr(), _st())
     return dqkv, d16
 
@@ -1656,14 +1657,13 @@ class _EncoderLayer16(torch.autograd.Function):
         fused = attn16_ok(T, dh)
         Oh = None
         if fused:
-            qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16)     # bf16 only: attention operand
-            if ATTN_F16:   # fp16 forward operand + the backward's bf16 copy from one epilogue
-                qkvh = torch.empty(NT, 3 * D, device=dev, dtype=torch.float16)
-                gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), None, 3 * D, bias=bqkv, C16=qkvh,
-                     c16_fp16=True, pre16=qkv)
-                Oh, O16, P, Pd = _attn16_fwd_f16(qkvh, B, T, nh, dh, p_attn, seeds[0])
-                del qkvh
+            if ATTN_F16:   # fp16 attention operand (the saved qkv: the backward recomputes from it)
+                qkv = torch.empty(NT, 3 * D, device=dev, dtype=torch.float16)
+                gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), None, 3 * D, bias=bqkv, C16=qkv,
+                     c16_fp16=True)
+                Oh, O16, P, Pd = _attn16_fwd_f16(qkv, B, T, nh, dh, p_attn, seeds[0])
             else:
+                qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16)     # bf16 only: attention operand
                 gemm(NT, 3 * D, D, op(x16, 0, D, True), op(wqkv16, 0, D, True), None, 3 * D, bias=bqkv, C16=qkv)
                 # P slot: lse2, Pd slot: the dropout keep bits for the backward
                 O16, P, Pd = _attn16_fwd(qkv, B, T, nh, dh, p_attn, seeds[0], want_mask=True)
@@ -2181,9 +2181,10 @@ class _ConformerAttnBlock(torch.autograd.Function):
         # QKV GEMMs then write only the bf16 operand, and the saved slots hold qkv16 / lse2 / dropout
         # keep bits / O16
         ctx.fused = bf16_mode() and attn16_ok(T, hd)
-        qkv = torch.empty(NT, 3 * D, device=dev, dtype=BF16 if ctx.fused else torch.float32)
-        # fused, ATTN_F16: the projections write the fp16 attention operand and the backward's bf16 copy
-        qkvh = torch.empty(NT, 3 * D, device=dev, dtype=torch.float16) if (ctx.fused and ATTN_F16) else None
+        # fused: the 16-bit attention operand (fp16 under ATTN_F16: the backward recomputes from it)
+        qkv = torch.empty(NT, 3 * D, device=dev, dtype=(torch.float16 if ATTN_F16 else BF16) if ctx.fused
+                          else torch.float32)
+        f16a = ctx.fused and ATTN_F16
         if bf16_mode():
             # the Q/K/V operands come straight from their producers as 16-bit copies (LayerNorm, rotary):
             # fp16 under forward_f16, else bf16; the fp32 rotated copy is never stored
@@ -2197,9 +2198,9 @@ class _ConformerAttnBlock(torch.autograd.Function):
             hr = None
             for i, (w, bb, src) in enumerate(((wq, bq, hr16), (wk, bk, hr16), (wv, bv, h16))):
                 wbuf, wop = _w_op16(w, half)
-                if qkvh is not None:
-                    gemm(NT, D, D, op(src, 0, D, True), wop, None, 3 * D, c_off=i * D, bias=bb, C16=qkvh,
-                         c16_fp16=True, pre16=qkv)
+                if f16a:
+                    gemm(NT, D, D, op(src, 0, D, True), wop, None, 3 * D, c_off=i * D, bias=bb, C16=qkv,
+                         c16_fp16=True)
                 elif ctx.fused:
                     gemm(NT, D, D, op(src, 0, D, True), wop, None, 3 * D, c_off=i * D, bias=bb, C16=qkv)
                 else:
@@ -2217,9 +2218,8 @@ class _ConformerAttnBlock(torch.autograd.Function):
             for i, (w, bb, src) in enumerate(((wq, bq, hr), (wk, bk, hr), (wv, bv, h))):
                 gemm(NT, D, D, op(src, 0, D, True), op(w, 0, D, True), qkv, 3 * D, c_off=i * D, bias=bb)
         y = torch.empty(NT, D, device=dev)
-        if qkvh is not None:
-            Oh, O, P, Pd = _attn16_fwd_f16(qkvh, B, T, nh, hd, p_attn, seeds[0])
-            del qkvh
+        if f16a:
+            Oh, O, P, Pd = _attn16_fwd_f16(qkv, B, T, nh, hd, p_attn, seeds[0])
             wbuf, wop = _w_op16(wo, True)
             gemm(NT, D, D, op(Oh, 0, D, True), wop, y, D, bias=bo, drop_p=p_out, seed=seeds[1], residual=x2)
             del Oh, wbuf
