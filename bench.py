@@ -163,30 +163,52 @@ def cpu_baseline(cfg, steps=5):
                       f"{steps} steps after 1 warm-up")
 
 
-def parity_check(cfg, device, steps=2):
-    """north_star parity: the CTC loss of `steps` consecutive Trainer steps (HIP, bf16, HipAdam over the
-    brain encoder, lr 1e-3) vs the fp32 CPU oracle on identical weights and inputs, deterministic
-    mode (dropout 0, LayerDrop 0: the reference's Philox masks cannot be reproduced); steps > 1 also
-    check the optimizer update. Tolerance 1e-3 rel (BASELINE.json north_star). Returns the record and
-    the oracle's per-step times (the Conformer's CPU baseline reuses them)."""
+def _hip_losses(cfg, device, steps, mode):
+    """CTC losses of `steps` consecutive deterministic Trainer steps (HipAdam lr 1e-3 over the brain
+    encoder) in precision `mode`, from the workload's deterministic weights; also returns them."""
+    from wav2vec2forbrain_amd import functional as Fn
     from wav2vec2forbrain_amd.train.train_loop import Trainer
     from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
     model = build(cfg, device, train_dropouts=False)
     model.train()
     sd = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
-    trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
-    batch = batch_on(cfg, device)
-    hip = [float(trainer._eager_body(batch).metrics["ctc_loss"]) for _ in range(steps)]
+    with Fn.precision(mode):
+        trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+        hip = [float(trainer._eager_body(batch_on(cfg, device)).metrics["ctc_loss"]) for _ in range(steps)]
     torch.cuda.synchronize()
+    Fn.set_deferred_wgrad([])
     del trainer, model
     free_device()
+    return hip, sd
+
+
+def parity_check(cfg, device, steps=2):
+    """north_star parity: the CTC loss of `steps` consecutive Trainer steps vs the fp32 CPU oracle on
+    identical weights and inputs, deterministic mode (dropout 0, LayerDrop 0: the reference's Philox
+    masks cannot be reproduced), HipAdam lr 1e-3 over the brain encoder between steps. Two HIP runs:
+      bf16  the bench's precision. The first step (identical weights) is the north-star check (1e-3
+            relative); later steps show how far the trajectories drift apart: Adam's early updates are
+            ~lr * sign(g), so gradient entries below bf16 resolution move a parameter by a full lr in a
+            rounding-chosen direction, and the drift grows with the step count.
+      fp32  exact-fp32 MFMA mode: the same trajectory must track the oracle step by step (1e-4), which
+            separates rounding drift from a wrong update.
+    Returns the record and the oracle's per-step times (the Conformer's CPU baseline reuses them)."""
+    b16, sd = _hip_losses(cfg, device, steps, "bf16")
+    f32, _ = _hip_losses(cfg, device, steps, "fp32")
     ref, times, threads, n_phys, model_name = oracle_steps(cfg, sd, steps, train_dropouts=False)
-    rel = [abs(h - r) / abs(r) for h, r in zip(hip, ref)]
-    rec = {"mode": "deterministic (dropout 0, LayerDrop 0), bf16 HIP Trainer steps vs fp32 CPU oracle, same "
+    rel = lambda hip: [abs(h - r) / abs(r) for h, r in zip(hip, ref)]
+    rb, rf = rel(b16), rel(f32)
+    rec = {"mode": "deterministic (dropout 0, LayerDrop 0) HIP Trainer steps vs fp32 CPU oracle, same "
                    "weights/inputs, Adam lr 1e-3 over the brain encoder between steps",
-           "steps": steps, "hip_ctc_loss": [round(v, 6) for v in hip], "oracle_ctc_loss": [round(v, 6) for v in ref],
-           "rel_err": [float(f"{r:.3e}") for r in rel], "max_rel_err": float(f"{max(rel):.3e}"), "tolerance": 1e-3,
-           "pass": max(rel) <= 1e-3}
+           "steps": steps, "oracle_ctc_loss": [round(v, 6) for v in ref],
+           "hip_ctc_loss": [round(v, 6) for v in b16], "rel_err": [float(f"{r:.3e}") for r in rb],
+           "max_rel_err": float(f"{max(rb):.3e}"),
+           "fp32_mode": {"hip_ctc_loss": [round(v, 6) for v in f32], "rel_err": [float(f"{r:.3e}") for r in rf],
+                         "tolerance": 1e-4},
+           "tolerance": 1e-3,
+           "criterion": "bf16 step 1 (identical weights) <= 1e-3 and every fp32-mode step <= 1e-4; bf16 steps "
+                        "after Adam updates reported as drift",
+           "pass": rb[0] <= 1e-3 and max(rf) <= 1e-4}
     return rec, (times, threads, n_phys, model_name)
 
 

@@ -14,3 +14,7 @@ for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WA
 done
 python3 tools/gemm_pmc_census.py report $O $(for k in 1 2 3 4; do find $O/p$k -name "*.db" | head -1; done) > $O/census_$C.txt 2>&1
 head -40 $O/census_$C.txt
+# the fused attention kernels' counters from the same passes, then drop the databases (gpurun copies
+# back at most 64 MiB of gpurun_out/)
+for k in 3 4; do db=$(find $O/p$k -name "*.db" | head -1); [ -n "$db" ] && python3 tools/pmc_summary.py $db attn16 >> $O/attn_pmc_$C.txt 2>&1; done
+find $O -name "*.db" -delete
