@@ -369,8 +369,10 @@ int b2p_gru_mc_debug_withhold(int member);
  * identical to b2p_softmax_fwd's. fwd runs one workgroup per (batch, head, 128 queries). bwd writes
  * [dQ | dK | dV] into dqkv (f32, may be NULL) and/or dqkv16 (bf16, may be NULL), same layout as qkv;
  * delta_ws: B*nh*T floats of workspace (row constants sum_key P_d dP_d). mask (optional, drop_p > 0):
- * uint32 [B][nh][T][8], written by fwd as the keep bits of each row (key k = bit k%32 of word k/32)
- * and read by bwd instead of re-hashing every (q, key) twice; NULL: bwd recomputes the hash. */
+ * 32 bytes per query row ([B][nh][T][32] uint8), written by fwd and read by bwd instead of re-hashing
+ * every (q, key) twice: byte 8*g + c with g = (key >> 2) & 3 and c = key >> 5 holds keys 32c + 4g + i
+ * (bit i) and 32c + 16 + 4g + i (bit 4 + i), i < 4 (each forward lane writes its own 8 bytes);
+ * NULL: bwd recomputes the hash. */
 int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
                    int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
                    b2p_stream_t stream);

@@ -246,9 +246,11 @@ def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
             # the keep bits the forward stored are the hash mask, bit for bit (integer check against
             # a numpy restatement of b2p_keep); the two backward forms then differ only by the
             # compiler's fp contraction of the identical arithmetic
-            words = mask.cpu().numpy().view(np.uint32)
-            bits = (words[..., :, None] >> np.arange(32, dtype=np.uint32)) & 1
-            bits = bits.reshape(B, nh, T, 256)[..., :T]
+            words = mask.cpu().numpy().view(np.uint32)          # (B, nh, T, 8): 32 bytes per query row
+            keys = np.arange(256)
+            w = (keys >> 7) + 2 * ((keys >> 2) & 3)             # byte 8*g + c, g = (key>>2)&3, c = key>>5
+            sh = (8 * ((keys >> 5) & 3) + 4 * ((keys >> 4) & 1) + (keys & 3)).astype(np.uint32)
+            bits = ((words[..., w] >> sh) & 1)[..., :T]
             np.testing.assert_array_equal(bits, _keep_mask_ref(seed, p, B, nh, T).astype(np.uint32))
             assert float((h32 - dq32).norm()) <= 1e-5 * float(dq32.norm())
         torch.cuda.synchronize()

@@ -24,16 +24,20 @@ B = int(sys.argv[1]) if len(sys.argv) > 1 else 32
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 249
 nh = int(sys.argv[3]) if len(sys.argv) > 3 else 12
 dh = 64
-q16 = (torch.randn(B * T, 3 * nh * dh, device="cuda") * 0.5).to(torch.bfloat16)
+q = torch.randn(B * T, 3 * nh * dh, device="cuda") * 0.5
 dO = torch.randn(B * T, nh * dh, device="cuda").to(torch.bfloat16)
 fl = 4.0 * B * nh * T * T * dh
-for p in (0.0, 0.1):
-    O16, lse2, mask = Fn._attn16_fwd(q16, B, T, nh, dh, p, 5, want_mask=True)
-    tf = timeit(lambda: Fn._attn16_fwd(q16, B, T, nh, dh, p, 5, want_mask=True))
-    tb = timeit(lambda: Fn._attn16_bwd(q16, dO, lse2, B, T, nh, dh, p, 5, mask=mask))
-    print(f"attn16 B={B} T={T} nh={nh} p={p}: fwd {tf:.1f} us ({fl / tf / 1e6:.0f} TFLOP/s), "
-          f"bwd {tb:.1f} us ({2.5 * fl / tb / 1e6:.0f} TFLOP/s)", flush=True)
-    if p > 0:   # the re-hashing variants (no stored mask), for the kernel trace
-        th_f = timeit(lambda: Fn._attn16_fwd(q16, B, T, nh, dh, p, 5))
-        th_b = timeit(lambda: Fn._attn16_bwd(q16, dO, lse2, B, T, nh, dh, p, 5))
-        print(f"  hash variants: fwd {th_f:.1f} us, bwd {th_b:.1f} us", flush=True)
+for kind in ("f16", "bf16"):
+    for p in (0.0, 0.1):
+        if kind == "f16":
+            q16 = q.to(torch.float16)
+            fwd = lambda: Fn._attn16_fwd_f16(q16, B, T, nh, dh, p, 5)
+            _, _, lse2, mask = fwd()
+        else:
+            q16 = q.to(torch.bfloat16)
+            fwd = lambda: Fn._attn16_fwd(q16, B, T, nh, dh, p, 5, want_mask=True)
+            _, lse2, mask = fwd()
+        tf = timeit(fwd)
+        tb = timeit(lambda: Fn._attn16_bwd(q16, dO, lse2, B, T, nh, dh, p, 5, mask=mask))
+        print(f"attn16[{kind}] B={B} T={T} nh={nh} p={p}: fwd {tf:.1f} us ({fl / tf / 1e6:.0f} TFLOP/s), "
+              f"bwd {tb:.1f} us ({2.5 * fl / tb / 1e6:.0f} TFLOP/s)", flush=True)

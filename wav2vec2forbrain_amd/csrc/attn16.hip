@@ -157,6 +157,10 @@ __device__ __forceinline__ float keep_scale(const DropCfg& dc, uint64_t idx) {
 // Dropout keep bits come two per hash (b2p_hash of idx >> 1, 16-bit halves) with the row stride TP
 // = T rounded up to even, so a lane's 4 consecutive keys need exactly 2 hashes.
 constexpr int FWD_NT = 256;
+// Stored keep mask: 32 bytes per query row, byte 8*g + c (g = (key >> 2) & 3, c = key >> 5) holds keys
+// 32c + 4g + i (bit i) and 32c + 16 + 4g + i (bit 4 + i): each forward lane writes its own 8 bytes.
+// Within 32-bit word (key >> 5) / 4 + 2g of the row: bit position of key
+__device__ __forceinline__ int mask_shift(int key) { return 8 * ((key >> 5) & 3) + 4 * ((key >> 4) & 1) + (key & 3); }
 constexpr int FWD_QB = 128;   // queries per workgroup
 // the 4 keep bits of keys key0 .. key0+3 (key0 % 4 == 0) of mask row `row` (32-bit element index:
 // b2p_hash with idx >> 32 == 0, checked on the host)
@@ -257,31 +261,29 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     f32x4 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    uint32_t mbits[2] = {0u, 0u};   // this lane's keep bits: byte c = keys 32c + 4g + i (bit i), +16 (bit 4 + i)
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      uint32_t word = 0;   // keep bits of keys 32c .. 32c+31 (this lane's 8 of them)
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const int key0 = (2 * c + half) * 16 + 4 * g;
         const uint32_t kb = DROP ? keep4_bits(rowlo + (uint32_t)key0, k32, thr16) : 0xFu;
-        if (DROP) word |= kb << (half * 16 + 4 * g);
+        if (DM == 2) mbits[c >> 2] |= kb << (8 * (c & 3) + 4 * half);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float pv = s[2 * c + half][i] * inv_s;
           s[2 * c + half][i] = (DROP && !((kb >> i) & 1u)) ? 0.f : pv;
         }
       }
-      if (DM == 2) {
-        // the mask as bits for the backward kernels ([b][h][q][8] words): OR over the 4 lanes of a query
-        word |= (uint32_t)__shfl_xor((int)word, 16, 64);
-        word |= (uint32_t)__shfl_xor((int)word, 32, 64);
-        if (qok && g == 0) maskw[(((int64_t)b * nh + h) * T + q) * 8 + c] = word;
-      }
       const bf16x8 bp = pack_acc_t<H>(s[2 * c], s[2 * c + 1]);
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt)
         o[dt] = mfma_t<H>(tr_frag(Vimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bp, o[dt]);
     }
+    // the keep bits for the backward kernels, each lane's own 8 bytes: mask row (32 bytes per query)
+    // = [lane group g][chunk c] bytes (mask_bit() below)
+    if (DM == 2 && qok)
+      *reinterpret_cast<uint2*>(maskw + (((int64_t)b * nh + h) * T + q) * 8 + 2 * g) = make_uint2(mbits[0], mbits[1]);
     const int64_t orow = (row0 + q) * D + h * DH;
     if (qok) {
 #pragma unroll
@@ -337,10 +339,9 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
     const int64_t o = ((int64_t)b * nh + h) * T + qq;
     del_s[qq] = qq < T ? delta[o] : 0.f;
     lse_s[qq] = qq < T ? lse2[o] : 0.f;
-    if (DM == 2) {   // the keep bits of keys 128kb .. 128kb+127 for every query row
-      const int wbase = (BWD_KB / 32) * kb;
+    if (DM == 2) {   // the keep bits of keys 128kb .. 128kb+127 for every query row: word 2g + kb, g = 0..3
 #pragma unroll
-      for (int j = 0; j < BWD_KB / 32; ++j) msk_s[4 * qq + j] = (qq < T && wbase + j < 8) ? maskw[o * 8 + wbase + j] : 0u;
+      for (int j = 0; j < 4; ++j) msk_s[4 * qq + j] = qq < T ? maskw[o * 8 + 2 * j + kb] : 0u;
     }
   }
   __syncthreads();
@@ -355,7 +356,8 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
     const char* dOimg = smem + TMAX * 128 + obase;
     const int key = kt * 16 + lr;
     const bool kok = key < T;
-    const int kw = (key >> 5) & 3;   // this key's word among the block's 4
+    const int kw = (key >> 2) & 3;                 // this key's word among the block's 4 (its lane group)
+    const int ksh = mask_shift(key);
     bf16x8 kf[2], vf[2];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
@@ -394,7 +396,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
           const bool ok = kok && qq < T;
           const float p = ok ? exp2_fast(fmaf(sv[i], c2, -lse_s[qq])) : 0.f;
           const float ksc = !ok ? 0.f
-                            : (DM == 2) ? (((mw[half][i] >> (key & 31)) & 1u) ? dc.scale : 0.f)
+                            : (DM == 2) ? (((mw[half][i] >> ksh) & 1u) ? dc.scale : 0.f)
                                               : keep_scale<DROP>(dc, (bh * T + qq) * (uint64_t)TP + key);
           pd[half][i] = p * ksc;
           ds[half][i] = p * (dp[i] * ksc - del_s[qq]);
@@ -469,12 +471,8 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
     const int64_t rowc = ((int64_t)b * nh + h) * T + (qok ? q : 0);
     const float ls = qok ? lse2[rowc] : 0.f;
     const uint64_t rowidx = (uint64_t)rowc * (uint64_t)TP;
-    uint32_t mw[8];   // this query row's keep bits (from the forward)
-    if (DM == 2) {
-      const uint4* mp = reinterpret_cast<const uint4*>(maskw + (int64_t)rowc * 8);
-      const uint4 m0 = qok ? mp[0] : make_uint4(0, 0, 0, 0), m1 = qok ? mp[1] : make_uint4(0, 0, 0, 0);
-      mw[0] = m0.x; mw[1] = m0.y; mw[2] = m0.z; mw[3] = m0.w; mw[4] = m1.x; mw[5] = m1.y; mw[6] = m1.z; mw[7] = m1.w;
-    }
+    uint2 mw = make_uint2(0u, 0u);   // this lane's keep bytes of the query row (keys kt*16 + 4g + i)
+    if (DM == 2 && qok) mw = *reinterpret_cast<const uint2*>(maskw + (int64_t)rowc * 8 + 2 * g);
     f32x4 P[16], PD[16];
     float dl = 0.f;
 #pragma unroll
@@ -490,7 +488,8 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
         const int key = kt * 16 + 4 * g + i;
         const bool ok = qok && key < T;
         const float p = ok ? exp2_fast(fmaf(sv[i], c2, -ls)) : 0.f;
-        const float kp = (DM == 2) ? (((mw[kt >> 1] >> ((kt & 1) * 16 + 4 * g + i)) & 1u) ? dc.scale : 0.f)
+        const float kp = (DM == 2) ? ((((kt < 8 ? mw.x : mw.y) >> (8 * ((kt >> 1) & 3) + 4 * (kt & 1) + i)) & 1u)
+                                          ? dc.scale : 0.f)
                                          : keep_scale<DROP>(dc, rowidx + key);
         const float pd = ok ? dp[i] * kp : 0.f;
         P[kt][i] = p;

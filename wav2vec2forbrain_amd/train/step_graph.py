@@ -27,6 +27,21 @@ from .. import _lib
 from .. import functional as Fn
 
 
+# One capture stream per (device, priority) for the whole process: every stream takes one of the few
+# hardware queues a process gets (GPU_MAX_HW_QUEUES, 4 by default), so captures (one per batch shape,
+# one per model) share it instead of each opening another.
+_CAPTURE_STREAMS: dict = {}
+
+
+def _capture_stream(dev, prio: bool):
+    key = (str(dev), prio)
+    s = _CAPTURE_STREAMS.get(key)
+    if s is None:
+        s = _CAPTURE_STREAMS[key] = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1]
+                                                      if prio else 0)
+    return s
+
+
 class StepGraph:
     def __init__(self, step_fn, optimizer=None, warmup: int = 2, warm_replays: int = 2, epoch=None):
         """step_fn() runs one step on the current stream and returns the loss tensor (no host
@@ -55,7 +70,7 @@ class StepGraph:
         # the captured main stream at the highest priority: the frozen-weight gradient side stream
         # (default priority) only takes CUs the main path leaves idle
         prio = int(os.environ.get("B2P_GRAPH_PRIORITY", "1"))
-        s = torch.cuda.Stream(device=dev, priority=torch.cuda.Stream.priority_range()[1] if prio else 0)
+        s = _capture_stream(dev, bool(prio))
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             for _ in range(self.warmup):         # allocator / side-stream warm-up on the capture stream
@@ -92,6 +107,11 @@ class StepGraph:
         return self.loss
 
     def release(self) -> None:
-        """Back to eager semantics (the seed counter is no longer mixed in)."""
+        """Back to eager semantics (the seed counter is no longer mixed in); the executable graph and
+        its resources are destroyed now rather than whenever the Python object is collected."""
         _lib.check(_lib.load().b2p_set_seed_epoch(None), "b2p_set_seed_epoch")
+        if self.graph is not None:
+            torch.cuda.synchronize()
+            self.graph.reset()
         self.graph = None
+        self.loss = None
