@@ -19,6 +19,10 @@ def one(variant):
     Fn.set_precision("bf16")
     args = types.SimpleNamespace(bs=32, seq=1024, steps=8, warmup=3, evaluator=False, no_roofline=True)
     dev = "cuda:0"
+    if variant.endswith("_nodefer"):   # frozen-weight gradients in-order on the main stream (no side branch)
+        orig = Fn.set_deferred_wgrad
+        Fn.set_deferred_wgrad = lambda params: orig([])
+        variant = variant[:-len("_nodefer")]
     if variant == "base_graph":
         r = bench.timed_run("base", args, 1, 0, dev, True)
         print(f"{variant}: base {r['dt'] / args.steps * 1e3:.2f} ms", flush=True)

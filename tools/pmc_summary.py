@@ -14,7 +14,7 @@ def summarise(db, filt="gemm_kernel"):
     for did, name, cn, v, d in rows:
         if filt not in name:
             continue
-        short = name.split("(")[0][-90:]
+        short = name.replace("(anonymous namespace)::", "").split("(")[0][-90:]
         agg[short][cn].append(v)
         dur[short][did] = d
     out = {}

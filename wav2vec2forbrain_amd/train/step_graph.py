@@ -67,9 +67,11 @@ class StepGraph:
         if self.opt is not None:
             self.opt.make_capturable(dev)
         Fn.set_gemm_timing(False)
-        # the captured main stream at the highest priority: the frozen-weight gradient side stream
-        # (default priority) only takes CUs the main path leaves idle
-        prio = int(os.environ.get("B2P_GRAPH_PRIORITY", "1"))
+        # the capture stream at normal priority (B2P_GRAPH_PRIORITY=1: the highest). A high-priority
+        # capture stream measured the same for the first graph of a process, but every graph captured
+        # after it replayed far slower (Conformer-large step 154 ms instead of 88 ms: the base run's
+        # graph before it in bench.py, or any earlier capture; tools/nested_probe.py, graph_probe.py)
+        prio = int(os.environ.get("B2P_GRAPH_PRIORITY", "0"))
         s = _capture_stream(dev, bool(prio))
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
