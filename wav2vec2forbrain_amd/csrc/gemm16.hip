@@ -279,6 +279,8 @@ using CfgSmall = Cfg<128, 128, 32, 3>;   // 4 waves, 3 workgroups/CU by LDS (48 
 // per FLOP than 128 x 128 (1/256 + 1/128 vs 2/128 of K per output) and 12 fragment reads per 32 MFMAs
 // instead of 8 per 16; 72 KB of LDS, 2 workgroups per CU (B2P_GEMM16_TALL)
 using CfgTall = Cfg<256, 128, 32, 3, 128>;
+// 128 x 128 x 64 tiles, 2 stages (64 KB, 2 workgroups/CU): half the barriers per K (B2P_GEMM16_K64)
+using CfgK64 = Cfg<128, 128, 64, 2>;
 // Measured and removed (DESIGN.md "rejected"): 128 x 128 x 64 two-stage tiles (no gain inside the step),
 // 128 x 64 tiles for N <= 1024 grids (59.3 -> 57.1 steps/s), 4-stage 128 x 128 x 32 (-10 % at K = 768),
 // 256 x 128 x 64 eight-wave tiles (lock-stepped waves idle the MFMA pipe at every barrier).
@@ -695,6 +697,11 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   const int64_t nwg_t = (int64_t)tmt * tn * nz;
   if (tall && nwg_t >= tall_min) {
     launch_cfg<CfgTall>(d, ea, st, dim3((unsigned)nwg_t), tmt, tn);
+    return 0;
+  }
+  static int k64 = getenv("B2P_GEMM16_K64") ? atoi(getenv("B2P_GEMM16_K64")) : 0;
+  if (k64 && (ks == 1 || d.kchunk % 64 == 0)) {
+    launch_cfg<CfgK64>(d, ea, st, dim3((unsigned)nwg), tm, tn);
     return 0;
   }
   launch_cfg<CfgSmall>(d, ea, st, dim3((unsigned)nwg), tm, tn);
