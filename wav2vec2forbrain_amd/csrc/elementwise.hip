@@ -2,6 +2,7 @@
 // activation backward, front-end smoothing / col2im, weight layout transforms, weight norm.
 // All fp32, float4-vectorised along the contiguous dimension where the layout allows.
 #include "common.h"
+#include <stdlib.h>
 #include "../../include/b2p_hip.h"
 
 namespace {
@@ -74,8 +75,19 @@ __global__ void __launch_bounds__(256) colsum_p2(const float* __restrict__ part,
   const int b = blockIdx.y;
   float s = 0.f;
   if (n < N) {
+    // four independent partial sums (loads issued together instead of one dependent chain: the
+    // launches are small, ~12 blocks, so each thread's latency is the kernel's time)
     const float* p = part + (int64_t)b * nblk * N + n;
-    for (int i = rg; i < nblk; i += 4) s += p[(int64_t)i * N];
+    float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+    int i = rg;
+    for (; i + 12 < nblk; i += 16) {
+      s0 += p[(int64_t)i * N];
+      s1 += p[(int64_t)(i + 4) * N];
+      s2 += p[(int64_t)(i + 8) * N];
+      s3 += p[(int64_t)(i + 12) * N];
+    }
+    for (; i < nblk; i += 4) s0 += p[(int64_t)i * N];
+    s = (s0 + s1) + (s2 + s3);
   }
   red[rg][c] = s;
   __syncthreads();
@@ -195,6 +207,7 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
 }
 
 constexpr int LN_BWD_ROWS = 16;   // rows per block (4 per wave): ~500 blocks at 8k rows
+template <bool PF>   // PF: prefetch the next row (B2P_LN_PREFETCH, default 1)
 __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, const float* __restrict__ x,
                                                 const float* __restrict__ gamma, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, float* __restrict__ dx,
@@ -213,19 +226,40 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
   for (int i = 0; i < LN_MAXV; ++i) {
     dg[i] = make_float4(0, 0, 0, 0); db[i] = make_float4(0, 0, 0, 0); dd[i] = make_float4(0, 0, 0, 0);
   }
+  // software-pipelined rows: row rr+1's dy / x are in flight while row rr is reduced and written
+  // (one wave per row: without the prefetch each row paid a full load latency before any math)
+  const int64_t row_base = (int64_t)blockIdx.x * LN_BWD_ROWS + wave * (LN_BWD_ROWS / 4);
+  float4 nd[LN_MAXV], nx[LN_MAXV];
+  auto fetch = [&](int64_t r) {
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      const int c = lane + 64 * i;
+      if (c < nv && r < rows) {
+        nd[i] = reinterpret_cast<const float4*>(dy + r * cols)[c];
+        nx[i] = reinterpret_cast<const float4*>(x + r * cols)[c];
+      }
+    }
+  };
+  fetch(row_base);
   for (int rr = 0; rr < LN_BWD_ROWS / 4; ++rr) {
-    const int64_t row = (int64_t)blockIdx.x * LN_BWD_ROWS + wave * (LN_BWD_ROWS / 4) + rr;
+    const int64_t row = row_base + rr;
     if (row >= rows) break;
     const float mu = mean[row], rs = rstd[row];
-    const float4* xr = reinterpret_cast<const float4*>(x + row * cols);
-    const float4* dyr = reinterpret_cast<const float4*>(dy + row * cols);
+    if (!PF && rr > 0) fetch(row);
+    float4 cd[LN_MAXV], cx[LN_MAXV];
+#pragma unroll
+    for (int i = 0; i < LN_MAXV; ++i) {
+      cd[i] = nd[i];
+      cx[i] = nx[i];
+    }
+    if (PF && rr + 1 < LN_BWD_ROWS / 4) fetch(row + 1);
     float4 xh[LN_MAXV], gg[LN_MAXV];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
       const int c = lane + 64 * i;
       if (c < nv) {
-        float4 d = dyr[c];
+        float4 d = cd[i];
         if (drop_p > 0.f) {
           const uint64_t base = (uint64_t)row * cols + 4 * c;
           bool kk[4];
@@ -235,7 +269,7 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
           d.z = kk[2] ? d.z * dscale : 0.f;
           d.w = kk[3] ? d.w * dscale : 0.f;
         }
-        const float4 xv = xr[c], g = g4[c];
+        const float4 xv = cx[i], g = g4[c];
         xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
         gg[i] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
         s1 += gg[i].x + gg[i].y + gg[i].z + gg[i].w;
@@ -615,7 +649,8 @@ extern "C" int b2p_layernorm_bwd16(const float* dy, const float* x, const float*
   if (rows <= 0) return 0;
   const int nblk = (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(ln_bwd_k, dim3(nblk), dim3(256), 0, st, dy, x, gamma, mean, rstd, dx, dx_accum, workspace,
+  static const bool pf = getenv("B2P_LN_PREFETCH") ? atoi(getenv("B2P_LN_PREFETCH")) != 0 : true;
+  hipLaunchKernelGGL(pf ? ln_bwd_k<true> : ln_bwd_k<false>, dim3(nblk), dim3(256), 0, st, dy, x, gamma, mean, rstd, dx, dx_accum, workspace,
                      rows, (int)cols, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
                      drop_seed, drop_p, dx_dropped, b2p_dropout_threshold(in_drop_p),
                      in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed, d16, b2p_seed_epoch());

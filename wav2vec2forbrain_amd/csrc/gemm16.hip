@@ -699,8 +699,13 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
     launch_cfg<CfgTall>(d, ea, st, dim3((unsigned)nwg_t), tmt, tn);
     return 0;
   }
+  // 128 x 128 x 64 two-stage tiles (B2P_GEMM16_K64: 0 never = default, 1 always, -1 for grids of < 512
+  // tiles). In isolation (tools/gemm_ab.py, L2-warm repeated launches; profiles/r03s_gemm_k64_ab.txt)
+  // the N = 768 encoder shapes and the 768 x 768 split-K weight gradient ran 7-15 % faster with -1, but
+  // inside the step (cold operands, side-stream concurrency) base and Conformer steps did not move
+  // (16.46 vs 16.44 ms, 88.2 vs 88.6 ms; profiles/r03t_k64_step_ab.txt), so the default stays off.
   static int k64 = getenv("B2P_GEMM16_K64") ? atoi(getenv("B2P_GEMM16_K64")) : 0;
-  if (k64 && (ks == 1 || d.kchunk % 64 == 0)) {
+  if ((k64 == 1 || (k64 < 0 && nwg < 512)) && (ks == 1 || d.kchunk % 64 == 0)) {
     launch_cfg<CfgK64>(d, ea, st, dim3((unsigned)nwg), tm, tn);
     return 0;
   }
