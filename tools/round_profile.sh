@@ -9,6 +9,8 @@ T=$1
 O=gpurun_out/$T
 mkdir -p $O
 stop() { echo "STOP after $1 (rc=$2)"; exit $2; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || stop smoke $?
+grep smoke: $O/smoke.txt
 timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --no-conformer > $O/pmc_fetch.log 2>&1 || stop fetch $?
 timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write -o pmc -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-parity --no-conformer > $O/pmc_write.log 2>&1 || stop write $?
 python tools/traffic.py $(find $O/pmc_fetch -name "*.db" | head -1) $(find $O/pmc_write -name "*.db" | head -1) $O/gemm_traffic.json || stop traffic $?
