@@ -73,11 +73,20 @@ def _gate_aware(cls):
     @functools.wraps(bwd)
     def backward(ctx, *grads):
         with _gated(ctx.gate):
-            return bwd(ctx, *grads)
+            res = bwd(ctx, *grads)
+            if _FLUSH_PER_BLOCK:   # the block's deferred weight gradients start now, beside the next block
+                flush_wgrad()
+            return res
 
     cls.forward = staticmethod(forward)
     cls.backward = staticmethod(backward)
     return cls
+
+
+# B2P_WGRAD_FLUSH=block: the deferred frozen-weight gradient GEMMs of every encoder block go to the side
+# stream as soon as the block's backward is issued (they then overlap the rest of the backward); the
+# default ("gru") holds them until the GRU recurrence backward, whose few CUs leave the chip idle.
+_FLUSH_PER_BLOCK = os.environ.get("B2P_WGRAD_FLUSH", "gru") == "block"
 
 
 def _prec() -> int:
