@@ -16,7 +16,8 @@ import os
 import torch  # noqa: F401  (must precede loading the HIP library: shared runtime)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libb2p_hip.so")
+# B2P_LIB_PATH: load another build of the library (A/B of compile-time variants: tools/build_variant.sh)
+LIB_PATH = os.environ.get("B2P_LIB_PATH") or os.path.join(_HERE, "libb2p_hip.so")
 
 c_i64 = ctypes.c_int64
 c_i32 = ctypes.c_int32

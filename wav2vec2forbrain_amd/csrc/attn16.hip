@@ -161,7 +161,10 @@ constexpr int FWD_NT = 256;
 // 32c + 4g + i (bit i) and 32c + 16 + 4g + i (bit 4 + i): each forward lane writes its own 8 bytes.
 // Within 32-bit word (key >> 5) / 4 + 2g of the row: bit position of key
 __device__ __forceinline__ int mask_shift(int key) { return 8 * ((key >> 5) & 3) + 4 * ((key >> 4) & 1) + (key & 3); }
-constexpr int FWD_QB = 128;   // queries per workgroup
+#ifndef B2P_ATTN_QB
+#define B2P_ATTN_QB 128
+#endif
+constexpr int FWD_QB = B2P_ATTN_QB;   // queries per workgroup (forward and dQ)
 // the 4 keep bits of keys key0 .. key0+3 (key0 % 4 == 0) of mask row `row` (32-bit element index:
 // b2p_hash with idx >> 32 == 0, checked on the host)
 __device__ __forceinline__ uint32_t keep4_bits(uint32_t key_lo, uint32_t k32, uint32_t thr16) {
@@ -443,7 +446,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
   const int64_t row0 = (int64_t)b * T;
   if (b2p_gated_off(dc.gate)) {   // LayerDrop: zero dQ (the bias reduction reads it)
-    for (int half = 0; half < 2; ++half) zero_block(dqkv, dqkv16, row0, qh * FWD_QB + 64 * half, T, ld, h * DH, tid);
+    for (int half = 0; half < FWD_QB / 64; ++half) zero_block(dqkv, dqkv16, row0, qh * FWD_QB + 64 * half, T, ld, h * DH, tid);
     return;
   }
   load_image(smem, qkv, row0, T, ld, D + h * DH, tid);                        // K (as stored: S = Q K^T)
