@@ -168,8 +168,13 @@ constexpr int FWD_QB = B2P_ATTN_QB;   // queries per workgroup (forward and dQ)
 // the 4 keep bits of keys key0 .. key0+3 (key0 % 4 == 0) of mask row `row` (32-bit element index:
 // b2p_hash with idx >> 32 == 0, checked on the host)
 __device__ __forceinline__ uint32_t keep4_bits(uint32_t key_lo, uint32_t k32, uint32_t thr16) {
+#ifdef B2P_HASH_1R
+  const uint32_t h0 = b2p_mix32((key_lo >> 1) ^ k32);
+  const uint32_t h1 = b2p_mix32(((key_lo >> 1) + 1) ^ k32);
+#else
   const uint32_t h0 = b2p_mix32(b2p_mix32((key_lo >> 1) ^ k32) + k32);
   const uint32_t h1 = b2p_mix32(b2p_mix32(((key_lo >> 1) + 1) ^ k32) + k32);
+#endif
   return ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) | ((h0 >> 16) >= thr16 ? 2u : 0u) |
          ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
 }

@@ -143,7 +143,11 @@ __device__ __forceinline__ uint32_t b2p_mix32(uint32_t x) {
 }
 __device__ __forceinline__ uint32_t b2p_hash(uint64_t seed, uint64_t idx) {
   const uint32_t k = (uint32_t)seed ^ b2p_mix32((uint32_t)(seed >> 32) + 0x9E3779B9u);   // per-launch key
+#ifdef B2P_HASH_1R   // measurement variant: one mixing round (tools/build_variant.sh)
+  return b2p_mix32((uint32_t)idx ^ k ^ ((uint32_t)(idx >> 32) * 0x85EBCA6Bu));
+#else
   return b2p_mix32(b2p_mix32((uint32_t)idx ^ k) + (uint32_t)(idx >> 32) * 0x85EBCA6Bu + k);
+#endif
 }
 // keep-probability threshold: keep iff hash >= thr, thr = round(p * 2^32)
 // Graph-replayed steps: the host-drawn seed of every dropout call is offset by a device-resident
