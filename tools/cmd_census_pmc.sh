@@ -7,10 +7,10 @@ O=gpurun_out/$1; C=${2:-base}; mkdir -p $O
 export CENSUS_CONFIG=$C
 rocprofv3 -L > $O/counters_list.txt 2>&1 || true
 i=0
-for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_MFMA" "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT"; do
+for P in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS" "SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VMEM GRBM_GUI_ACTIVE GRBM_COUNT"; do
   i=$((i+1))
   timeout -s KILL 300 rocprofv3 --pmc $P -d $O/p$i -o pmc -- python3 tools/gemm_pmc_census.py run $O > $O/p$i.log 2>&1 \
-    || { echo "pass $i ($P) failed"; tail -5 $O/p$i.log; }
+    || { echo "pass $i ($P) failed"; tail -5 $O/p$i.log; find $O -name "*.db" -delete; exit 1; }
 done
 python3 tools/gemm_pmc_census.py report $O $(for k in 1 2 3 4; do find $O/p$k -name "*.db" | head -1; done) > $O/census_$C.txt 2>&1
 head -40 $O/census_$C.txt
