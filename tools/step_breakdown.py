@@ -11,7 +11,7 @@ def main():
     d, j = sys.argv[1], int(sys.argv[2])
     ntop = int(sys.argv[3]) if len(sys.argv) > 3 else 30
     ks = sorted(dispatches(d), key=lambda r: r[3])
-    ad = [i for i, k in enumerate(ks) if "adam_rec_k" in k[0]]
+    ad = [i for i, k in enumerate(ks) if "adam_rec_k" in k[0] or "adam_gated_k" in k[0]]
     ad = [a for n, a in enumerate(ad) if n == 0 or a - ad[n - 1] > 4]
     a, b = ad[j] + 1, ad[j + 1] + 1
     step = ks[a:b]
