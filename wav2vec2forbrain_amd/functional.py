@@ -140,6 +140,8 @@ def _fp32_if(name: str):
 # accumulate into p.grad in the GEMM epilogue (beta = 1) instead of autograd's separate add.
 # join_wgrad() orders the side stream back into the main stream (train step, optimizer).
 _DIAG_SKIP_ACC = os.environ.get("B2P_DIAG_SKIP_SMALL_ACC") == "1"   # diagnostic only
+# workgroups a 128 x 128 split-K GEMM aims for (the split count is capped at one slice per 1024 of K)
+_SPLITK_WGS = int(os.environ.get("B2P_SPLITK_WGS", "512"))
 _PP_SPLIT = os.environ.get("B2P_PP_SPLIT", "0") == "1"   # every eligible split-K GEMM on the ping-pong kernel
 # split-K GEMMs with at least this many outputs go to the 256 x 256 ping-pong kernel: the Conformer's
 # frozen weight gradients (4096 x 1024, 3072 x 1024; K = 7968 tokens) -8.6 ms per step; the base
@@ -479,7 +481,7 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
             # (the frozen weight gradients, K = tokens): fewer, larger tiles than the 128 x 128 split
             ks = kpp
         elif blocks < 240:
-            ks = min(-(-512 // blocks), K // 1024)
+            ks = min(-(-_SPLITK_WGS // blocks), K // 1024)
         if ks >= 2:
             q = 64 if b16 else 32
             kchunk = -(-K // ks)
