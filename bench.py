@@ -186,10 +186,10 @@ def parity_check(cfg, device, steps=2):
     """north_star parity: the CTC loss of `steps` consecutive Trainer steps vs the fp32 CPU oracle on
     identical weights and inputs, deterministic mode (dropout 0, LayerDrop 0: the reference's Philox
     masks cannot be reproduced), HipAdam lr 1e-3 over the brain encoder between steps. Two HIP runs:
-      bf16  the bench's precision. The first step (identical weights) is the north-star check (1e-3
-            relative); later steps show how far the trajectories drift apart: Adam's early updates are
-            ~lr * sign(g), so gradient entries below bf16 resolution move a parameter by a full lr in a
-            rounding-chosen direction, and the drift grows with the step count.
+      bf16  the bench's precision; every step must be within the north-star 1e-3 relative. After the
+            first update the losses are those of different weights: Adam's early updates are
+            ~lr * sign(g), so every gradient entry whose sign the rounding flips moves its parameter by
+            2 lr (tools/traj_err.py measures how much each block's rounding contributes).
       fp32  exact-fp32 MFMA mode: the same trajectory must track the oracle step by step (1e-4), which
             separates rounding drift from a wrong update.
     Returns the record and the oracle's per-step times (the Conformer's CPU baseline reuses them)."""
@@ -206,9 +206,8 @@ def parity_check(cfg, device, steps=2):
            "fp32_mode": {"hip_ctc_loss": [round(v, 6) for v in f32], "rel_err": [float(f"{r:.3e}") for r in rf],
                          "tolerance": 1e-4},
            "tolerance": 1e-3,
-           "criterion": "bf16 step 1 (identical weights) <= 1e-3 and every fp32-mode step <= 1e-4; bf16 steps "
-                        "after Adam updates reported as drift",
-           "pass": rb[0] <= 1e-3 and max(rf) <= 1e-4}
+           "criterion": "every bf16 step <= 1e-3 (north_star) and every fp32-mode step <= 1e-4",
+           "pass": max(rb) <= 1e-3 and max(rf) <= 1e-4}
     return rec, (times, threads, n_phys, model_name)
 
 
@@ -369,6 +368,7 @@ def main():
     torch.manual_seed(1234)
     from wav2vec2forbrain_amd import functional as Fn
     Fn.SEEDS.reseed(1234 * 65537 + rank)
+    Fn.LD_SEEDS.reseed(1234 * 65537 + 7919)   # device LayerDrop draws: equal on every rank
     Fn.set_precision("bf16")
     use_graph = True if args.graph is None else bool(args.graph)
 
@@ -451,7 +451,45 @@ def conformer_record(args, device):
                 f"oracle fwd+bwd+Adam (fp32, torch-CPU, {threads} threads), bs={args.bs} L={args.seq}, the 3 "
                 "deterministic parity steps (dropout / LayerDrop 0, no extrapolation)")
             rec["vs_cpu"] = round(rec["value"] / rec["cpu_baseline"]["value"], 1)
+    log("conformer_large: exact-fp32 mode steps")
+    rec["fp32_mode"] = fp32_mode_record("conformer", args, device)
+    if "cpu_baseline" in rec:
+        rec["fp32_mode"]["vs_cpu"] = round(rec["fp32_mode"]["value"] / rec["cpu_baseline"]["value"], 1)
     return rec
+
+
+def fp32_mode_record(kind, args, device, steps=3):
+    """Precision-matched throughput: the same Trainer step in the exact-fp32 MFMA mode
+    (v_mfma_f32_*_f32: fp32 operands, fp32 accumulate; the reference computes in fp32), train mode,
+    eager steps, 1 warm-up + `steps` timed. Its ratio to the CPU baseline is the precision-matched
+    GPU/CPU figure; the headline bf16 record stays the bench value."""
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.train.train_loop import Trainer
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+    cfg = make_config(args.bs, args.seq, kind)
+    model = build(cfg, device)
+    model.train()
+    for m in model.modules():
+        if hasattr(m, "sync_metrics"):
+            m.sync_metrics = False
+    with Fn.precision("fp32"):
+        trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+        trainer.use_graphs = False
+        batch = batch_on(cfg, device)
+        trainer.train_step(batch)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            out = trainer.train_step(batch)
+        torch.cuda.synchronize()
+        dt = time.perf_counter() - t0
+        loss = float(out.loss)
+    Fn.set_deferred_wgrad([])
+    del trainer, model, batch
+    free_device()
+    return {"value": round(steps / dt, 4), "unit": "steps/s", "ms_per_step": round(dt / steps * 1e3, 2),
+            "steps": steps, "warmup": 1, "dtype": "fp32 (exact-fp32 MFMA, the reference's arithmetic)",
+            "step_mode": "eager Trainer.train_step", "ctc_loss": round(loss, 5)}
 
 
 def gemm_traffic(kind="base"):

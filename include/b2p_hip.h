@@ -227,6 +227,24 @@ int b2p_day_reduce(const float* per_sample, const int64_t* day_idx, int64_t B, i
  * mode's GRU layer-0 projection and weight-gradient operand. */
 int b2p_unfold16(const float* x, uint16_t* U, int64_t B, int64_t L, int64_t C, int64_t k,
                  int64_t stride, b2p_stream_t stream);
+/* Implicit-Unfold operands (L % s == 0, k % s == 0; functional._GRULayer): the Unfold of x (B, L, C)
+ * is the overlapping-row view of a 16-bit copy of x (row stride s*C), never materialised; the input
+ * gradient of the layer-0 projection is one GEMM over the overlapping-row view of the padded dgi
+ * (b2p_pad_rows16) and the weight copy wb, with no (B*T, k*C) intermediate or col2im.
+ * Replaces nn.Unfold((k,1), stride) + nn.GRU's layer-0 input projection (src/model/b2p2t_model.py:
+ * 108-113, 162-167; src/model/brain_feature_extractor.py:39-47, 61-65) and their autograd.
+ *  b2p_unfold_weight16: rows of w0 (G x C*k, reference layout [n][c*k + tap]) then w1 (may be NULL):
+ *    wf[n][tap*C + c] (fp16 when fp16 = 1, else bf16; forward B operand) and, when wb != NULL,
+ *    wb[j*Ntot + n][r*C + c] = bf16(w[n][c*k + s*(k/s-1-j) + r]), j < k/s, Ntot = rows of w0 + w1.
+ *  b2p_pad_rows16: dst (lead + B*R rows of N) bf16: row lead + b*R + t = src[b][t] (src (B, T, N)
+ *    fp32) for t < T, all other rows 0.
+ *  b2p_cast16_tail: y[i] = 16-bit(x[i]) for i < n, 0 up to n_total (the tail an overlapping-row view
+ *    reads past the last sample). */
+int b2p_unfold_weight16(const float* w0, const float* w1, int64_t G, int64_t C, int64_t k, int64_t stride,
+                        uint16_t* wf, int fp16, uint16_t* wb, b2p_stream_t stream);
+int b2p_pad_rows16(const float* src, uint16_t* dst, int64_t B, int64_t T, int64_t N, int64_t R, int64_t lead,
+                   b2p_stream_t stream);
+int b2p_cast16_tail(const float* x, uint16_t* y, int64_t n, int64_t n_total, int fp16, b2p_stream_t stream);
 /* out[o][tap*I + i] = in[o][i*ntaps + tap]   (conv weight (O, I, taps) -> tap-major GEMM B)
  * inverse=1 does the opposite mapping; flip=1 reads tap (ntaps-1-tap). */
 int b2p_conv_weight_permute(const float* in, float* out, int64_t O, int64_t I, int64_t ntaps,

@@ -137,19 +137,25 @@ def test_gru_layer(unfold, h0, B, H):
 @pytest.mark.parametrize("H,B,T,h0,unfold", [(32, 3, 17, True, False), (64, 5, 23, True, False), (128, 20, 40, False, False),
                                                (256, 33, 57, True, False), (256, 32, 249, False, True),
                                                (384, 20, 40, True, False), (512, 33, 57, True, False),
-                                               (512, 32, 249, False, True)])
-def test_gru_layer_bf16_persistent(H, B, T, h0, unfold):
+                                               (512, 32, 249, False, True), (256, 5, 57, True, "ragged"),
+                                               (512, 7, 30, False, "ragged")])
+@pytest.mark.parametrize("f16", [False, True])
+def test_gru_layer_bf16_persistent(H, B, T, h0, unfold, f16):
     """bf16 mode: the persistent MFMA recurrences — one CU per (direction, 16 rows) for H <= 256
     (csrc/gru16.hip), H/64 CUs exchanging the state through L2 for H = 384 / 512 (csrc/grumc.hip,
-    the Conformer encoder's H = 512) — vs the fp32 oracle GRU (nn.GRU semantics). bf16 MFMA operands
-    (W_hh, h) -> relative L2 tolerance 2e-2 on outputs and every gradient; B not a multiple of the
-    16-row tile; both directions; optional h0."""
+    the Conformer encoder's H = 512) — vs the fp32 oracle GRU (nn.GRU semantics). 16-bit MFMA
+    operands -> relative L2 tolerance 2e-2 on outputs and every gradient; B not a multiple of the
+    16-row tile; both directions; optional h0. unfold: layer 0 over the implicit Unfold view (L a
+    multiple of the stride: overlapping-row GEMM operands, no col2im) or, "ragged", over an L that is
+    not (the materialised fallback). f16: the forward under Fn.forward_f16 (fp16 projection operands,
+    as the models run their brain encoder) — the outputs then within 4e-3 (the recurrence's fp16
+    operands: 3 more significant bits than bf16)."""
     Fn = _fn()
     from oracle.b2p2t_oracle import gru_direction, unfold as unfold_ref
     torch.manual_seed(11)
     if unfold:
         C, k, s = 16, 32, 4
-        L = (T - 1) * s + k
+        L = (T - 1) * s + k + (2 if unfold == "ragged" else 0)
         xsrc = torch.randn(B, L, C)
         x_ref_fn = lambda x: unfold_ref(x, k, s)
     else:
@@ -174,8 +180,9 @@ def test_gru_layer_bf16_persistent(H, B, T, h0, unfold):
         xs = xsrc.cuda().requires_grad_(True)
         x_in = Fn.Unfolded(xs, k, s) if unfold else xs
         hg = hz.cuda().requires_grad_(True) if h0 else None
-        out = Fn.gru_layer(x_in, H, 2, wg, hg)
-        assert _rel(out.detach().cpu(), ref.detach()) < 2e-2
+        with Fn.forward_f16(f16):
+            out = Fn.gru_layer(x_in, H, 2, wg, hg)
+        assert _rel(out.detach().cpu(), ref.detach()) < (4e-3 if f16 else 2e-2)
         got = torch.autograd.grad(out, [xs, *wg] + ([hg] if h0 else []), dout.cuda())
     for i, (a, b) in enumerate(zip(got, refg)):
         assert _rel(a.cpu(), b) < 3e-2, i

@@ -57,6 +57,7 @@ def test_captured_layerdrop_redraws_per_replay(name):
     cfg = CFG[name]
     nl = cfg["layers"]
     Fn.SEEDS.reseed(1234)
+    Fn.LD_SEEDS.reseed(1234)
 
     # ---- captured step, replayed
     model = _model(name)
@@ -132,6 +133,7 @@ def test_captured_layerdrop_adam_leaves_dropped_layers(name):
     from wav2vec2forbrain_amd.train.step_graph import StepGraph
     cfg = CFG[name]
     Fn.SEEDS.reseed(4321)
+    Fn.LD_SEEDS.reseed(4321)
     model = _model(name)
     batch = _batch(cfg)
     opt = HipAdam(model.parameters(), lr=1e-2, weight_decay=1e-2)

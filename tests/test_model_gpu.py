@@ -309,3 +309,36 @@ def test_conformer_fp16_operands_at_large_magnitudes(gain, exact):
         with torch.no_grad():
             ref = float(conformer_forward_loss(sd, b, oracle_cfg(cfg), training=True))
         assert abs(got - ref) <= LOSS_RTOL_BF16 * abs(ref), (got, ref)
+
+
+@pytest.mark.parametrize("name", ["conformer_large_bs32", "base_bs32"])
+def test_brain_encoder_gradients_bf16(name):
+    """The gradients Adam consumes under unfreeze_strategy=brain_encoder (the bench's config): every
+    brain_encoder.* gradient of one bf16 step vs the reference's (sampled entries of the golden
+    fixture), relative L2 per tensor, plus the agreement of signs weighted by magnitude — Adam's first
+    update is ~lr * sign(g), so sum(|g_ref| [sign(g) != sign(g_ref)]) / sum(|g_ref|) is the share of the
+    reference's first-order descent that a sign flip gives away. Measured (round 4, fp16 brain encoder
+    forward, bf16 backward): relative L2 ~1.3e-2 on every tensor (the error enters with the encoder's
+    input gradient, so it is the same for all of them), lost descent ~1e-4."""
+    fx = load_fixture(name)
+    model, out = _run(name, "bf16")
+    params = dict(model.named_parameters())
+    worst, lost_n, lost_d = 0.0, 0.0, 0.0
+    rows = []
+    for n in fx["param_names"]:
+        if not n.startswith("brain_encoder.") or float(fx["gnorm/" + n]) == 0.0:
+            continue
+        g = params[n].grad
+        r = fx["gval/" + n] if "gval/" + n in fx else fx["grad/" + n].reshape(-1)
+        idx = fx["gidx/" + n] if "gidx/" + n in fx else np.arange(r.size)
+        v = g.reshape(-1)[torch.from_numpy(idx).cuda()].cpu().numpy()
+        e = float(np.linalg.norm(v - r) / np.linalg.norm(r))
+        worst = max(worst, e)
+        lost_n += float(np.abs(r)[np.sign(v) != np.sign(r)].sum())
+        lost_d += float(np.abs(r).sum())
+        rows.append((e, n))
+    rows.sort(reverse=True)
+    print(f"{name}: worst brain_encoder gradient rel L2 {worst:.3e} ({rows[0][1]}); sign-lost descent "
+          f"{lost_n / lost_d:.2e}; " + ", ".join(f"{n.split('.')[-1]} {e:.2e}" for e, n in rows[:6]))
+    assert worst <= 3e-2, rows[:4]
+    assert lost_n / lost_d <= 1e-3

@@ -27,6 +27,25 @@ __device__ __forceinline__ uint2 b2p_pack16x4(float4 v, bool half) {
   return make_uint2((uint32_t)b2p_16_bits(v.x, half) | ((uint32_t)b2p_16_bits(v.y, half) << 16),
                     (uint32_t)b2p_16_bits(v.z, half) | ((uint32_t)b2p_16_bits(v.w, half) << 16));
 }
+// 8 fp16 values in a 16-bit container vector (the data movement is the same as bf16's) and the fp16
+// MFMA on such containers: the GRU forward recurrences (gru16 / grumc) keep W_hh and h in fp16 —
+// both are bounded (|h| < 1, W_hh ~ U(-1/sqrt(H), 1/sqrt(H))) and get 3 more significant bits
+typedef _Float16 b2p_f16x8 __attribute__((ext_vector_type(8)));
+__device__ __forceinline__ bf16x8 b2p_pack8_f16(const float* p) {
+  const float4 a = *reinterpret_cast<const float4*>(p);
+  const float4 b = *reinterpret_cast<const float4*>(p + 4);
+  const b2p_f16x8 r = {(_Float16)a.x, (_Float16)a.y, (_Float16)a.z, (_Float16)a.w,
+                       (_Float16)b.x, (_Float16)b.y, (_Float16)b.z, (_Float16)b.w};
+  return __builtin_bit_cast(bf16x8, r);
+}
+__device__ __forceinline__ f32x4 b2p_mfma_f16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(b2p_f16x8, a), __builtin_bit_cast(b2p_f16x8, b), c,
+                                                0, 0, 0);
+}
+__device__ __forceinline__ uint2 b2p_pack_f16x4(float4 v) {
+  return make_uint2((uint32_t)b2p_f16_bits(v.x) | ((uint32_t)b2p_f16_bits(v.y) << 16),
+                    (uint32_t)b2p_f16_bits(v.z) | ((uint32_t)b2p_f16_bits(v.w) << 16));
+}
 __device__ __forceinline__ float b2p_bf16_to_f32(uint16_t b) {
   return __builtin_bit_cast(float, (uint32_t)b << 16);
 }

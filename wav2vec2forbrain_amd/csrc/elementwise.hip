@@ -794,6 +794,116 @@ extern "C" int b2p_unfold16(const float* x, uint16_t* u, int64_t B, int64_t L, i
   return 0;
 }
 
+// ------------------------------------------------------------------ implicit Unfold operands
+// The Unfold((k,1), stride s) of a (B, L, C) tensor with L % s == 0 and k % s == 0 is never
+// materialised: its row (b, t) is the contiguous slab x[b][s*t .. s*t+k)[.], i.e. row b*(L/s) + t of
+// the flat tensor read with row stride s*C (overlapping rows). Three GEMMs use that view
+// (functional._GRULayer): the layer-0 projection gi = U W^T, its weight gradient dW = dgi^T U, and
+// the input gradient, computed without the (B*T, k*C) fp32 matrix and its col2im as
+//   dX viewed (B*L/s, s*C) = G (B*L/s, (k/s)*N) . Wb ((k/s)*N, s*C),
+//   G row (b, q) = dgi rows t = q-k/s+1 .. q of sample b (zero outside [0, T)),
+//   Wb[j*N + n][r*C + c] = W[n][c*k + s*(k/s-1-j) + r].
+// G is the overlapping-row view (row stride N) of dgi laid out with k/s-1 zero rows in front and
+// L/s rows per sample (rows t >= T zero): b2p_pad_rows16 writes that layout.
+
+// One workgroup per weight row n of W (reference layout [n][c*k + tap]): the row is transposed
+// through LDS (row stride k+1: conflict-free tap-major reads); writes wf[n][tap*C + c] (16-bit,
+// fp16 when half) and, when wb != NULL, the k/s rows wb[j*Ntot + n][.] (bf16).
+__global__ void __launch_bounds__(256) unfold_weight16_k(const float* __restrict__ w0, const float* __restrict__ w1,
+                                                         int64_t G, int C, int k, int s, uint16_t* __restrict__ wf,
+                                                         int half, uint16_t* __restrict__ wb, int64_t Ntot) {
+  extern __shared__ float tile[];   // C * (k + 1)
+  const int64_t n = blockIdx.x;
+  const int CK = C * k;
+  const float* src = n < G ? w0 + n * CK : w1 + (n - G) * CK;
+  for (int t = threadIdx.x; t < CK; t += 256) {
+    const int c = t / k, tap = t - c * k;
+    tile[c * (k + 1) + tap] = src[t];
+  }
+  __syncthreads();
+  const int C4 = C / 4;
+  for (int e4 = threadIdx.x; e4 < CK / 4; e4 += 256) {   // 4 consecutive channels of one tap
+    const int tap = e4 / C4, c = 4 * (e4 - tap * C4);
+    const float* tp = tile + c * (k + 1) + tap;
+    const float4 v = make_float4(tp[0], tp[k + 1], tp[2 * (k + 1)], tp[3 * (k + 1)]);
+    reinterpret_cast<uint2*>(wf + n * CK)[e4] = b2p_pack16x4(v, half != 0);
+  }
+  if (!wb) return;
+  const int J = k / s, SC = s * C;
+  for (int e4 = threadIdx.x; e4 < CK / 4; e4 += 256) {
+    const int e = 4 * e4;
+    const int j = e / SC, rc = e - j * SC;
+    const int r = rc / C, c = rc - r * C;
+    const int tap = s * (J - 1 - j) + r;
+    const float* tp = tile + c * (k + 1) + tap;
+    const float4 v = make_float4(tp[0], tp[k + 1], tp[2 * (k + 1)], tp[3 * (k + 1)]);
+    *reinterpret_cast<uint2*>(wb + ((int64_t)j * Ntot + n) * SC + rc) = b2p_pack_bf16x4(v);
+  }
+}
+
+extern "C" int b2p_unfold_weight16(const float* w0, const float* w1, int64_t G, int64_t C, int64_t k, int64_t stride,
+                                   uint16_t* wf, int fp16, uint16_t* wb, b2p_stream_t stream) {
+  B2P_CHECK_ARG(w0 && wf, "unfold_weight16: NULL pointer");
+  B2P_CHECK_ARG(C % 4 == 0 && k > 0 && stride > 0 && k % stride == 0, "unfold_weight16: bad geometry");
+  B2P_CHECK_ARG(((uintptr_t)wf & 7u) == 0 && ((uintptr_t)wb & 7u) == 0, "unfold_weight16: alignment");
+  const size_t lds = (size_t)C * (k + 1) * sizeof(float);
+  B2P_CHECK_ARG(lds <= 64 * 1024, "unfold_weight16: C * (k + 1) floats must fit 64 KB of LDS");
+  const int64_t Ntot = w1 ? 2 * G : G;
+  if (G <= 0) return 0;
+  hipLaunchKernelGGL(unfold_weight16_k, dim3((unsigned)Ntot), dim3(256), lds, (hipStream_t)stream, w0, w1, G, (int)C,
+                     (int)k, (int)stride, wf, fp16, wb, Ntot);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+// dst row (lead + b*R + t) = bf16(src[b][t]) for t < T, every other row (the lead rows, t >= T) zero
+__global__ void pad_rows16_k(const float* __restrict__ src, uint16_t* __restrict__ dst, int64_t T, int64_t R,
+                             int64_t lead, int64_t N4, int64_t total4) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total4) return;
+  const int64_t row = i / N4, c4 = i - row * N4;
+  uint2 v = make_uint2(0u, 0u);
+  if (row >= lead) {
+    const int64_t rr = row - lead, b = rr / R, t = rr - b * R;
+    if (t < T) v = b2p_pack_bf16x4(reinterpret_cast<const float4*>(src + (b * T + t) * N4 * 4)[c4]);
+  }
+  reinterpret_cast<uint2*>(dst)[i] = v;
+}
+
+extern "C" int b2p_pad_rows16(const float* src, uint16_t* dst, int64_t B, int64_t T, int64_t N, int64_t R,
+                              int64_t lead, b2p_stream_t stream) {
+  B2P_CHECK_ARG(src && dst, "pad_rows16: NULL pointer");
+  B2P_CHECK_ARG(N % 4 == 0 && R >= T && lead >= 0, "pad_rows16: bad geometry");
+  B2P_CHECK_ARG(((uintptr_t)src & 15u) == 0 && ((uintptr_t)dst & 7u) == 0, "pad_rows16: alignment");
+  const int64_t total4 = (lead + B * R) * (N / 4);
+  if (total4 <= 0) return 0;
+  hipLaunchKernelGGL(pad_rows16_k, dim3(nblocks(total4)), dim3(256), 0, (hipStream_t)stream, src, dst, T, R, lead,
+                     N / 4, total4);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+// y[i] = 16-bit(x[i]) for i < n, 0 for n <= i < n_total (the zero tail an overlapping-row view reads)
+__global__ void cast16_tail_k(const float* __restrict__ x, uint16_t* __restrict__ y, int64_t n4, int64_t total4,
+                              int half) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= total4) return;
+  reinterpret_cast<uint2*>(y)[i] = i < n4 ? b2p_pack16x4(reinterpret_cast<const float4*>(x)[i], half != 0)
+                                          : make_uint2(0u, 0u);
+}
+
+extern "C" int b2p_cast16_tail(const float* x, uint16_t* y, int64_t n, int64_t n_total, int fp16,
+                               b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && y, "cast16_tail: NULL pointer");
+  B2P_CHECK_ARG(n % 4 == 0 && n_total % 4 == 0 && n_total >= n, "cast16_tail: sizes must be multiples of 4");
+  B2P_CHECK_ARG(((uintptr_t)x & 15u) == 0 && ((uintptr_t)y & 7u) == 0, "cast16_tail: alignment");
+  if (n_total <= 0) return 0;
+  hipLaunchKernelGGL(cast16_tail_k, dim3(nblocks(n_total / 4)), dim3(256), 0, (hipStream_t)stream, x, y, n / 4,
+                     n_total / 4, fp16);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int b2p_softmax_fwd(const float* S, float* P, float* Pd, int64_t rows, int64_t n, int64_t ld,
                                float drop_p, uint64_t drop_seed, b2p_stream_t stream) {
   B2P_CHECK_ARG(S && P && Pd, "softmax_fwd: NULL pointer");

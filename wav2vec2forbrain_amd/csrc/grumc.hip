@@ -4,9 +4,10 @@
 //
 // One launch runs the whole time loop. A recurrence (direction d, 16 batch rows) is spread over
 // P = H/64 workgroups ("members"), one per CU: member m owns hidden units [64m, 64m+64) and keeps
-// their W_hh rows (r, z, n: 192 x H bf16) in registers as MFMA A-fragments for the whole launch, so
-// W_hh is read from HBM once per launch instead of once per step. Per step the members exchange
-// the new state through L2 as tagged 8-byte granules ({tag = step+1, two bf16}: written by one sc1
+// their W_hh rows (r, z, n: 192 x H; fp16 in the forward, bf16 in the backward) in registers as MFMA
+// A-fragments for the whole launch, so W_hh is read from HBM once per launch instead of once per
+// step. Per step the members exchange the new state through L2 as tagged 8-byte granules ({tag =
+// step+1, two fp16 h values / three bf16 dgh values}: written by one sc1
 // store, polled by sc1 loads until every tag matches; MI355X_MICROARCH.md 'Workgroup dispatch, XCD
 // placement & inter-workgroup visibility', cdna_hip_programming.md Guideline 16 R2) — no fences,
 // no flags, no grid barrier. The exchange slots are zeroed by a memset before every launch (so tags
@@ -51,11 +52,8 @@ __device__ __forceinline__ unsigned long long get_granule(const unsigned long lo
 __device__ __forceinline__ unsigned pack2(float a, float b) {
   return (unsigned)b2p_bf16_bits(a) | ((unsigned)b2p_bf16_bits(b) << 16);
 }
-__device__ __forceinline__ bf16x8 pack8(const float* p) {
-  const float4 a = *reinterpret_cast<const float4*>(p);
-  const float4 b = *reinterpret_cast<const float4*>(p + 4);
-  bf16x8 r = {(__bf16)a.x, (__bf16)a.y, (__bf16)a.z, (__bf16)a.w, (__bf16)b.x, (__bf16)b.y, (__bf16)b.z, (__bf16)b.w};
-  return r;
+__device__ __forceinline__ unsigned pack2h(float a, float b) {
+  return (unsigned)b2p_f16_bits(a) | ((unsigned)b2p_f16_bits(b) << 16);
 }
 __device__ __forceinline__ bf16x8 pack8_strided(const float* p, int64_t stride) {
   bf16x8 r;
@@ -167,7 +165,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
   constexpr int NGR = P * 512 / NTH;          // granules swept per lane
   constexpr int G3 = 3 * H;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  unsigned* hw = reinterpret_cast<unsigned*>(smem);   // [2][BG][HPW] u32 (bf16 pairs)
+  unsigned* hw = reinterpret_cast<unsigned*>(smem);   // [2][BG][HPW] u32 (fp16 pairs)
 
   int d, bg, m;
   if (!place(P, ndir * nbg, d, bg, m, nbg)) return;
@@ -185,7 +183,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
 #pragma unroll
   for (int g = 0; g < 3; ++g)
 #pragma unroll
-    for (int s = 0; s < KS; ++s) wf[g][s] = pack8(W + (int64_t)(g * H + u0 + lr) * H + 32 * s + 8 * lq);
+    for (int s = 0; s < KS; ++s) wf[g][s] = b2p_pack8_f16(W + (int64_t)(g * H + u0 + lr) * H + 32 * s + 8 * lq);
   float4 bh[3];
 #pragma unroll
   for (int g = 0; g < 3; ++g)
@@ -201,7 +199,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
       a = h0[((int64_t)d * B + bb) * H + 2 * c];
       c2 = h0[((int64_t)d * B + bb) * H + 2 * c + 1];
     }
-    hw[r * HPW + c] = pack2(a, c2);
+    hw[r * HPW + c] = pack2h(a, c2);
   }
   if (h0 && bok) {
     const float4 v = *reinterpret_cast<const float4*>(h0 + ((int64_t)d * B + b) * H + j0);
@@ -256,7 +254,7 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
     for (int ks = 0; ks < KS; ++ks) {
       const bf16x8 bf = *reinterpret_cast<const bf16x8*>(hrow + 16 * ks);
 #pragma unroll
-      for (int q = 0; q < 3; ++q) acc[q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wf[q][ks], bf, acc[q], 0, 0, 0);
+      for (int q = 0; q < 3; ++q) acc[q] = b2p_mfma_f16(wf[q][ks], bf, acc[q]);
     }
     const float gnv[4] = {g[2].x, g[2].y, g[2].z, g[2].w};
     float hh[4];
@@ -273,12 +271,12 @@ __global__ void __launch_bounds__(NTH, 1) grumc_fwd(const float* __restrict__ gi
       st_n[i] = nn;
       st_g[i] = acc[2][i];
     }
-    // publish h_s (bf16 pairs) FIRST: the other members wait on it, and a later store or load issued
+    // publish h_s (fp16 pairs) FIRST: the other members wait on it, and a later store or load issued
     // before it would delay it; then this step's outputs and the next step's input projection
     if (s + 1 < T && m != withhold) {   // withhold: test knob (b2p_gru_mc_debug_withhold), -1 = off
       unsigned long long* dst = xg + (s & 1) * P * 512 + m * 512 + lr * 32 + w * 8 + lq * 2;
-      put_granule(dst, (unsigned)(s + 1), pack2(hh[0], hh[1]), local);
-      put_granule(dst + 1, (unsigned)(s + 1), pack2(hh[2], hh[3]), local);
+      put_granule(dst, (unsigned)(s + 1), pack2h(hh[0], hh[1]), local);
+      put_granule(dst + 1, (unsigned)(s + 1), pack2h(hh[2], hh[3]), local);
     }
     store_out(s);
     if (s + 1 < T) load_gi(s + 1, gc);

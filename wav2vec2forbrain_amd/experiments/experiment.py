@@ -57,9 +57,11 @@ class Experiment(metaclass=ABCMeta):
         # the host torch seed stays equal on every rank (identical initial weights, identical host
         # LayerDrop draws in eager steps); the dropout masks and the device LayerDrop draws of captured
         # steps come from the functional seed stream, offset by the rank so that the ranks' halves of a
-        # global batch draw independent masks, as one process would over its rows
+        # global batch draw independent masks, as one process would over its rows;
+        # the device LayerDrop draws come from a stream without the offset (every rank skips alike)
         from .. import functional as Fn
         Fn.SEEDS.reseed(self.base_config.seed * 65537 + self.rank)
+        Fn.LD_SEEDS.reseed(self.base_config.seed * 65537 + 7919)   # rank-independent (device LayerDrop)
 
         self.dataloader_train = self._create_dataloader(split="train")
         self.dataloader_val = self._create_dataloader(split="val")

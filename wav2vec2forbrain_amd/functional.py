@@ -39,6 +39,7 @@ class _State:
     nosplit = False  # no split-K (deferred weight gradients issued on concurrent side streams)
     sync_bn = None   # process group for synchronised BatchNorm statistics (sync_batchnorm())
     gate = None      # LayerDrop gate (device int32) of the layer being issued in a captured step
+    block = None     # error attribution: the B2P_FP32_OPS block whose forward is being issued
 
 
 _state = _State()
@@ -126,10 +127,42 @@ _FP32_OPS = set(filter(None, os.environ.get("B2P_FP32_OPS", "").split(",")))
 @contextlib.contextmanager
 def _fp32_if(name: str):
     if name in _FP32_OPS:
-        with precision("fp32"):
-            yield
+        old = _state.block
+        _state.block = name
+        try:
+            with precision("fp32"):
+                yield
+        finally:
+            _state.block = old
     else:
         yield
+
+
+# error attribution (tools/traj_err.py): with B2P_FP32_BWD=1 a block's backward runs in the precision
+# its forward ran in, so B2P_FP32_OPS=<block> puts that block's forward AND backward in exact fp32
+_BWD_FOLLOWS_FWD = [os.environ.get("B2P_FP32_BWD", "0") == "1"]
+_FP32_BWD_OPS: set = set()   # blocks whose backward follows their forward's precision regardless
+
+
+def _prec_follow(cls):
+    fwd, bwd = cls.forward, cls.backward
+
+    @functools.wraps(fwd)
+    def forward(ctx, *args):
+        ctx.prec_fwd = _state.prec
+        ctx.block = _state.block
+        return fwd(ctx, *args)
+
+    @functools.wraps(bwd)
+    def backward(ctx, *grads):
+        if (_BWD_FOLLOWS_FWD[0] or ctx.block in _FP32_BWD_OPS) and ctx.prec_fwd != _state.prec:
+            with precision({0: "bf16", 1: "fp32"}[ctx.prec_fwd]):
+                return bwd(ctx, *grads)
+        return bwd(ctx, *grads)
+
+    cls.forward = staticmethod(forward)
+    cls.backward = staticmethod(backward)
+    return cls
 
 
 # -------------------------------------------------------------------------------------------
@@ -372,6 +405,10 @@ class _SeedStream:
 
 
 SEEDS = _SeedStream()
+# the device LayerDrop draws of captured steps: a stream of its own that is NOT offset by the rank (the
+# reference skips a layer for the whole batch, and every rank's host draw in eager steps comes from
+# the equal host torch seed), so replayed data-parallel steps drop the same layers on every rank
+LD_SEEDS = _SeedStream()
 
 
 def _chk(t: torch.Tensor, name: str) -> None:
@@ -813,6 +850,7 @@ def _ln_bwd16(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0,
 # =====================================================================================
 # front end: GaussianSmoothing -> day linear (+bias) -> softsign
 # =====================================================================================
+@_prec_follow
 class _FrontEnd(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, day_idxs, day_weights, day_bias, taps):
@@ -855,7 +893,8 @@ class _FrontEnd(torch.autograd.Function):
 def front_end(x, day_idxs, day_weights, day_bias, taps):
     """b2p2t_model.py:150-159: permute -> GaussianSmoothing -> einsum(btd,bdk) + day_bias -> Softsign.
     Returns the (B, L, 256) softsign output (the Unfold is implicit in the GRU layer-0 projection)."""
-    return _FrontEnd.apply(x.contiguous(), day_idxs.to(torch.int64).contiguous(), day_weights, day_bias, taps)
+    with _fp32_if("front"):
+        return _FrontEnd.apply(x.contiguous(), day_idxs.to(torch.int64).contiguous(), day_weights, day_bias, taps)
 
 
 # =====================================================================================
@@ -882,11 +921,17 @@ class Unfolded:
         return win.permute(0, 1, 3, 2).reshape(B, self.T, C * self.kernel)
 
 
+# bf16 mode's GRU layer 0 reads the Unfold through an implicit overlapping-row view (B2P_UNFOLD_IMPLICIT=0:
+# the materialised bf16 unfold + col2im of round 3, for A/B checks)
+_UNFOLD_IMPLICIT = [os.environ.get("B2P_UNFOLD_IMPLICIT", "1") != "0"]
 # persistent MFMA recurrence in bf16 mode (B2P_GRU16=0 selects the per-step fp32 kernels, for A/B checks)
 _GRU16 = [os.environ.get("B2P_GRU16", "1") != "0"]
 # hidden sizes one CU cannot hold (Conformer H = 512): the multi-CU persistent kernels (csrc/grumc.hip)
 # in bf16 mode (B2P_GRUMC=0: per-step kernels, for A/B checks)
 _GRUMC = [os.environ.get("B2P_GRUMC", "1") != "0"]
+# diagnostic (tools/traj_err.py): None = the backward follows the forward's choice; True / False force
+# the multi-CU / per-step fp32 backward recurrence (same saved layout)
+_GRUMC_BWD = [None]
 
 
 def _gru_mc_ws(B, H, ndir, dev):
@@ -965,6 +1010,7 @@ def _stack2(a, b):
     return a.unsqueeze(0) if b is None else torch.stack([a, b], 0)
 
 
+@_prec_follow
 class _GRULayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, unf_meta, H, ndir, h0, *weights):
@@ -992,21 +1038,44 @@ class _GRULayer(torch.autograd.Function):
         if use16 and bhh[0] is not None:
             bih = [(b if b is not None else torch.zeros(G3, device=dev))
                    + torch.cat([bh[:2 * H], torch.zeros(H, device=dev)]) for b, bh in zip(bih, bhh)]
-        if unf_meta is not None:
+        implicit = (unf_meta is not None and bf16_mode() and L % stride == 0 and ktaps % stride == 0 and C % 4 == 0
+                    and _UNFOLD_IMPLICIT[0])
+        if implicit:
+            # implicit Unfold (csrc/elementwise.hip "implicit Unfold operands"): the GEMM reads a 16-bit copy
+            # of x through an overlapping-row view (row stride stride*C); fp16 operands under forward_f16
+            half = _state.fwd16
+            N3 = ndir * G3
+            wf = torch.empty(N3, IN, device=dev, dtype=torch.float16 if half else BF16)
+            # the backward-data operand of the same weights, written in the same pass when needed
+            wperm = (torch.empty((ktaps // stride) * N3, stride * C, device=dev, dtype=BF16)
+                     if ctx.needs_input_grad[0] else None)
+            _lib.call("b2p_unfold_weight16", _p(wih[0]), _p(wih[1]) if ndir == 2 else None, G3, C, ktaps, stride,
+                      _p(wf), int(half), _p(wperm), _st())
+            n_s, tail = B * L * C, (ktaps - stride) * C
+            s16 = torch.empty(n_s + tail, device=dev, dtype=torch.float16 if half else BF16)
+            _lib.call("b2p_cast16_tail", _p(x), _p(s16), n_s, n_s + tail, int(half), _st())
+            bias_cat = torch.cat([b if b is not None else torch.zeros(G3, device=dev) for b in bih]) \
+                if any(b is not None for b in bih) else None
+            gemm(T, N3, IN, op(s16, 0, stride * C, True, bs1=L * C), op(wf, 0, IN, True), gi, N3, cbs1=T * N3, nz1=B,
+                 bias=bias_cat)
+            del wf
+            U16 = None if half else s16    # the bf16 copy doubles as the weight-gradient operand
+            del s16
+        elif unf_meta is not None:
             # tap-major weight copy: W'[n][tap*C + c] = W[n][c*k + tap] for both directions
             wperm = torch.empty(ndir * G3, IN, device=dev)
             for d in range(ndir):
                 _lib.call("b2p_conv_weight_permute", _p(wih[d]), _p(wperm, d * G3 * IN), G3, C, ktaps, 0, _st())
             bias_cat = torch.cat([b if b is not None else torch.zeros(G3, device=dev) for b in bih]) \
                 if any(b is not None for b in bih) else None
-            if bf16_mode():
+            if bf16_mode() and not _state.fwd16:
                 # bf16 operands: the tap-major unfold materialised once in bf16 (it is also the
                 # weight-gradient operand) and a bf16 copy of the permuted weight
                 U16 = torch.empty(B * T, IN, device=dev, dtype=BF16)
                 _lib.call("b2p_unfold16", _p(x), _p(U16), B, L, C, ktaps, stride, _st())
                 wperm = cast16(wperm)
                 gemm(B * T, ndir * G3, IN, op(U16, 0, IN, True), op(wperm, 0, IN, True), gi, ndir * G3, bias=bias_cat)
-            else:
+            else:   # fp32 mode, or fp16 operands (forward_f16): the fp32-operand kernel rounds while staging
                 U16 = None
                 A = conv_op(x, 0, C, T, L, stride, 0, C * ktaps, L * C, True)
                 A.conv_Cg = C  # inner j = tap*C + c
@@ -1046,6 +1115,7 @@ class _GRULayer(torch.autograd.Function):
                       _st())
         ctx.save_for_backward(x, out, saved, whh_s, h0, wperm, hL, U16, *wih)
         ctx.meta = (unf_meta, H, ndir, B, T, IN, bih[0] is not None, bhh[0] is not None, use16, usemc)
+        ctx.implicit = unf_meta is not None and implicit
         ctx.whh0 = whh[0]
         return out
 
@@ -1053,6 +1123,8 @@ class _GRULayer(torch.autograd.Function):
     def backward(ctx, dout):
         x, out, saved, whh_s, h0, wperm, hL, U16, *wih = ctx.saved_tensors
         unf_meta, H, ndir, B, T, IN, has_bih, has_bhh, use16, usemc = ctx.meta
+        if not use16 and _GRUMC_BWD[0] is not None:
+            usemc = _GRUMC_BWD[0] and bool(_lib.load().b2p_gru_mc_supported(H))
         dev = out.device
         dout = dout.contiguous()
         G3 = 3 * H
@@ -1106,7 +1178,33 @@ class _GRULayer(torch.autograd.Function):
                 colsum(_view_off(dgi, d * G3), B * T, G3, db, ld=ndir * G3)
                 grads[4 * d + 2] = db
         dx = None
-        if unf_meta is not None:
+        if ctx.implicit:
+            # dgi in the padded row layout (k/s - 1 zero rows in front, L/s rows per sample, rows t >= T
+            # zero): the weight gradient reads it as the k-major A operand, the input gradient as the
+            # overlapping-row view (one GEMM straight into dx, no col2im)
+            ktaps, stride = unf_meta
+            _, L, C = x.shape
+            R, lead, N3 = L // stride, ktaps // stride - 1, ndir * G3
+            dgp = torch.empty((lead + B * R) * N3, device=dev, dtype=BF16)
+            _lib.call("b2p_pad_rows16", _p(dgi), _p(dgp), B, T, N3, R, lead, _st())
+            if any(ctx.needs_input_grad[5 + 4 * d] for d in range(ndir)):
+                s16b = U16
+                if s16b is None:
+                    n_s, tail = B * L * C, (ktaps - stride) * C
+                    s16b = torch.empty(n_s + tail, device=dev, dtype=BF16)
+                    _lib.call("b2p_cast16_tail", _p(x), _p(s16b), n_s, n_s + tail, 0, _st())
+                dwp = torch.empty(N3, IN, device=dev)
+                gemm(N3, IN, B * R, op(dgp, lead * N3, N3, False), op(s16b, 0, stride * C, False), dwp, IN)
+                del s16b
+                for d in range(ndir):
+                    dw = torch.empty(G3, IN, device=dev)
+                    _lib.call("b2p_conv_weight_permute", _p(dwp, d * G3 * IN), _p(dw), G3, C, ktaps, 1, _st())
+                    grads[4 * d] = dw
+            if ctx.needs_input_grad[0]:
+                dx = torch.empty(B, L, C, device=dev)
+                gemm(B * R, stride * C, (ktaps // stride) * N3, op(dgp, 0, N3, True), op(wperm, 0, stride * C, False),
+                     dx, stride * C)
+        elif unf_meta is not None:
             ktaps, stride = unf_meta
             _, L, C = x.shape
             dgi16 = cast16(dgi) if U16 is not None else None
@@ -1169,6 +1267,7 @@ def gru_layer(x, H, ndir, weights, h0=None):
 # =====================================================================================
 # Linear / dropout
 # =====================================================================================
+@_prec_follow
 class _Linear(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, W, b, act):
@@ -1289,7 +1388,7 @@ def layerdrop_layer(layer, x, p):
     always runs, its output or its input is selected by the device draw of this replay, and float
     buffers it updates in place (Conformer BatchNorm running statistics) are restored when it is
     skipped. Eager steps keep the reference's host draw and skip the layer outright."""
-    seed = SEEDS.next()
+    seed = LD_SEEDS.next()
     if LAYERDROP_LOG is not None:
         LAYERDROP_LOG.append(seed)
     bufs = [b for b in layer.buffers() if b.is_floating_point() and b.numel() % 4 == 0]
@@ -1323,6 +1422,7 @@ def layerdrop_keep(p, seed, epoch=None) -> bool:
 # =====================================================================================
 # Wav2Vec2 positional conv embedding + residual + LayerNorm + dropout
 # =====================================================================================
+@_prec_follow
 class _PosConvLN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, seed):
@@ -1438,7 +1538,9 @@ def _posconv16_bwd(ctx, e16, wg, wv, w, norms, pre, dxsum, dlg, dlb):
 def pos_conv_ln(e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, training):
     """dropout(LN(e + gelu(posconv(e)))); ln_g = ln_b = None: dropout(e + gelu(posconv(e))) (stable-LN)."""
     p = drop_p if training else 0.0
-    return _PosConvLN.apply(e.contiguous(), wg, wv, cbias, ln_g, ln_b, groups, eps, p, SEEDS.next() if p > 0 else 0)
+    seed = SEEDS.next() if p > 0 else 0
+    with _fp32_if("posconv"):
+        return _PosConvLN.apply(e.contiguous(), wg, wv, cbias, ln_g, ln_b, groups, eps, p, seed)
 
 
 # =====================================================================================
@@ -1548,6 +1650,7 @@ def _attn16_bwd(qkv16, dO16, lse2, B, T, nh, dh, p_attn, seed, want32=True, mask
 # post-LN transformer encoder layer (Wav2Vec2EncoderLayer)
 # =====================================================================================
 @_gate_aware
+@_prec_follow
 class _EncoderLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cfg, wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
@@ -1647,6 +1750,7 @@ class _EncoderLayer(torch.autograd.Function):
 
 
 @_gate_aware
+@_prec_follow
 class _EncoderLayer16(torch.autograd.Function):
     """bf16-operand variant of _EncoderLayer (same math, same dropout masks): Q/K/V fused into one
     GEMM over the concatenated bf16 weight, every projection reading bf16 copies written by the
@@ -1824,9 +1928,10 @@ def encoder_layer(x, params, nh, eps, p_attn, p_hid, p_act, training):
         p_attn = p_hid = p_act = 0.0
     seeds = tuple(SEEDS.next() for _ in range(4)) if training else (0, 0, 0, 0)
     cfg = (nh, eps, float(p_attn), float(p_hid), float(p_act), seeds)
-    if bf16_mode():
-        return _EncoderLayer16.apply(x.contiguous(), cfg, *params)
-    return _EncoderLayer.apply(x.contiguous(), cfg, *params)
+    with _fp32_if("enc"):
+        if bf16_mode():
+            return _EncoderLayer16.apply(x.contiguous(), cfg, *params)
+        return _EncoderLayer.apply(x.contiguous(), cfg, *params)
 
 
 # =====================================================================================
@@ -2032,6 +2137,7 @@ def _act_dropout_cast16(pre, act, p, seed):
 
 
 @_gate_aware
+@_prec_follow
 class _FFNBlock(torch.autograd.Function):
     """y = x + scale * dropout_h(W2 dropout_a(act(W1 LN(x) + b1)) + b2)   (macaron half-step, scale 0.5)"""
 
@@ -2177,6 +2283,7 @@ def rotary_tables(T, D, base, device):
 
 
 @_gate_aware
+@_prec_follow
 class _ConformerAttnBlock(torch.autograd.Function):
     """y = x + dropout(linear_out(Attn(q=k=rotary(LN x), v=LN x)))  (TF conf Wav2Vec2ConformerSelfAttention)"""
 
@@ -2405,6 +2512,7 @@ def sync_batchnorm(group):
 
 
 @_gate_aware
+@_prec_follow
 class _ConvModule(torch.autograd.Function):
     """y = x + dropout(pw2(act(BN(dwconv(GLU(pw1(LN x)))))))   (TF conf Wav2Vec2ConformerConvolutionModule)"""
 

@@ -181,7 +181,10 @@ class W2VConformerBrainEncoderModel(B2TModel):
         self.process_group = None
 
     def forward(self, batch: B2tSampleBatch):
-        encoded_brain = self.brain_encoder.forward(batch)
+        # the brain encoder's forward GEMMs on fp16 operands too: its GRU features feed every later
+        # step's update (bf16 operands there put 3.7e-4 relative into the step-1 loss, tools/traj_err.py)
+        with Fn.forward_f16(self.forward_f16):
+            encoded_brain = self.brain_encoder.forward(batch)
         targets = batch.target
         assert targets is not None
         targets = targets.masked_fill(targets < 1, -100)

@@ -264,13 +264,22 @@ class W2VBrainEncoderModel(B2TModel):
         self.pre_w2v_head_for_additional_loss = None
         self.blank = 0
         self.sync_metrics = True   # reference reads ctc_loss.item() inside forward (:94)
+        # bf16 mode: the brain encoder's forward GEMMs (day layer, GRU input projections, FC stack) and
+        # GRU recurrences on fp16 operands (Fn.forward_f16; backward stays bf16)
+        self.brain_forward_f16 = True
+        # ... and the encoder's fp32-operand forward GEMMs (the stable-LN blocks' projections, lm_head):
+        # bf16 noise on the logits biases the convex CTC loss (plumbing_stable: -1.4e-3 relative with
+        # bf16 stable-LN blocks, tools/fixture_err2.py); the post-LN layers stage their own 16-bit copies
+        self.forward_f16 = True
 
     def forward(self, batch: B2tSampleBatch):
-        encoded_brain = self.brain_encoder.forward(batch)
+        with Fn.forward_f16(self.brain_forward_f16):
+            encoded_brain = self.brain_encoder.forward(batch)
         targets = batch.target
         assert targets is not None
         targets = targets.masked_fill(targets < 1, -100)
-        w2v_output, hidden_states = self.w2v_encoder.forward(encoded_brain.logits)
+        with Fn.forward_f16(self.forward_f16):
+            w2v_output, hidden_states = self.w2v_encoder.forward(encoded_brain.logits)
         ctc_loss = (
             Fn.ctc_loss(w2v_output, targets, encoded_brain.logit_lens, batch.target_lens, self.blank)
             if batch.target_lens is not None and encoded_brain.logit_lens is not None else None)

@@ -88,13 +88,47 @@ class HipAdam(torch.optim.Optimizer):
         return sd
 
     def load_state_dict(self, state_dict) -> None:
-        """In the device form the loaded step counts go into the existing device counters; the
-        moment tensors are replaced, so steps captured before the load must be captured again."""
+        """Device form: captured steps hold raw pointers to the moment tensors and step counters, so the
+        loaded values are copied INTO the existing tensors (the pointers stay valid and graphs captured
+        before the load replay from the loaded state). A trainable parameter absent from the loaded
+        state (torch.optim.Adam keeps none for a parameter that never had a gradient, and state_dict()
+        drops step-0 entries) gets zero moments and step 0 again, as make_capturable() creates them."""
+        if not self.capturable:
+            super().load_state_dict(state_dict)
+            return
+        keep = {p: (st.get("exp_avg"), st.get("exp_avg_sq")) for p, st in self.state.items() if len(st)}
         super().load_state_dict(state_dict)
-        if self.capturable:
-            for group, d in zip(self.param_groups, self._dev):
-                steps = [float(self.state[p]["step"]) if len(self.state[p]) else 0.0 for p in group["params"]]
-                d["steps"].copy_(torch.tensor(steps, dtype=torch.float64))
+        for group, d in zip(self.param_groups, self._dev):
+            for p in group["params"]:
+                old = keep.get(p)
+                st = self.state[p]
+                if old is None or old[0] is None:
+                    if p.requires_grad and len(st) == 0:
+                        raise RuntimeError("HipAdam (device form): a trainable parameter without device state")
+                    continue
+                ea, eas = old
+                if len(st):
+                    ea.copy_(st["exp_avg"])
+                    eas.copy_(st["exp_avg_sq"])
+                else:
+                    ea.zero_()
+                    eas.zero_()
+                    st["step"] = torch.tensor(0.0)
+                st["exp_avg"], st["exp_avg_sq"] = ea, eas
+            steps = [float(self.state[p]["step"]) if len(self.state[p]) else 0.0 for p in group["params"]]
+            d["steps"].copy_(torch.tensor(steps, dtype=torch.float64))
+
+    def add_param_group(self, param_group) -> None:
+        """torch.optim.Optimizer.add_param_group; in the device form the new group gets its device lr,
+        step counters and state right away (a replayed update walks every group's device record)."""
+        super().add_param_group(param_group)
+        if getattr(self, "capturable", False):
+            self.capturable = False
+            dev, self._dev = self._dev, []
+            device = dev[0]["lr"].device if dev else self.param_groups[0]["params"][0].device
+            self.make_capturable(device)
+            # the existing groups keep their device tensors (captured steps point at them)
+            self._dev[:len(dev)] = dev
 
     def prepare_replay(self) -> None:
         """Stream-ordered refresh of each group's device lr (LR schedulers change it on the host)."""
@@ -114,6 +148,8 @@ class HipAdam(torch.optim.Optimizer):
         return f.data_ptr() if f is not None else 0
 
     def _step_device(self, lib, stream):
+        if len(self._dev) != len(self.param_groups):
+            raise RuntimeError("HipAdam (device form): param groups without device state")
         capturing = Fn.capturing()
         ld_gates = Fn.layerdrop_param_gates() if capturing else {}
         for group, d in zip(self.param_groups, self._dev):

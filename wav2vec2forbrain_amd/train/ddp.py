@@ -32,7 +32,7 @@ import torch.distributed as dist
 
 class GradBucketReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, process_group=None,
-                 average: bool = True, overlap: bool = True, grad_views: bool = True):
+                 average: bool = True, overlap: bool = True, grad_views: bool = True, track_used: bool = True):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
@@ -75,6 +75,15 @@ class GradBucketReducer:
         dev = self.params[0].device if self.params else torch.device("cpu")
         self.used = torch.ones(max(len(self.params), 1), dtype=torch.int32, device=dev)
         self.gates = {id(p): self.used[k] for k, p in enumerate(self.params)}
+        # track_used=False (frozen parameters: nobody reads their gates, their gradients come from the
+        # deferred GEMMs, not from autograd hooks): no flag exchange at all
+        self.track_used = track_used
+        # eager steps: the local flags go up through a persistent pinned buffer (stream-ordered copy; the
+        # event guards the buffer against being refilled before the previous step's copy has run)
+        self._loc_host = (torch.ones(max(len(self.params), 1), dtype=torch.int32).pin_memory()
+                          if dev.type == "cuda" else None)
+        self._loc_event = None
+        self._pos = {id(p): k for k, p in enumerate(self.params)}
         self._layer_gates = None   # graph-replayed steps: the device LayerDrop flags (make_layer_gates)
         self._seen: set = set()
         self._reset()
@@ -122,12 +131,23 @@ class GradBucketReducer:
         """Local used flags -> MAX over ranks into self.used (the optimizer's gates)."""
         if not self.params:
             return
+        if not self.track_used:
+            return
         if self._layer_gates is not None:
             flags, idx = self._layer_gates
             torch.index_select(torch.cat([f.reshape(1) for f in flags]), 0, idx, out=self.used)
+        elif self._loc_host is not None:
+            if self._loc_event is not None:
+                self._loc_event.synchronize()
+            loc = self._loc_host.numpy()
+            loc[:] = 0
+            loc[[self._pos[i] for i in self._seen if i in self._pos]] = 1
+            self.used.copy_(self._loc_host, non_blocking=True)
+            self._loc_event = torch.cuda.Event()
+            self._loc_event.record()
         else:
             loc = torch.tensor([1 if id(p) in self._seen else 0 for p in self.params], dtype=torch.int32)
-            self.used.copy_(loc, non_blocking=False)
+            self.used.copy_(loc)
         if self.world > 1:
             dist.all_reduce(self.used, op=dist.ReduceOp.MAX, group=self.pg)
 

@@ -58,7 +58,7 @@ class Trainer:
                 # included; averaging those too keeps every rank's clip coefficient equal to the
                 # single-process global-batch one (they accumulate across steps identically on all
                 # ranks once averaged, so averaging the running sum each step is exact)
-                self.frozen_reducer = GradBucketReducer(frozen, overlap=False, grad_views=False)
+                self.frozen_reducer = GradBucketReducer(frozen, overlap=False, grad_views=False, track_used=False)
         # frozen parameters (not optimised): their gradient GEMMs run deferred beside the GRU backward
         Fn.set_deferred_wgrad(frozen)
         # replayed steps (see train_step): a cache of captured steps keyed by the batch shape
