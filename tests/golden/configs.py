@@ -32,14 +32,16 @@ CONFIGS = [
          fc_hidden=[], learnable_h0=False, full_grad_max=4096, infeasible=False, stable=True),
     # the bench workloads themselves (BASELINE configs[1] and configs[2]) at bs=32, 1024-bin windows:
     # loss, per-parameter gradient norms and sampled gradient entries (inputs are regenerated from the
-    # seed, not stored: x alone would be 33 MB)
+    # seed, not stored: x alone would be 33 MB), and the bench's 3-step Adam trajectory over the brain
+    # encoder (bench.py parity: lr 1e-3, frozen w2v)
     dict(name="base_bs32", seed=42, B=32, L=1024, in_lens=[1024] * 32, tgt_range=(60, 120), hidden_size=768,
          layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2, bidirectional=True,
-         fc_hidden=[], learnable_h0=False, full_grad_max=0, infeasible=False, big=True),
+         fc_hidden=[], learnable_h0=False, full_grad_max=0, infeasible=False, big=True,
+         adam=dict(steps=3, lr=1e-3, w2v_lr=None, wd=0.0)),
     dict(name="conformer_large_bs32", seed=42, B=32, L=1024, in_lens=[1024] * 32, tgt_range=(60, 120),
          hidden_size=1024, layers=24, heads=16, ffn=4096, pos_k=128, pos_groups=16, gru_hidden=512, gru_layers=3,
          bidirectional=True, fc_hidden=[256], learnable_h0=False, full_grad_max=0, infeasible=False, conformer=True,
-         dw_kernel=31, big=True),
+         dw_kernel=31, big=True, adam=dict(steps=3, lr=1e-3, w2v_lr=None, wd=0.0)),
     # BASELINE configs[3] per GPU: wav2vec2-large-960h architecture (post-LN forced by the reference,
     # w2v_custom_feat_extractor.py:18-19,36-41: 1024/24L/16H/4096), GRU H256x2, fc [] (the 512 -> 1024
     # projection), 32 samples x 1024 bins; plus 2 Adam steps over the brain encoder (frozen w2v)

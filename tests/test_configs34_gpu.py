@@ -1,5 +1,7 @@
-"""BASELINE configs[3] and configs[4] on one GPU (their per-GPU workloads), against trajectories the
-reference's own modules and optimizer produced (tests/golden/make_golden.py: adam_trajectory):
+"""Adam trajectories against the ones the reference's own modules and optimizer produced
+(tests/golden/make_golden.py: adam_trajectory): the bench workloads (base_bs32 = configs[1],
+conformer_large_bs32 = configs[2]: 3 steps over the brain encoder, lr 1e-3, as bench.py's parity) and
+BASELINE configs[3] and configs[4] on one GPU (their per-GPU workloads):
 
   large960_bs32           wav2vec2-large-960h (post-LN 1024/24L/16H/4096), GRU H256x2, fc [] (the
                           512 -> 1024 projection), 32 x 1024 bins; unfreeze_strategy=brain_encoder,
@@ -28,7 +30,12 @@ pytestmark = pytest.mark.gpu
 
 LOSS_RTOL = 1e-3        # BASELINE.json north_star: the loss at the reference's weights
 FP32_TRAJ_RTOL = 1e-4   # exact-fp32 mode, every step of the trajectory
-BF16_TRAJ_RTOL = 2e-2   # bf16 mode, steps after the first Adam update (Adam amplifies operand rounding)
+# bf16 mode, steps after the first Adam update. The bench workloads (BASELINE configs[1] / configs[2], the
+# bench.py parity trajectories) hold the north-star 1e-3 at every step; configs[3] / configs[4] per GPU
+# are held to what is measured there (24-layer post-LN encoder on bf16 operands; all 618 M parameters
+# updated), see DESIGN.md section 4
+BF16_TRAJ_RTOL = {"base_bs32": 1e-3, "conformer_large_bs32": 1e-3, "large960_bs32": 5e-3,
+                  "conformer_large_ft_bs8": 1e-2}
 
 
 def _trajectory(name, mode):
@@ -57,7 +64,7 @@ def _trajectory(name, mode):
     return losses, deltas, trainer
 
 
-@pytest.mark.parametrize("name", ["large960_bs32", "conformer_large_ft_bs8"])
+@pytest.mark.parametrize("name", ["base_bs32", "conformer_large_bs32", "large960_bs32", "conformer_large_ft_bs8"])
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
 def test_adam_trajectory_matches_reference(name, mode):
     fx = load_fixture(name)
@@ -69,7 +76,7 @@ def test_adam_trajectory_matches_reference(name, mode):
         assert max(rel) <= FP32_TRAJ_RTOL, (losses, ref, rel)
     else:
         assert rel[0] <= LOSS_RTOL, (losses, ref, rel)
-        assert max(rel[1:]) <= BF16_TRAJ_RTOL, (losses, ref, rel)
+        assert max(rel[1:]) <= BF16_TRAJ_RTOL[name], (losses, ref, rel)
     # parameter updates: every parameter the reference's Adam moved moved here by about as much, and
     # every parameter it left alone (unused inpLayer* / hidden_start / conformer pos_conv_embed:
     # grad None) stayed bit-identical
