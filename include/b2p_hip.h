@@ -96,8 +96,8 @@ typedef struct {
   /* bf16 LDS-DMA kernel only (both operands bf16), nz1*nz2 == 1, no split-K:                   */
   uint16_t* pre16;            /* optional bf16 pre-activation store (instead of pre_out)       */
   const uint16_t* aux16;      /* act_bwd operand in bf16 (instead of aux; strides of aux)      */
-  float* colsum_part;         /* optional: per-128-row-tile column sums of the final value,
-                               * [ceil(M/128)][N] floats (fused bias gradient; b2p_colsum_parts) */
+  float* colsum_part;         /* optional: column sums of the final value per 64 output rows,
+                               * [ceil(M/64)][N] floats (fused bias gradient; b2p_colsum_parts) */
 } b2p_epilogue;
 
 typedef struct {
@@ -245,6 +245,10 @@ int b2p_unfold_weight16(const float* w0, const float* w1, int64_t G, int64_t C, 
 int b2p_pad_rows16(const float* src, uint16_t* dst, int64_t B, int64_t T, int64_t N, int64_t R, int64_t lead,
                    b2p_stream_t stream);
 int b2p_cast16_tail(const float* x, uint16_t* y, int64_t n, int64_t n_total, int fp16, b2p_stream_t stream);
+/* records {dst, a, b, count} (int64 each; a / b may be 0 = NULL): dst[i] = a[i] + b[i] (fp32), all
+ * records in one launch: the per-step assembly of stacked / concatenated small parameter tensors
+ * (nn.GRU W_hh of both directions, b_ih + b_hh folds; src/model/brain_feature_extractor.py:39-47) */
+int b2p_gather_recs(const int64_t* recs, int nrec, b2p_stream_t stream);
 /* out[o][tap*I + i] = in[o][i*ntaps + tap]   (conv weight (O, I, taps) -> tap-major GEMM B)
  * inverse=1 does the opposite mapping; flip=1 reads tap (ntaps-1-tap). */
 int b2p_conv_weight_permute(const float* in, float* out, int64_t O, int64_t I, int64_t ntaps,

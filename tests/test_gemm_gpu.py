@@ -303,24 +303,28 @@ def test_bf16_epilogue_pre16_aux16_colsum(M, N, K):
 _TILE_ENV = {"small": {"B2P_GEMM16_PP": "0", "B2P_GEMM16_K64": "0"},
              "small64": {"B2P_GEMM16_PP": "0", "B2P_GEMM16_K64": "1"},
              "big": {"B2P_GEMM16_PP": "0", "B2P_GEMM16_BIG": "1"},
-             "pp": {"B2P_GEMM16_PP": "2"}}
+             "pp": {"B2P_GEMM16_PP": "2", "B2P_GEMM16_PP192": "0"},
+             "pp192": {"B2P_GEMM16_PP": "2", "B2P_GEMM16_PP192": "2"}}
 _TILE_CASES = [(lay, M, N, K) for lay in ("AB", "Ab", "ab") for (M, N, K) in ((4096, 1536, 512), (3000, 1544, 776))]
 
 
-@pytest.mark.parametrize("tile", ["small", "small64", "big", "pp"])
+@pytest.mark.parametrize("tile", ["small", "small64", "big", "pp", "pp192"])
 def test_bf16_tile_configs(tile):
     """Every bf16 tile configuration (128x128x32 3-stage and 128x128x64 2-stage 4-wave; 256x128x64
-    8-wave; 256x256x64 8-wave ping-pong), forced by environment (read once per process -> one subprocess per configuration),
+    8-wave; 256x256x64 and 192x256x64 8-wave ping-pong), forced by environment (read once per process -> one subprocess per configuration),
     against torch fp32 on the same bf16 operands with a full epilogue (bias, GELU, residual, bf16
-    copy, fused column sums), plus split-K and batched launches.
-    (mn-contiguous operands need ld % 8 == 0, so M, N are multiples of 8.)"""
+    copy, fused column sums), plus split-K and batched launches. The 192-row ping-pong tile takes
+    k-contiguous A launches without column sums, so it also runs every case without them and on fp16
+    operands. (mn-contiguous operands need ld % 8 == 0, so M, N are multiples of 8.)"""
     import os
     import subprocess
     import sys
     env = dict(os.environ, **_TILE_ENV[tile])
     code = ("import tests.test_gemm_gpu as t\n"
             "for c in t._TILE_CASES: t._check_tile_case(*c)\n"
-            "t._check_tile_splitk_batched()\n")
+            "t._check_tile_splitk_batched()\n"
+            "for c in t._TILE_CASES: t._check_tile_case(*c, cs=False)\n"
+            "for c in t._TILE_CASES: t._check_tile_case(*c, cs=False, f16=True)\n")
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
@@ -345,10 +349,12 @@ def _check_tile_splitk_batched():
     _close16(out, (a.double() @ w.double().transpose(1, 2)).float(), 2e-6)
 
 
-def _check_tile_case(layout, M, N, K):
+def _check_tile_case(layout, M, N, K, cs=True, f16=False):
     Fn = _fn()
     torch.manual_seed(5)
-    bf = torch.bfloat16
+    bf = torch.float16 if f16 else torch.bfloat16
+    if f16 and layout != "AB":
+        return
     if layout == "AB":
         a, w = torch.randn(M, K, device="cuda").to(bf), torch.randn(N, K, device="cuda").to(bf)
         A, Bo, ref = Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), a.float() @ w.float().t()
@@ -362,13 +368,18 @@ def _check_tile_case(layout, M, N, K):
     res = torch.randn(M, N, device="cuda")
     out = torch.empty(M, N, device="cuda")
     o16 = torch.empty(M, N, device="cuda", dtype=bf)
-    parts = Fn.colsum_parts_buf(M, N, "cuda")
-    Fn.gemm(M, N, K, A, Bo, out, N, bias=bias, act=Fn.ACT["gelu"], residual=res, C16=o16, colsum_part=parts)
+    parts = Fn.colsum_parts_buf(M, N, "cuda") if cs else None
+    if f16:
+        o16 = torch.empty(M, N, device="cuda", dtype=torch.float16)
+        Fn.gemm(M, N, K, A, Bo, out, N, bias=bias, act=Fn.ACT["gelu"], residual=res, C16=o16, c16_fp16=True)
+    else:
+        Fn.gemm(M, N, K, A, Bo, out, N, bias=bias, act=Fn.ACT["gelu"], residual=res, C16=o16, colsum_part=parts)
     want = F.gelu(ref + bias) + res
     _close(out, want, "bf16", scale=want.abs().max().item())
     _close(o16.float(), want, "bf16", scale=want.abs().max().item())
-    cs = Fn.colsum_from_parts(parts, torch.empty(N, device="cuda"))
-    assert float((cs - want.sum(0)).abs().max()) <= 1e-4 * float(want.abs().sum(0).max())
+    if cs:
+        csum = Fn.colsum_from_parts(parts, torch.empty(N, device="cuda"))
+        assert float((csum - want.sum(0)).abs().max()) <= 1e-4 * float(want.abs().sum(0).max())
 
 
 @pytest.mark.parametrize("fwd16", [False, True])

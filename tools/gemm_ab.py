@@ -53,6 +53,8 @@ def case(M, N, K, epi, a_k=True, b_k=True):
         kw["seed"] = 7
     if "r" in epi:
         kw["residual"] = torch.randn(M, N, device=dev)
+    if "c" in epi:   # fused bias-gradient column sums
+        kw["colsum_part"] = Fn.colsum_parts_buf(M, N, dev)
     fn = lambda: Fn.gemm(M, N, K, A, B, C, N, **kw)
     us = timeit(fn)
     tf = 2.0 * M * N * K / (us * 1e-6) / 1e12
@@ -61,7 +63,7 @@ def case(M, N, K, epi, a_k=True, b_k=True):
 
 SHAPES = [
     (7968, 3072, 768, "badh", True, True),    # FFN1 forward
-    (7968, 3072, 768, "gdh", True, True),     # FFN1 dgrad (GELU', dropout)
+    (7968, 3072, 768, "gdhc", True, True),    # FFN1 dgrad (GELU', dropout, bias-gradient column sums)
     (7968, 768, 3072, "bdrf", True, True),    # FFN2 forward
     (7968, 768, 3072, "rf", True, True),      # dx1
     (7968, 2304, 768, "bh", True, True),      # QKV
@@ -70,6 +72,10 @@ SHAPES = [
     (7968, 768, 768, "h", True, True),        # dO
     (3072, 768, 7968, "f", False, False),     # weight gradients (K = tokens, split-K)
     (768, 768, 7968, "f", False, False),
+    (7968, 4096, 1024, "badh", True, True),   # Conformer-large FFN1 forward
+    (7968, 1024, 4096, "bdrf", True, True),   # Conformer-large FFN2 forward
+    (7968, 3072, 1024, "bh", True, True),     # Conformer-large QKV
+    (4096, 1024, 7968, "f", False, False),    # Conformer-large FFN weight gradient
 ]
 
 if __name__ == "__main__":

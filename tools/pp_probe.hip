@@ -1,8 +1,11 @@
 // Diagnostic: per-workgroup clock stamps of the 256x256 ping-pong GEMM (start, after the prologue,
 // after the K loop, end). Build: hipcc -O3 --offload-arch=gfx950 -DB2P_PP_STAMPS tools/pp_probe.hip
-//   -Lwav2vec2forbrain_amd -lb2p_hip -o build/pp_probe ; run: build/pp_probe M N K
+//   -Lwav2vec2forbrain_amd -lb2p_hip -o probe_bin/pp_probe ; run: probe_bin/pp_probe M N K
 #define B2P_PP_STAMPS 1
 #include "../wav2vec2forbrain_amd/csrc/gemm16.hip"
+#include "../wav2vec2forbrain_amd/csrc/gemm16_nt.hip"
+#include "../wav2vec2forbrain_amd/csrc/gemm16_nt16.hip"
+#include "../wav2vec2forbrain_amd/csrc/gemm16_misc.hip"
 #include <algorithm>
 #include <vector>
 

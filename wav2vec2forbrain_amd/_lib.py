@@ -88,6 +88,7 @@ _SIGS = {
     "b2p_unfold_weight16": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_p]),
     "b2p_pad_rows16": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_cast16_tail": (c_i32, [c_p, c_p, c_i64, c_i64, c_i32, c_p]),
+    "b2p_gather_recs": (c_i32, [c_p, c_i32, c_p]),
     "b2p_conv_weight_permute": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_conv_weight_transpose_flip": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_weight_norm_workspace": (c_i64, [c_i64, c_i64, c_i64]),

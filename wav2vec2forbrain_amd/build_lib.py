@@ -29,9 +29,21 @@ def _headers_mtime() -> float:
     return max((os.path.getmtime(h) for h in hs), default=0.0)
 
 
+def _inc_mtime(src: str) -> float:
+    """Newest mtime of the csrc/*.inc files a source includes (kernel templates shared by several
+    instantiation units: only their includers rebuild when they change)."""
+    import re
+    t = 0.0
+    for name in re.findall(r'#include "([^"]+\.inc)"', open(src).read()):
+        f = os.path.join(CSRC, name)
+        if os.path.exists(f):
+            t = max(t, os.path.getmtime(f))
+    return t
+
+
 def _compile(src: str, hmt: float, verbose: bool) -> str:
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hmt):
+    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hmt, _inc_mtime(src)):
         return obj
     cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
     audit = os.environ.get("B2P_BUILD_AUDIT") == "1"

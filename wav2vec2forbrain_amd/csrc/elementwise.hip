@@ -904,6 +904,42 @@ extern "C" int b2p_cast16_tail(const float* x, uint16_t* y, int64_t n, int64_t n
   return 0;
 }
 
+// ------------------------------------------------------------------ small-tensor assembly
+// dst = (a ? a : 0) + (b ? b : 0) over `count` floats, up to GATHER_MAXR records per launch (one
+// grid row each): the per-step stacking / concatenation of GRU weights and biases (W_hh of both
+// directions, folded b_ih + b_hh[r,z]) in one launch instead of a torch cat / stack / add each.
+constexpr int GATHER_MAXR = 16;
+struct GatherRecs { int64_t r[GATHER_MAXR][4]; };
+__global__ void gather_rec_k(GatherRecs g) {
+  const int64_t* r = g.r[blockIdx.y];
+  float* dst = reinterpret_cast<float*>(r[0]);
+  const float* a = reinterpret_cast<const float*>(r[1]);
+  const float* b = reinterpret_cast<const float*>(r[2]);
+  const int64_t n = r[3];
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = (a ? a[i] : 0.f) + (b ? b[i] : 0.f);
+}
+
+extern "C" int b2p_gather_recs(const int64_t* recs, int nrec, b2p_stream_t stream) {
+  B2P_CHECK_ARG(recs != nullptr || nrec == 0, "gather_recs: NULL records");
+  for (int c0 = 0; c0 < nrec; c0 += GATHER_MAXR) {
+    const int nc = nrec - c0 < GATHER_MAXR ? nrec - c0 : GATHER_MAXR;
+    GatherRecs g;
+    int64_t maxn = 0;
+    for (int i = 0; i < nc; ++i) {
+      for (int k = 0; k < 4; ++k) g.r[i][k] = recs[4 * (c0 + i) + k];
+      B2P_CHECK_ARG(g.r[i][3] <= 0 || g.r[i][0], "gather_recs: NULL destination");
+      maxn = g.r[i][3] > maxn ? g.r[i][3] : maxn;
+    }
+    if (maxn <= 0) continue;
+    const int64_t bx = (maxn + 255) / 256;
+    hipLaunchKernelGGL(gather_rec_k, dim3((unsigned)(bx < 512 ? bx : 512), (unsigned)nc), dim3(256), 0,
+                       (hipStream_t)stream, g);
+  }
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int b2p_softmax_fwd(const float* S, float* P, float* Pd, int64_t rows, int64_t n, int64_t ld,
                                float drop_p, uint64_t drop_seed, b2p_stream_t stream) {
   B2P_CHECK_ARG(S && P && Pd, "softmax_fwd: NULL pointer");

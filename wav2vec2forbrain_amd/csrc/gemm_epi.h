@@ -29,6 +29,7 @@ struct EpiArgs {
   int32_t vec4;   // every C-shaped tensor allows 16-B (C16: 8-B) accesses at n % 4 == 0
   const uint64_t* epoch;   // graph-replay dropout seed offset (b2p_seed_eff)
   const int32_t* gate;     // LayerDrop gate (b2p_gate): closed -> no K loop
+  uint32_t rk;             // gemm16 epilogue kind bits of this launch (EK_RUNTIME instantiations)
 };
 
 __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, int z2, int m, int n,
@@ -190,6 +191,7 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
   ea.vec4 = v ? 1 : 0;
   ea.epoch = b2p_seed_epoch();
   ea.gate = b2p_gate();
+  ea.rk = 0;
   return ea;
 }
 

@@ -632,8 +632,8 @@ def _colsum_ws(M, N, device):
 
 
 def colsum_parts_buf(M, N, device):
-    """Workspace for a GEMM epilogue's fused column sums (one row per 128-row tile)."""
-    return torch.empty(-(-M // 128), N, device=device)
+    """Workspace for a GEMM epilogue's fused column sums (one row per 64 output rows)."""
+    return torch.empty(-(-M // 64), N, device=device)
 
 
 def colsum_from_parts(parts, out):
@@ -1035,9 +1035,23 @@ class _GRULayer(torch.autograd.Function):
         # into the input projection bias
         use16 = bf16_mode() and _GRU16[0] and bool(_lib.load().b2p_gru16_supported(H))
         usemc = bf16_mode() and not use16 and _GRUMC[0] and bool(_lib.load().b2p_gru_mc_supported(H))
-        if use16 and bhh[0] is not None:
-            bih = [(b if b is not None else torch.zeros(G3, device=dev))
-                   + torch.cat([bh[:2 * H], torch.zeros(H, device=dev)]) for b, bh in zip(bih, bhh)]
+        # the step's stacked recurrent weights / biases and the concatenated input-projection bias (with
+        # b_hh's r/z parts folded in for gru16), assembled by ONE launch (b2p_gather_recs)
+        whh_s = torch.empty(ndir, G3, H, device=dev)
+        bhh_s = torch.empty(ndir, G3, device=dev) if bhh[0] is not None else None
+        has_bias = any(b is not None for b in bih) or (use16 and bhh[0] is not None)
+        bias_cat = torch.empty(ndir * G3, device=dev) if has_bias else None
+        recs = []
+        for d in range(ndir):
+            recs += [_p(whh_s, d * G3 * H), _p(whh[d]), 0, G3 * H]
+            if bhh_s is not None:
+                recs += [_p(bhh_s, d * G3), _p(bhh[d]), 0, G3]
+            if bias_cat is not None:
+                fold = use16 and bhh[0] is not None
+                recs += [_p(bias_cat, d * G3), _p(bih[d]) or 0, _p(bhh[d]) if fold else 0, 2 * H,
+                         _p(bias_cat, d * G3 + 2 * H), _p(bih[d], 2 * H) or 0, 0, H]
+        arr = (ctypes.c_int64 * len(recs))(*recs)
+        _lib.call("b2p_gather_recs", arr, len(recs) // 4, _st())
         implicit = (unf_meta is not None and bf16_mode() and L % stride == 0 and ktaps % stride == 0 and C % 4 == 0
                     and _UNFOLD_IMPLICIT[0])
         if implicit:
@@ -1054,8 +1068,6 @@ class _GRULayer(torch.autograd.Function):
             n_s, tail = B * L * C, (ktaps - stride) * C
             s16 = torch.empty(n_s + tail, device=dev, dtype=torch.float16 if half else BF16)
             _lib.call("b2p_cast16_tail", _p(x), _p(s16), n_s, n_s + tail, int(half), _st())
-            bias_cat = torch.cat([b if b is not None else torch.zeros(G3, device=dev) for b in bih]) \
-                if any(b is not None for b in bih) else None
             gemm(T, N3, IN, op(s16, 0, stride * C, True, bs1=L * C), op(wf, 0, IN, True), gi, N3, cbs1=T * N3, nz1=B,
                  bias=bias_cat)
             del wf
@@ -1066,8 +1078,6 @@ class _GRULayer(torch.autograd.Function):
             wperm = torch.empty(ndir * G3, IN, device=dev)
             for d in range(ndir):
                 _lib.call("b2p_conv_weight_permute", _p(wih[d]), _p(wperm, d * G3 * IN), G3, C, ktaps, 0, _st())
-            bias_cat = torch.cat([b if b is not None else torch.zeros(G3, device=dev) for b in bih]) \
-                if any(b is not None for b in bih) else None
             if bf16_mode() and not _state.fwd16:
                 # bf16 operands: the tap-major unfold materialised once in bf16 (it is also the
                 # weight-gradient operand) and a bf16 copy of the permuted weight
@@ -1083,11 +1093,21 @@ class _GRULayer(torch.autograd.Function):
         else:
             _chk(x, "gru.x")
             wperm = U16 = None
-            for d in range(ndir):
-                gemm(B * T, G3, IN, op(x, 0, IN, True), op(wih[d], 0, IN, True), gi, ndir * G3, c_off=d * G3,
-                     bias=bih[d])
-        whh_s = torch.stack(whh, 0).contiguous()
-        bhh_s = torch.stack(bhh, 0).contiguous() if bhh[0] is not None else None
+            if bf16_mode() and IN % 8 == 0:
+                # both directions' projections as ONE GEMM over the stacked 16-bit W_ih (fp16 under
+                # forward_f16), N = ndir * 3H
+                half = _state.fwd16
+                w16 = torch.empty(ndir * G3, IN, device=dev, dtype=torch.float16 if half else BF16)
+                for d in range(ndir):
+                    _lib.call("b2p_cast16_2d", _p(wih[d]), G3, IN, IN, _p(w16, d * G3 * IN), IN, int(half), _st())
+                x16 = torch.empty(B * T, IN, device=dev, dtype=w16.dtype)
+                _lib.call("b2p_cast16_2d", _p(x), B * T, IN, IN, _p(x16), IN, int(half), _st())
+                gemm(B * T, ndir * G3, IN, op(x16, 0, IN, True), op(w16, 0, IN, True), gi, ndir * G3, bias=bias_cat)
+                del w16, x16
+            else:
+                for d in range(ndir):
+                    gemm(B * T, G3, IN, op(x, 0, IN, True), op(wih[d], 0, IN, True), gi, ndir * G3, c_off=d * G3,
+                         bias=None if bias_cat is None else _view_off(bias_cat, d * G3))
         out = torch.empty(B, T, ndir * H, device=dev)
         saved = None if use16 else torch.empty(B, T, ndir, 4, H, device=dev)
         if h0 is not None:
