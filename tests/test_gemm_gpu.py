@@ -369,14 +369,18 @@ def _check_tile_case(layout, M, N, K, cs=True, f16=False):
     out = torch.empty(M, N, device="cuda")
     o16 = torch.empty(M, N, device="cuda", dtype=bf)
     parts = Fn.colsum_parts_buf(M, N, "cuda") if cs else None
-    if f16:
+    ob = None
+    if f16:   # fp16 output copy plus the second (bf16) copy C16b
         o16 = torch.empty(M, N, device="cuda", dtype=torch.float16)
-        Fn.gemm(M, N, K, A, Bo, out, N, bias=bias, act=Fn.ACT["gelu"], residual=res, C16=o16, c16_fp16=True)
+        ob = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        Fn.gemm(M, N, K, A, Bo, out, N, bias=bias, act=Fn.ACT["gelu"], residual=res, C16=o16, c16_fp16=True, C16b=ob)
     else:
         Fn.gemm(M, N, K, A, Bo, out, N, bias=bias, act=Fn.ACT["gelu"], residual=res, C16=o16, colsum_part=parts)
     want = F.gelu(ref + bias) + res
     _close(out, want, "bf16", scale=want.abs().max().item())
     _close(o16.float(), want, "bf16", scale=want.abs().max().item())
+    if ob is not None:
+        assert torch.equal(ob, out.to(torch.bfloat16))
     if cs:
         csum = Fn.colsum_from_parts(parts, torch.empty(N, device="cuda"))
         assert float((csum - want.sum(0)).abs().max()) <= 1e-4 * float(want.abs().sum(0).max())

@@ -610,6 +610,41 @@ def test_encoder_layer_bf16_operands_match_fp32_path():
         assert torch.equal(Fn.weight16(w), w.to(torch.bfloat16))   # ... the epoch bump can
 
 
+def test_encoder_layer_f16_forward_matches_fp32_path():
+    """_EncoderLayer16 under Fn.forward_f16 (fused attention, dh 64): every forward GEMM operand fp16
+    (QKV / out-projection / FFN inputs and weights; the producers also write the backward's bf16
+    operands) vs _EncoderLayer in fp32 with the same dropout seeds: the output within fp16 rounding
+    (an order of magnitude under the bf16 forward's), every gradient at bf16 level; the layer's
+    output carries both 16-bit copies for the next layer."""
+    Fn = _fn()
+    torch.manual_seed(23)
+    B, T, D, nh, Ff = 2, 200, 128, 2, 256
+    shapes = [(D, D), (D,), (D, D), (D,), (D, D), (D,), (D, D), (D,), (D,), (D,), (Ff, D), (Ff,), (D, Ff), (D,), (D,), (D,)]
+    ps = [(torch.randn(*s) / math.sqrt(s[-1])).cuda() for s in shapes]
+    ps[8] = torch.ones(D, device="cuda"); ps[14] = torch.ones(D, device="cuda")
+    x = torch.randn(B, T, D, device="cuda")
+    cfg = (nh, 1e-5, 0.1, 0.1, 0.1, (41, 42, 43, 44))
+    dy = torch.randn(B, T, D, device="cuda")
+    res, outs = [], []
+    for cls, mode, f16 in ((Fn._EncoderLayer, "fp32", False), (Fn._EncoderLayer16, "bf16", False),
+                           (Fn._EncoderLayer16, "bf16", True)):
+        with Fn.precision(mode), Fn.forward_f16(f16):
+            pg = [p.clone().requires_grad_(True) for p in ps]
+            xg = x.clone().requires_grad_(True)
+            out = cls.apply(xg, cfg, *pg)
+            outs.append(out)
+            res.append([out] + list(torch.autograd.grad(out, [xg] + pg, dy)))
+    e16, eb = _rel(res[2][0].cpu(), res[0][0].cpu()), _rel(res[1][0].cpu(), res[0][0].cpu())
+    assert e16 < 3e-3 and e16 < 0.35 * eb, (e16, eb)
+    for i, (a, b) in enumerate(zip(res[0], res[2])):
+        if i in (0, 5):     # output (above); k_proj bias gradient: mathematically 0
+            continue
+        assert _rel(b.cpu(), a.cpu()) < 3e-2, (i, _rel(b.cpu(), a.cpu()))
+    o, od = outs[2], outs[2].detach()
+    assert o._h16[1].dtype == torch.float16 and torch.equal(o._h16[1], od.to(torch.float16))
+    assert o._b16[1].dtype == torch.bfloat16 and torch.equal(o._b16[1], od.to(torch.bfloat16))
+
+
 def test_dropout_seed_epoch_counter():
     """Graph-replay seed counter (b2p_set_seed_epoch): counter 0 reproduces the eager mask, every
     b2p_seed_epoch_step gives a new mask, NULL restores eager semantics; the GEMM epilogue and the

@@ -9,7 +9,8 @@ Fn._BWD_FOLLOWS_FWD), against the exact-fp32 mode of the same model on the same 
 usage: python tools/traj_err.py [conformer|base] [steps] [variant,variant,...]
 variants: names of Fn._FP32_OPS sets joined by '+', e.g. attn+ffn ; '-' = plain bf16; prefix F: = the
 forward only (backward in bf16), except blocks marked *name (forward and backward); recur / recurfwd /
-recurbwd = the GRU recurrence on the per-step fp32 kernels in both passes / the forward / the backward."""
+recurbwd = the GRU recurrence on the per-step fp32 kernels in both passes / the forward / the backward;
+prefix B: = the blocks' backward only (Fn._FP32_BWD_ONLY), forward in the mode's precision."""
 import os
 import sys
 import time
@@ -31,12 +32,14 @@ Fn._BWD_FOLLOWS_FWD[0] = True
 RECUR = {"recur": (False, None), "recurfwd": (False, True), "recurbwd": (True, False)}
 
 
-def run(mode, ops, fwd_only=False):
+def run(mode, ops, fwd_only=False, bwd_only=()):
     Fn._BWD_FOLLOWS_FWD[0] = not fwd_only
     Fn._FP32_OPS.clear()
     Fn._FP32_OPS.update(o.lstrip("*") for o in ops if o not in RECUR)
     Fn._FP32_BWD_OPS.clear()
     Fn._FP32_BWD_OPS.update(o[1:] for o in ops if o.startswith("*"))
+    Fn._FP32_BWD_ONLY.clear()
+    Fn._FP32_BWD_ONLY.update(bwd_only)
     Fn._GRUMC[0], Fn._GRUMC_BWD[0] = True, None
     for o in ops:   # multi-CU GRU recurrence (bf16 MFMA) vs per-step fp32 kernels, per direction of the pass
         if o in RECUR:
@@ -63,6 +66,7 @@ def run(mode, ops, fwd_only=False):
     del trainer, model
     torch.cuda.empty_cache()
     Fn._FP32_OPS.clear()
+    Fn._FP32_BWD_ONLY.clear()
     return grads, losses
 
 
@@ -72,9 +76,10 @@ lg_ref = gref.pop("<logits>")
 print(f"[{kind}] fp32 mode losses {['%.6f' % v for v in lref]} ({time.time() - t0:.1f} s)", flush=True)
 for v in variants:
     fo = v.startswith("F:")
-    ops = [] if v in ("-", "F:-") else v[2 * fo:].split("+")
+    bo = v.startswith("B:")
+    ops = [] if v in ("-", "F:-") else v[2 * (fo or bo):].split("+")
     t0 = time.time()
-    g, l = run("bf16", ops, fo)
+    g, l = run("bf16", [] if bo else ops, fo, ops if bo else ())
     lg = g.pop("<logits>")
     lerr = float((lg - lg_ref).double().norm() / lg_ref.double().norm())
     num = den = eff_n = eff_d = 0.0

@@ -44,7 +44,7 @@ class Epilogue(ctypes.Structure):
         ("act", c_i32), ("act_bwd", c_i32), ("aux", c_p), ("ldaux", c_i64), ("abs1", c_i64),
         ("abs2", c_i64), ("drop_p", c_f32), ("flags", c_i32), ("drop_seed", c_u64),
         ("residual", c_p), ("ldr", c_i64), ("rbs1", c_i64), ("rbs2", c_i64), ("C16", c_p),
-        ("pre16", c_p), ("aux16", c_p), ("colsum_part", c_p),
+        ("pre16", c_p), ("aux16", c_p), ("colsum_part", c_p), ("C16b", c_p),
     ]
 
 

@@ -443,8 +443,9 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   }
   B2P_CHECK_ARG(!(d.A.conv && d.B.conv), "gemm: at most one implicit-conv operand");
   if (d.ep.act_bwd != B2P_ACT_NONE) B2P_CHECK_ARG(d.ep.aux != nullptr || d.ep.aux16 != nullptr, "gemm: act_bwd needs aux");
-  if (d.ep.pre16 || d.ep.aux16 || d.ep.colsum_part) {
-    B2P_CHECK_ARG(bf16_ops, "gemm: pre16 / aux16 / colsum_part need the bf16-operand kernel");
+  if (d.ep.pre16 || d.ep.aux16 || d.ep.colsum_part || d.ep.C16b) {
+    B2P_CHECK_ARG(bf16_ops, "gemm: pre16 / aux16 / colsum_part / C16b need the bf16-operand kernel");
+    B2P_CHECK_ARG(!d.ep.C16b || d.ksplit <= 1, "gemm: C16b needs a launch without split-K");
     B2P_CHECK_ARG(!d.ep.colsum_part || (d.nz1 * d.nz2 == 1 && d.ksplit <= 1 && d.N % 4 == 0),
                   "gemm: colsum_part needs nz1*nz2 == 1, no split-K and N %% 4 == 0");
   }

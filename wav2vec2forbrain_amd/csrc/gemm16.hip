@@ -47,6 +47,7 @@ static uint32_t epi_kind(const b2p_gemm_desc& d, const EpiArgs& ea) {
   if (e.C) k |= EK_C32;
   if (e.C16) k |= EK_C16 | ((e.flags & B2P_EPI_C16_FP16) ? EK_C16H : 0u);
   if (e.colsum_part) k |= EK_CSUM;
+  if (e.C16b) k |= EK_C16B;
   return k;
 }
 
@@ -59,8 +60,8 @@ static int run(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, uns
 
 int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   const EpiArgs ea = make_epi_args(d);
-  if ((d.ep.colsum_part || d.ep.pre16 || d.ep.aux16) && !ea.vec4) {
-    b2p_set_error("gemm16: colsum_part / pre16 / aux16 need 16-B aligned C-shaped tensors and N %% 4 == 0");
+  if ((d.ep.colsum_part || d.ep.pre16 || d.ep.aux16 || d.ep.C16b) && !ea.vec4) {
+    b2p_set_error("gemm16: colsum_part / pre16 / aux16 / C16b need 16-B aligned C-shaped tensors and N %% 4 == 0");
     return 1;
   }
   const int ks = d.ksplit > 1 ? d.ksplit : 1;

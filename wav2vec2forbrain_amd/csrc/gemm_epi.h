@@ -55,6 +55,7 @@ __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, 
   if (e.residual) v += e.residual[(int64_t)z1 * e.rbs1 + (int64_t)z2 * e.rbs2 + (int64_t)m * e.ldr + n];
   if (e.C) e.C[coff] = v;
   if (e.C16) e.C16[coff] = b2p_16_bits(v, e.flags & B2P_EPI_C16_FP16);
+  if (e.C16b) e.C16b[coff] = b2p_bf16_bits(v);
 }
 
 // Four consecutive columns n .. n+3 of row m (n % 4 == 0), vectorised when ea.vec4 is set.
@@ -123,6 +124,7 @@ __device__ __forceinline__ float4 epilogue_store4(const EpiArgs& a, int z, int z
   if (e.C) *reinterpret_cast<float4*>(e.C + coff) = make_float4(v[0], v[1], v[2], v[3]);
   if (e.C16) *reinterpret_cast<uint2*>(e.C16 + coff) = b2p_pack16x4(make_float4(v[0], v[1], v[2], v[3]),
                                                                        e.flags & B2P_EPI_C16_FP16);
+  if (e.C16b) *reinterpret_cast<uint2*>(e.C16b + coff) = b2p_pack_bf16x4(make_float4(v[0], v[1], v[2], v[3]));
   return make_float4(v[0], v[1], v[2], v[3]);
 }
 
@@ -187,6 +189,7 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
   if (e.act_bwd != B2P_ACT_NONE)
     v = v && (e.aux16 ? ((uintptr_t)e.aux16 & 7u) == 0 : a16(e.aux)) && s4(e.ldaux) && s4(e.abs1) && s4(e.abs2);
   if (e.pre16) v = v && ((uintptr_t)e.pre16 & 7u) == 0;
+  if (e.C16b) v = v && ((uintptr_t)e.C16b & 7u) == 0;
   if (e.residual) v = v && a16(e.residual) && s4(e.ldr) && s4(e.rbs1) && s4(e.rbs2);
   ea.vec4 = v ? 1 : 0;
   ea.epoch = b2p_seed_epoch();

@@ -126,22 +126,23 @@ _FP32_OPS = set(filter(None, os.environ.get("B2P_FP32_OPS", "").split(",")))
 
 @contextlib.contextmanager
 def _fp32_if(name: str):
-    if name in _FP32_OPS:
-        old = _state.block
-        _state.block = name
-        try:
+    old = _state.block
+    _state.block = name
+    try:
+        if name in _FP32_OPS:
             with precision("fp32"):
                 yield
-        finally:
-            _state.block = old
-    else:
-        yield
+        else:
+            yield
+    finally:
+        _state.block = old
 
 
 # error attribution (tools/traj_err.py): with B2P_FP32_BWD=1 a block's backward runs in the precision
 # its forward ran in, so B2P_FP32_OPS=<block> puts that block's forward AND backward in exact fp32
 _BWD_FOLLOWS_FWD = [os.environ.get("B2P_FP32_BWD", "0") == "1"]
 _FP32_BWD_OPS: set = set()   # blocks whose backward follows their forward's precision regardless
+_FP32_BWD_ONLY: set = set()  # blocks whose backward runs in exact fp32 (forward unchanged)
 
 
 def _prec_follow(cls):
@@ -155,6 +156,9 @@ def _prec_follow(cls):
 
     @functools.wraps(bwd)
     def backward(ctx, *grads):
+        if ctx.block in _FP32_BWD_ONLY and _state.prec != 1:
+            with precision("fp32"):
+                return bwd(ctx, *grads)
         if (_BWD_FOLLOWS_FWD[0] or ctx.block in _FP32_BWD_OPS) and ctx.prec_fwd != _state.prec:
             with precision({0: "bf16", 1: "fp32"}[ctx.prec_fwd]):
                 return bwd(ctx, *grads)
@@ -462,7 +466,7 @@ def conv_op(t, off, ld, T_out, T_in, stride, pad, Cg, sample_stride, k_inner=Tru
 def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1, nz2=1, alpha=1.0,
          beta=0.0, bias=None, biasbs1=0, bias_gather=None, pre_out=None, act=0, act_bwd=0, aux=None, ldaux=0, abs1=0, abs2=0,
          drop_p=0.0, seed=0, residual=None, r_off=0, ldr=0, rbs1=0, rbs2=0, timing=0, C16=None, pre16=None,
-         aux16=None, colsum_part=None, c16_fp16=False):
+         aux16=None, colsum_part=None, c16_fp16=False, C16b=None):
     """C may be None when only the bf16 copy C16 (same strides) is wanted. Both operands bf16
     (Operand.dtype 1) selects the LDS-DMA kernel (gemm16.hip)."""
     d = GemmDesc()
@@ -489,6 +493,7 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     e.pre16 = _p(pre16, c_off) if pre16 is not None else None
     e.aux16 = _p(aux16, c_off) if aux16 is not None else None
     e.colsum_part = _p(colsum_part)
+    e.C16b = _p(C16b, c_off) if C16b is not None else None
     e.flags = _lib.EPI_C16_FP16 if c16_fp16 else 0
     d.ep = e
     d.precision = 2 if ((_state.fwd16 and _state.prec == 0 and A.dtype == 0) or A.dtype == 2) else _prec()
@@ -505,7 +510,7 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     d.flops = 2.0 * M * N * K * nz1 * nz2
     ws = None
     plain = (bias is None and pre_out is None and act == 0 and act_bwd == 0 and drop_p == 0.0 and residual is None
-             and colsum_part is None and pre16 is None)
+             and colsum_part is None and pre16 is None and C16b is None)
     if plain and K >= 2048 and not _state.nosplit:
         b16 = A.dtype != 0
         bn = 64 if (N <= 64 and not b16) else 128
@@ -744,21 +749,24 @@ def cast16(x, out=None):
     return out
 
 
-def weight16(*ws):
-    """bf16 copy of fp32 weight(s), rows concatenated ([wq; wk; wv] -> one QKV operand); cached
-    until any source tensor changes (version counter or optimiser epoch)."""
-    key = tuple(id(w) for w in ws)
+def weight16(*ws, half=False):
+    """bf16 (fp16 when half) copy of fp32 weight(s), rows concatenated ([wq; wk; wv] -> one QKV
+    operand); cached until any source tensor changes (version counter or optimiser epoch)."""
+    key = (("H",) if half else ()) + tuple(id(w) for w in ws)
     st = _stamp(ws)
     cache = _cache_ok(ws)
     hit = _W16.get(key) if cache else None
     if hit is not None and hit[0] == st:
         return hit[1]
     rows = sum(w.shape[0] for w in ws)
-    out = torch.empty((rows,) + tuple(ws[0].shape[1:]), device=ws[0].device, dtype=BF16)
+    out = torch.empty((rows,) + tuple(ws[0].shape[1:]), device=ws[0].device, dtype=torch.float16 if half else BF16)
     off = 0
     for w in ws:
         _chk(w, "weight16")
-        _lib.call("b2p_cast_bf16", _p(w), _p(out, off), w.numel(), _st())
+        if half:
+            _lib.call("b2p_cast16_2d", _p(w), 1, w.numel(), w.numel(), _p(out, off), w.numel(), 1, _st())
+        else:
+            _lib.call("b2p_cast_bf16", _p(w), _p(out, off), w.numel(), _st())
         off += w.numel()
     if cache:
         _W16[key] = (st, out)
@@ -818,6 +826,21 @@ def to16(x):
     if t is not None and t[0] == x._version:
         return t[1]
     return cast16(x.contiguous())
+
+
+def attach16h(x, xh) -> None:
+    """Marks xh as the fp16 copy of x (the forward_f16 GEMM operand), beside attach16's bf16 copy."""
+    x._h16 = (x._version, xh)
+
+
+def to16h(x):
+    t = getattr(x, "_h16", None)
+    if t is not None and t[0] == x._version:
+        return t[1]
+    xc = x.contiguous()
+    out = torch.empty(xc.shape, device=x.device, dtype=torch.float16)
+    _lib.call("b2p_cast16_2d", _p(xc), 1, xc.numel(), xc.numel(), _p(out), xc.numel(), 1, _st())
+    return out
 
 
 def _ln_fwd16(x2d, g, b, eps, drop_p=0.0, seed=0):
@@ -1787,9 +1810,12 @@ class _EncoderLayer16(torch.autograd.Function):
         dev = x.device
         x2 = x.view(NT, D)
         x16 = to16(x).view(NT, D)
-        wqkv16 = weight16(wq, wk, wv)
         bqkv = bias_cat(bq, bk, bv) if any(b is not None for b in (bq, bk, bv)) else None
         fused = attn16_ok(T, dh)
+        if fused and ATTN_F16 and _state.fwd16:
+            return _EncoderLayer16._forward_f16(ctx, x, x16, cfg, bqkv, B, T, D, nh, dh, wq, bq, wk, bk, wv, bv, wo,
+                                                bo, g1, be1, w1, b1, w2, b2, g2, be2)
+        wqkv16 = weight16(wq, wk, wv)
         Oh = None
         if fused:
             if ATTN_F16:   # fp16 attention operand (the saved qkv: the backward recomputes from it)
@@ -1834,6 +1860,51 @@ class _EncoderLayer16(torch.autograd.Function):
         ctx.has_b = [b is not None for b in (bq, bk, bv, bo, b1, b2)]
         res = out.view(B, T, D)
         attach16(res, out16.view(B, T, D))
+        return res
+
+    @staticmethod
+    def _forward_f16(ctx, x, x16, cfg, bqkv, B, T, D, nh, dh, wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2,
+                     g2, be2):
+        """forward_f16: every GEMM operand of the layer in fp16 (the QKV, out-projection and FFN inputs and
+        weights; 11 significant bits instead of bf16's 8, same MFMA rate). The producers write the
+        backward's bf16 operands beside the fp16 ones (LayerNorm: y16b; FFN1 epilogue: C16b; attention:
+        Ob), so the backward is the bf16 one, unchanged."""
+        nh, eps, p_attn, p_hid, p_act, seeds = cfg
+        NT = B * T
+        F = w1.shape[0]
+        dev = x.device
+        x2 = x.view(NT, D)
+        xh = to16h(x).view(NT, D)
+        qkv = torch.empty(NT, 3 * D, device=dev, dtype=torch.float16)
+        gemm(NT, 3 * D, D, op(xh, 0, D, True), op(weight16(wq, wk, wv, half=True), 0, D, True), None, 3 * D,
+             bias=bqkv, C16=qkv, c16_fp16=True)
+        Oh, O16, P, Pd = _attn16_fwd_f16(qkv, B, T, nh, dh, p_attn, seeds[0])
+        y1 = torch.empty(NT, D, device=dev)
+        gemm(NT, D, D, op(Oh, 0, D, True), op(weight16(wo, half=True), 0, D, True), y1, D, bias=bo, drop_p=p_hid,
+             seed=seeds[1], residual=x2)
+        del Oh
+        x1, x1h, m1, r1, x1_16 = _ln_fwd_x16(y1, g1, be1, eps, True, want32=True, want_b16=True)
+        pre = torch.empty(NT, F, device=dev, dtype=BF16)        # bf16 pre-activation: GELU' operand
+        fh = torch.empty(NT, F, device=dev, dtype=torch.float16)
+        f16 = torch.empty(NT, F, device=dev, dtype=BF16)       # the dW2 operand
+        gemm(NT, F, D, op(x1h, 0, D, True), op(weight16(w1, half=True), 0, D, True), None, F, bias=b1, pre16=pre,
+             act=ACT["gelu"], drop_p=p_act, seed=seeds[2], C16=fh, c16_fp16=True, C16b=f16)
+        del x1h
+        y2 = torch.empty(NT, D, device=dev)
+        gemm(NT, D, F, op(fh, 0, F, True), op(weight16(w2, half=True), 0, F, True), y2, D, bias=b2, drop_p=p_hid,
+             seed=seeds[3], residual=x1)
+        del x1, fh
+        out, outh, m2, r2, out16 = _ln_fwd_x16(y2, g2, be2, eps, True, want32=True, want_b16=True)
+        ctx.save_for_backward(x16, qkv, P, Pd, O16, y1, x1_16, m1, r1, pre, f16, y2, m2, r2,
+                              wq, wk, wv, wo, g1, w1, w2, g2)
+        ctx.cfg = cfg
+        ctx.shape = (B, T, D)
+        ctx.fused = True
+        ctx.prm = (wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2)
+        ctx.has_b = [b is not None for b in (bq, bk, bv, bo, b1, b2)]
+        res = out.view(B, T, D)
+        attach16(res, out16.view(B, T, D))
+        attach16h(res, outh.view(B, T, D))
         return res
 
     @staticmethod
