@@ -81,8 +81,11 @@ SHAPES = [
 if __name__ == "__main__":
     tag = " ".join(f"{k}={v}" for k, v in sorted(os.environ.items()) if k.startswith("B2P_GEMM16"))
     tot = 0.0
+    only = os.environ.get("GEMM_AB_ONLY")   # e.g. 3072x768x7968
     with Fn.precision("bf16"):
         for M, N, K, epi, ak, bk in SHAPES:
+            if only and f"{M}x{N}x{K}" not in only.split(","):
+                continue
             us, tf = case(M, N, K, epi, ak, bk)
             tot += us
             print(f"[{tag or 'default'}] {M}x{N}x{K} {epi:5s} {'A' if ak else 'a'}{'B' if bk else 'b'}: "

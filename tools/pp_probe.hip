@@ -37,6 +37,10 @@ int main(int argc, char** argv) {
   }
   d.ep.act = act;
   d.ep.ldc = N; d.ep.alpha = 1.f;
+  if (getenv("PP_DIAG")) {   // K-loop ablation (gemm16_impl.inc g_pp_diag)
+    const int dg = atoi(getenv("PP_DIAG"));
+    hipMemcpyToSymbol(HIP_SYMBOL(g_pp_diag), &dg, sizeof(dg));
+  }
   hipEvent_t e0, e1;
   hipEventCreate(&e0); hipEventCreate(&e1);
   for (int it = 0; it < 5; ++it) b2p_gemm16_launch(d, 0);

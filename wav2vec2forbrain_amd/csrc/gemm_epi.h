@@ -4,6 +4,7 @@
 #pragma once
 #include "common.h"
 #include "../../include/b2p_hip.h"
+#include <stdlib.h>
 
 namespace {
 
