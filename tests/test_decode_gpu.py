@@ -170,6 +170,42 @@ def test_ctc_prefix_beam_matches_oracle(beam, tmin, prune):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("tmin,prune,nb", [(-5.0, -10.0, 8), (-1e30, -1e30, 2)])
+def test_ctc_prefix_beam_production_settings(tmin, prune, nb):
+    """The reference's test decoding settings: beam 100 (pyctcdecode's default
+    lm_decode_beam_width, /root/reference/src/train/evaluator.py:189-198), T' = 249 frames (a
+    1,000-bin window), B = 8, the 32-token character vocabulary, ragged lengths, pyctcdecode's pruning
+    constants and none. Device search == oracle (best prefix and its log probability); the device time
+    of a B = 8 and a B = 32 batch is printed."""
+    from wav2vec2forbrain_amd import functional as Fn
+    from oracle.ctc_beam_oracle import ctc_prefix_beam
+    g = torch.Generator().manual_seed(11)
+    B, T, C = 8, 249, 32
+    logits = torch.randn(B, T, C, generator=g) * 2.5
+    logits[:, :, 0] += 2.0
+    lens = torch.tensor([249, 249, 240, 200, 249, 131, 249, 64], dtype=torch.int32)
+    tok, n, score = Fn.ctc_prefix_beam(logits.cuda(), lens.cuda(), beam=100, token_min_logp=tmin,
+                                       beam_prune_logp=prune)
+    tok, n, score = tok.cpu().numpy(), n.cpu().numpy(), score.cpu().numpy()
+    for b in range(nb):
+        ref, ref_score = ctc_prefix_beam(logits[b].numpy(), 100, 0, tmin, prune, int(lens[b]))
+        assert tuple(tok[b, :n[b]]) == ref, (b, tok[b, :n[b]], ref)
+        assert abs(float(score[b]) - float(ref_score)) <= 1e-4 * max(1.0, abs(float(ref_score))), (b, score[b], ref_score)
+    for bb in (8, 32):
+        lg = (torch.randn(bb, T, C, generator=g) * 2.5).cuda()
+        Fn.ctc_prefix_beam(lg, beam=100, token_min_logp=tmin, beam_prune_logp=prune)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(5):
+            Fn.ctc_prefix_beam(lg, beam=100, token_min_logp=tmin, beam_prune_logp=prune)
+        e1.record()
+        torch.cuda.synchronize()
+        print(f"ctc_prefix_beam beam 100 T 249 C 32 B {bb} prune ({tmin:g}, {prune:g}): "
+              f"{e0.elapsed_time(e1) / 5:.3f} ms per batch")
+
+
+@pytest.mark.gpu
 def test_ctc_prefix_beam_peaked_path_equals_greedy():
     """With one dominant class per frame the beam search returns the greedy (collapsed) path."""
     from wav2vec2forbrain_amd import functional as Fn

@@ -33,6 +33,22 @@ from .. import functional as Fn
 _CAPTURE_STREAMS: dict = {}
 
 
+def live_graph_nodes(module_prefix: str = "wav2vec2forbrain_amd") -> int:
+    """Number of live autograd nodes of custom Functions defined under module_prefix (the backward
+    contexts of this package's fused ops). A node outlives its step when the caller still holds a
+    graph output (a loss or logits with grad_fn) or retained the graph; capturing a step then
+    segfaulted inside hipStreamEndCapture (round 3, test_trainer_replay_matches_eager)."""
+    import gc
+    gc.collect()
+    n = 0
+    for o in gc.get_objects():
+        if isinstance(o, torch.autograd.function.BackwardCFunction):
+            cls = getattr(o, "_forward_cls", None)
+            if cls is not None and cls.__module__.startswith(module_prefix):
+                n += 1
+    return n
+
+
 def _capture_stream(dev, prio: bool):
     key = (str(dev), prio)
     s = _CAPTURE_STREAMS.get(key)
@@ -59,6 +75,11 @@ class StepGraph:
         self.epoch = epoch
 
     def capture(self) -> None:
+        live = live_graph_nodes()
+        if live:
+            raise RuntimeError(
+                f"StepGraph.capture: {live} autograd nodes of an earlier step are still alive (an output "
+                "with grad_fn is held, or a graph was retained); detach or drop them before capturing")
         dev = torch.device("cuda", torch.cuda.current_device())
         lib = _lib.load()
         if self.epoch is None:
