@@ -30,6 +30,12 @@ def main():
     for g, p, n in sorted(gaps, key=lambda x: -x[0])[:10]:
         print(f"  gap {g / 1e3:8.1f} us  after {str(p).replace('(anonymous namespace)::', '')[:55]}  "
               f"before {n.replace('(anonymous namespace)::', '')[:55]}")
+    # the torch kernels of the step with their neighbours (what launched them)
+    for i, k in enumerate(step):
+        if "at::native" in k[0] or "rocclr" in k[0]:
+            nb = lambda x: x.replace("(anonymous namespace)::", "")[:48]
+            print(f"  torch: {nb(k[0])}  after {nb(step[i - 1][0]) if i else '-'}  before "
+                  f"{nb(step[i + 1][0]) if i + 1 < len(step) else '-'}")
     agg = {}
     for k in step:
         n = k[0].replace("(anonymous namespace)::", "")

@@ -1323,6 +1323,7 @@ class _Linear(torch.autograd.Function):
         ctx.save_for_backward(x, W, pre)
         ctx.act = act
         ctx.has_b = b is not None
+        ctx.prm = (W, b)
         return out
 
     @staticmethod
@@ -1342,6 +1343,7 @@ class _Linear(torch.autograd.Function):
         if ctx.has_b and ctx.needs_input_grad[2]:
             db = torch.empty(N, device=x.device)
             colsum(dy, dy.numel() // N, N, db)
+        dW, db = _defer_small(ctx.prm, (dW, db))   # frozen: one batched side-stream add, not autograd's
         return dx, dW, db, None
 
 
@@ -1470,6 +1472,7 @@ class _PosConvLN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, e, wg, wv, cbias, ln_g, ln_b, groups, eps, drop_p, seed):
         _chk(e, "pos_conv.x")
+        ctx.prm = (wg, wv, cbias, ln_g, ln_b)
         B, T, D = e.shape
         O, Ig, K = wv.shape            # (D, D/groups, k)
         dev = e.device
@@ -1545,6 +1548,7 @@ class _PosConvLN(torch.autograd.Function):
             A = conv_op(dpre, 0, D, T, T, 1, K - 1 - pad, Og, T * D, True, bs1=Og)
             gemm(B * T, Ig, K * Og, A, op(wt, 0, K * Og, True, bs1=Ig * K * Og), de, D, cbs1=Ig, nz1=groups,
                  residual=dxsum, rbs1=Ig, ldr=D)
+        dg, dv, dcb, dlg, dlb = _defer_small(ctx.prm, (dg, dv, dcb, dlg, dlb))
         return de, dg, dv, dcb, dlg, dlb, None, None, None, None
 
 
