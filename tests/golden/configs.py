@@ -14,6 +14,10 @@ CONFIGS = [
     dict(name="plumbing_base", seed=42, B=2, L=512, in_lens=[512, 384], tgt_range=(20, 50), hidden_size=768,
          layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2, bidirectional=True,
          fc_hidden=[], learnable_h0=False, full_grad_max=4096, infeasible=False),
+    # the base architecture on 1,280-bin windows (T' = 313 frames: the 512-key fused attention class)
+    dict(name="base_L1280", seed=50, B=2, L=1280, in_lens=[1280, 1100], tgt_range=(30, 60), hidden_size=768,
+         layers=12, heads=12, ffn=3072, pos_k=128, pos_groups=16, gru_hidden=256, gru_layers=2, bidirectional=True,
+         fc_hidden=[], learnable_h0=False, full_grad_max=4096, infeasible=False, long=True),
     # Conformer (rotary) tiny: every conformer code path, full small gradients
     dict(name="tiny_conf", seed=44, B=2, L=96, in_lens=[96, 88], tgt_range=(2, 8), hidden_size=64, layers=2,
          heads=4, ffn=128, pos_k=16, pos_groups=4, gru_hidden=32, gru_layers=2, bidirectional=True, fc_hidden=[48],

@@ -212,7 +212,7 @@ def _keep_mask_ref(seed, p, B, nh, T):
 
 
 @pytest.mark.parametrize("B,T,nh,p", [(2, 249, 12, 0.0), (2, 249, 12, 0.1), (3, 100, 4, 0.1), (1, 17, 2, 0.0),
-                                       (2, 256, 3, 0.1)])
+                                       (2, 256, 3, 0.1), (2, 313, 4, 0.1), (1, 257, 2, 0.0), (1, 512, 2, 0.1)])
 @pytest.mark.parametrize("variant", ["hash", "mask", "epoch", "f16"])
 def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
     """csrc/attn16.hip (bf16 MFMA, scores on-chip) vs the unfused fp32 attention core (GEMM ->
@@ -222,7 +222,9 @@ def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
     (must equal the re-hashed result bit for bit); epoch = both paths under a graph-replay seed
     counter (the fused forward, fused backward and unfused kernels must offset the seed alike);
     f16 = the bf16 precision mode's default: fp16 forward operands (b2p_attn16_fwd_f16, O in fp16 plus
-    its bf16 copy) and the backward recomputing the scores from them (b2p_attn16_bwd_f16)."""
+    its bf16 copy) and the backward recomputing the scores from them (b2p_attn16_bwd_f16).
+    T' in 257..512 runs the 512-key kernels (K / V 128 KB of LDS; no stored keep mask, the backward
+    rehashes; dQ recomputes the scores in a second pass), T' = 313 being a 1,280-bin window."""
     import ctypes
     Fn = _fn()
     torch.manual_seed(7)
@@ -248,7 +250,7 @@ def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
             O16, lse2, mask = Fn._attn16_fwd(q16, B, T, nh, dh, p, seed, want_mask=True)
         dq32, dq16 = Fn._attn16_bwd(q16, dO.to(torch.bfloat16), lse2, B, T, nh, dh, p, seed,
                                     mask=mask if variant in ("mask", "f16") else None)
-        if variant == "mask" and p > 0:
+        if variant == "mask" and p > 0 and mask is not None:
             h32, _ = Fn._attn16_bwd(q16, dO.to(torch.bfloat16), lse2, B, T, nh, dh, p, seed)
             # the keep bits the forward stored are the hash mask, bit for bit (integer check against
             # a numpy restatement of b2p_keep); the two backward forms then differ only by the

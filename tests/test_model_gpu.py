@@ -32,13 +32,14 @@ def _run(name, mode):
     return model, out
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "base_L1280", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
                                   "base_bs32", "conformer_large_bs32", "large960_bs32", "conformer_large_ft_bs8"])
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
 def test_step_matches_reference_golden(name, mode):
     """One deterministic training step (forward, CTC, backward) vs the reference's own modules run on
     the same weights and inputs (tests/golden/make_golden.py). base_bs32 / conformer_large_bs32 are
     the bench workloads themselves (BASELINE configs[1] / configs[2], bs=32, 1024-bin windows);
+    base_L1280 runs 1,280-bin windows (T' = 313: the 512-key fused attention class);
     large960_bs32 is configs[3] per GPU (wav2vec2-large-960h, post-LN, 32 x 1024) and
     conformer_large_ft_bs8 configs[4] per GPU (8 x 1024, two padded samples)."""
     fx = load_fixture(name)

@@ -10,7 +10,7 @@ import torch
 from tests.helpers import CFG, load_fixture, oracle_cfg, oracle_state, batch_dict, build_model
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "base_L1280", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
                                   "base_bs32", "conformer_large_bs32", "large960_bs32", "conformer_large_ft_bs8"])
 def test_state_dict_keys_match_reference(name):
     fx = load_fixture(name)
@@ -24,7 +24,7 @@ def test_state_dict_keys_match_reference(name):
 _SLOW = pytest.mark.skipif(os.environ.get("B2P_SLOW_ORACLE") != "1", reason="set B2P_SLOW_ORACLE=1")
 
 
-@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_b", "plumbing_base", "base_L1280", "tiny_conf", "conformer_large_b2", "tiny_stable", "plumbing_stable",
                                   "base_bs32", pytest.param("conformer_large_bs32", marks=_SLOW),
                                   pytest.param("large960_bs32", marks=_SLOW),
                                   pytest.param("conformer_large_ft_bs8", marks=_SLOW)])
@@ -53,8 +53,9 @@ def test_oracle_matches_reference_golden(name):
         ref_norm = float(fx["gnorm/" + n])
         # gradients that are mathematically ~0 (e.g. attention key bias) are compared absolutely
         assert abs(float(g.double().norm()) - ref_norm) <= 1e-4 * ref_norm + 1e-6 * gmax, n
-        # fp32 summation-order noise through 24 layers at bs=32 reaches ~1.3e-6 * gmax on single entries
-        atol = (3e-6 if cfg.get("big") else 1e-6) * gmax
+        # fp32 summation-order noise through 24 layers at bs=32 reaches ~1.3e-6 * gmax on single entries;
+        # through the 313-step GRU recurrence of the 1,280-bin windows 3.6e-6 * gmax (one GRU bias entry)
+        atol = (3e-6 if cfg.get("big") else 5e-6 if cfg.get("long") else 1e-6) * gmax
         if "grad/" + n in fx:
             np.testing.assert_allclose(g.numpy(), fx["grad/" + n], rtol=1e-3, atol=atol, err_msg=n)
         else:

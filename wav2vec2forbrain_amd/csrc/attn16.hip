@@ -2,8 +2,9 @@
 // softmax(Q K^T * scale) -> dropout -> @ V, no mask (reference: HF Wav2Vec2Attention / eager
 // attention, TF w2v:438-463,529-545; Conformer TF conf:458-470). bf16 precision mode only.
 //
-// T' (= 249 frames at the 1024-bin windows) <= 256 and head size 64, so one (batch, head)'s whole
-// K and V fit in 64 KB of LDS: no online softmax is needed. Scores never touch HBM (the unfused
+// T' <= 512 and head size 64 (TM = 256: T' = 249 frames at the 1024-bin windows; TM = 512: windows up
+// to 2,080 bins), so one (batch, head)'s whole K and V fit in 64 / 128 KB of LDS: no online softmax is
+// needed. Scores never touch HBM (the unfused
 // path writes and re-reads a (B, heads, T', T') fp32 tensor ~6 times per layer).
 //   fwd   (b, h, 128-query block): S^T = K Q^T (keys in registers, query on the lane), in-register
 //         softmax (2 cross-lane shuffles per reduction), O^T = V^T P^T with P^T taken straight
@@ -22,7 +23,7 @@
 
 namespace {
 constexpr int DH = 64;     // head size
-constexpr int TMAX = 256;  // max sequence length (keys / queries)
+constexpr int TMAX = 256;  // sequence-length class of the stored keep mask (keys / queries <= 256)
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 constexpr float LOG2E = 1.4426950408889634f;
@@ -75,12 +76,13 @@ __device__ __forceinline__ bf16x8 pack_acc_t(const f32x4& a, const f32x4& b) {
 }
 __device__ __forceinline__ float exp2_fast(float x) { return __builtin_amdgcn_exp2f(x); }
 
-// Load rows [0, 256) of a head slice (64 bf16 at column `col` of a row-major [B*T][ld] bf16
+// Load rows [0, TM) of a head slice (64 bf16 at column `col` of a row-major [B*T][ld] bf16
 // matrix) into an LDS image; rows >= T are zero. 256 threads, 8 chunks of 16 B each.
+template <int TM>
 __device__ __forceinline__ void load_image(char* img, const uint16_t* base, int64_t row0, int T, int64_t ld, int col,
                                            int tid) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < TM / 32; ++k) {
     const int idx = tid + 256 * k;
     const int r = idx >> 3, c = idx & 7;
     uint4 v = make_uint4(0, 0, 0, 0);
@@ -102,11 +104,11 @@ __device__ __forceinline__ bf16x8 to_b16(const bf16x8& x) {
   else return x;
 }
 // load_image with each 16-B chunk converted fp16 -> bf16 on the way (H), else a plain copy
-template <bool H>
+template <bool H, int TM>
 __device__ __forceinline__ void load_image_b16(char* img, const uint16_t* base, int64_t row0, int T, int64_t ld,
                                                int col, int tid) {
 #pragma unroll
-  for (int k = 0; k < 8; ++k) {
+  for (int k = 0; k < TM / 32; ++k) {
     const int idx = tid + 256 * k;
     const int r = idx >> 3, c = idx & 7;
     bf16x8 v = bf16x8{};
@@ -179,10 +181,12 @@ __device__ __forceinline__ uint32_t keep4_bits(uint32_t key_lo, uint32_t k32, ui
          ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
 }
 
-template <int DM, bool H>   // DM 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward
+template <int DM, bool H, int TM>   // DM 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward
 __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
                                                        uint16_t* __restrict__ Ob16, float* __restrict__ lse2, int T,
                                                        int nh, float scale, DropCfg dc, uint32_t* __restrict__ maskw) {
+  static_assert(TM == TMAX || DM != 2, "the stored keep mask covers T <= 256");
+  constexpr int NKT = TM / 16;   // key tiles
   constexpr bool DROP = DM != 0;
   if (b2p_gated_off(dc.gate)) return;   // LayerDrop: this replay skips the layer (outputs unused)
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
@@ -203,8 +207,8 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) qf[ks] = q < T ? gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g) : bf16x8{};
   }
-  load_image(smem, qkv, row0, T, ld, D + h * DH, tid);
-  load_image(smem + TMAX * 128, qkv, row0, T, ld, 2 * D + h * DH, tid);
+  load_image<TM>(smem, qkv, row0, T, ld, D + h * DH, tid);
+  load_image<TM>(smem + TM * 128, qkv, row0, T, ld, 2 * D + h * DH, tid);
   __syncthreads();
   const float c2 = scale * LOG2E;
   const uint32_t k32 = (uint32_t)dc.seed ^ b2p_mix32((uint32_t)(dc.seed >> 32) + 0x9E3779B9u);   // b2p_hash key
@@ -215,7 +219,7 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     uint32_t obase = 0;
     asm volatile("" : "+v"(obase));
     const char* Kimg = smem + obase;
-    const char* Vimg = smem + TMAX * 128 + obase;
+    const char* Vimg = smem + TM * 128 + obase;
     const int q = qt * 16 + lr;
     const bool qok = q < T;
     if (qt != qt0) {
@@ -223,9 +227,9 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
       for (int ks = 0; ks < 2; ++ks) qf[ks] = qok ? gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g) : bf16x8{};
     }
     // S^T: tile kt = keys kt*16 + 4g + i (registers) x query q (lane)
-    f32x4 s[16];
+    f32x4 s[NKT];
 #pragma unroll
-    for (int kt = 0; kt < 16; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
       s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) s[kt] = mfma_t<H>(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], s[kt]);
@@ -234,7 +238,7 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     // that hold them (wave-uniform test), the scale is folded into the exponent's FMA
     float m = -INFINITY;
 #pragma unroll
-    for (int kt = 0; kt < 16; ++kt) {
+    for (int kt = 0; kt < NKT; ++kt) {
       if (kt * 16 + 16 <= T) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) m = fmaxf(m, s[kt][i]);
@@ -252,7 +256,7 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     const float mc = m * c2;
     float sum = 0.f;
 #pragma unroll
-    for (int kt = 0; kt < 16; ++kt)
+    for (int kt = 0; kt < NKT; ++kt)
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const float e = exp2_fast(fmaf(s[kt][i], c2, -mc));
@@ -271,7 +275,7 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
     uint32_t mbits[2] = {0u, 0u};   // this lane's keep bits: byte c = keys 32c + 4g + i (bit i), +16 (bit 4 + i)
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < NKT / 2; ++c) {
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const int key0 = (2 * c + half) * 16 + 4 * g;
@@ -314,18 +318,19 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
 // bf16) columns [D + h*64, ...) and [2D + h*64, ...). One workgroup per (batch, head, 128 keys): Q and
 // dO are staged once for 128 keys (4 waves x key tiles w and w + 4).
 constexpr int BWD_KB = 128;
-template <int DM, bool H>   // DM 0: no dropout, 1: hash the keep mask, 2: keep bits in memory; H: fp16 qkv
+template <int DM, bool H, int TM>   // DM 0: no dropout, 1: hash the keep mask, 2: keep bits in memory; H: fp16 qkv
 __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restrict__ qkv, const float* __restrict__ delta,
                                                         const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                         float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
                                                         int nh, float scale, DropCfg dc,
                                                         const uint32_t* __restrict__ maskw) {
+  static_assert(TM == TMAX || DM != 2, "the stored keep mask covers T <= 256");
   constexpr bool DROP = DM != 0;
   dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  float* lse_s = reinterpret_cast<float*>(smem + 2 * TMAX * 128);
-  float* del_s = lse_s + TMAX;
-  uint32_t* msk_s = reinterpret_cast<uint32_t*>(del_s + TMAX);   // [q][4]: this block's 128 keys' bits
+  float* lse_s = reinterpret_cast<float*>(smem + 2 * TM * 128);
+  float* del_s = lse_s + TM;
+  uint32_t* msk_s = reinterpret_cast<uint32_t*>(del_s + TM);   // [q][4]: this block's 128 keys' bits (TM 256)
   const int nkb = (T + BWD_KB - 1) / BWD_KB;
   const int bhi = blockIdx.x / nkb, kb = blockIdx.x - bhi * nkb;
   const int b = bhi / nh, h = bhi - b * nh;
@@ -340,10 +345,9 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
     }
     return;
   }
-  load_image(smem, qkv, row0, T, ld, h * DH, tid);
-  load_image(smem + TMAX * 128, dO16, row0, T, D, h * DH, tid);
-  {
-    const int qq = tid;   // one thread per query row: row constants lse2 and delta (from the dQ pass)
+  load_image<TM>(smem, qkv, row0, T, ld, h * DH, tid);
+  load_image<TM>(smem + TM * 128, dO16, row0, T, D, h * DH, tid);
+  for (int qq = tid; qq < TM; qq += 256) {   // one thread per query row: lse2 and delta (from the dQ pass)
     const int64_t o = ((int64_t)b * nh + h) * T + qq;
     del_s[qq] = qq < T ? delta[o] : 0.f;
     lse_s[qq] = qq < T ? lse2[o] : 0.f;
@@ -361,7 +365,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
     uint32_t obase = 0;   // opaque image bases: no hoisting of the unrolled body's LDS addresses
     asm volatile("" : "+v"(obase));
     const char* Qimg = smem + obase;
-    const char* dOimg = smem + TMAX * 128 + obase;
+    const char* dOimg = smem + TM * 128 + obase;
     const int key = kt * 16 + lr;
     const bool kok = key < T;
     const int kw = (key >> 2) & 3;                 // this key's word among the block's 4 (its lane group)
@@ -434,7 +438,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
 // rounding — otherwise the residual feeds a systematic, Q-correlated error into dK. Pass 1 keeps
 // P and dP*keep in registers, pass 2 forms dS and dQ^T += K^T dS^T. One workgroup per (batch, head,
 // 128 queries): K and V staged once, 4 waves x query tiles w and w + 4.
-template <int DM, bool H>   // DM 0: no dropout, 1: hash the keep mask, 2: keep bits in memory; H: fp16 qkv
+template <int DM, bool H, int TM>   // DM 0: no dropout, 1: hash the keep mask, 2: keep bits in memory; H: fp16 qkv
 __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restrict__ qkv, float* __restrict__ delta,
                                                        const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                        float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
@@ -454,8 +458,9 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
     for (int half = 0; half < FWD_QB / 64; ++half) zero_block(dqkv, dqkv16, row0, qh * FWD_QB + 64 * half, T, ld, h * DH, tid);
     return;
   }
-  load_image(smem, qkv, row0, T, ld, D + h * DH, tid);                        // K (as stored: S = Q K^T)
-  load_image_b16<H>(smem + TMAX * 128, qkv, row0, T, ld, 2 * D + h * DH, tid);  // V in bf16 (dP = dO V^T)
+  static_assert(TM == TMAX || DM != 2, "the stored keep mask covers T <= 256");
+  load_image<TM>(smem, qkv, row0, T, ld, D + h * DH, tid);                        // K (as stored: S = Q K^T)
+  load_image_b16<H, TM>(smem + TM * 128, qkv, row0, T, ld, 2 * D + h * DH, tid);  // V in bf16 (dP = dO V^T)
   __syncthreads();
   const float c2 = scale * LOG2E;
   const int TP = T + (T & 1);
@@ -464,7 +469,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
     uint32_t obase = 0;   // opaque image bases: no hoisting of the unrolled body's LDS addresses
     asm volatile("" : "+v"(obase));
     const char* Kimg = smem + obase;
-    const char* Vimg = smem + TMAX * 128 + obase;
+    const char* Vimg = smem + TM * 128 + obase;
     const int q = qt * 16 + lr;
     const bool qok = q < T;
     bf16x8 qf[2], df[2];
@@ -479,6 +484,60 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
     const int64_t rowc = ((int64_t)b * nh + h) * T + (qok ? q : 0);
     const float ls = qok ? lse2[rowc] : 0.f;
     const uint64_t rowidx = (uint64_t)rowc * (uint64_t)TP;
+    if constexpr (TM > TMAX) {
+      // T' > 256: the per-key P / dP*keep of 32 key tiles do not fit in registers beside the rest, so pass 1
+      // forms delta and pass 2 recomputes S and dP per 32-key chunk (6 -> 10 MFMAs per key tile)
+      auto sdp = [&](int kt, f32x4& p4, f32x4& pd4) __attribute__((always_inline)) {
+        f32x4 sv = f32x4{0.f, 0.f, 0.f, 0.f}, dp = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          sv = mfma_t<H>(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], sv);
+          dp = mfma(row_frag(Vimg, kt * 16 + lr, 32 * ks + 8 * g), df[ks], dp);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int key = kt * 16 + 4 * g + i;
+          const bool ok = qok && key < T;
+          p4[i] = ok ? exp2_fast(fmaf(sv[i], c2, -ls)) : 0.f;
+          pd4[i] = ok ? dp[i] * keep_scale<DROP>(dc, rowidx + key) : 0.f;
+        }
+      };
+      float dl = 0.f;
+#pragma unroll 2
+      for (int kt = 0; kt < TM / 16; ++kt) {
+        f32x4 p4, pd4;
+        sdp(kt, p4, pd4);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dl += p4[i] * pd4[i];
+      }
+      dl += __shfl_xor(dl, 16, 64);
+      dl += __shfl_xor(dl, 32, 64);
+      if (qok && g == 0) delta[rowc] = dl;
+      f32x4 dq[4];
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 2
+      for (int c = 0; c < TM / 32; ++c) {
+        f32x4 ds[2];
+#pragma unroll
+        for (int half = 0; half < 2; ++half) {
+          f32x4 p4, pd4;
+          sdp(2 * c + half, p4, pd4);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ds[half][i] = p4[i] * (pd4[i] - dl);
+        }
+        const bf16x8 bs = pack_acc(ds[0], ds[1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          dq[dt] = mfma(to_b16<H>(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr)), bs, dq[dt]);
+      }
+      if (qok) {
+        const int64_t r = (row0 + q) * ld + h * DH;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) store_out(dqkv, dqkv16, r + dt * 16 + 4 * g, dq[dt], scale);
+      }
+      continue;
+    }
     uint2 mw = make_uint2(0u, 0u);   // this lane's keep bytes of the query row (keys kt*16 + 4g + i)
     if (DM == 2 && qok) mw = *reinterpret_cast<const uint2*>(maskw + (int64_t)rowc * 8 + 2 * g);
     f32x4 P[16], PD[16];
@@ -540,38 +599,37 @@ DropCfg drop_cfg(float p, uint64_t seed) {
   d.scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
   return d;
 }
-constexpr size_t FWD_LDS = 2 * TMAX * 128;
-constexpr size_t BWD_LDS = 2 * TMAX * 128 + 2 * TMAX * 4 + 4 * TMAX * 4;
+template <int TM>
+constexpr size_t fwd_lds() { return 2 * TM * 128; }
+template <int TM>
+constexpr size_t bwd_lds() { return 2 * TM * 128 + 2 * TM * 4 + (TM == TMAX ? 4 * TM * 4 : 0); }
 
 template <typename K>
 int set_lds(K kern, size_t bytes) {
   B2P_CHECK_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
   return 0;
 }
+template <bool H, int TM>
+int init_attrs_t() {
+  int rc = 0;
+  rc |= set_lds(attn16_fwd_k<0, H, TM>, fwd_lds<TM>());
+  rc |= set_lds(attn16_fwd_k<1, H, TM>, fwd_lds<TM>());
+  rc |= set_lds(attn16_bwd_dkv_k<0, H, TM>, bwd_lds<TM>());
+  rc |= set_lds(attn16_bwd_dkv_k<1, H, TM>, bwd_lds<TM>());
+  rc |= set_lds(attn16_bwd_dq_k<0, H, TM>, fwd_lds<TM>());
+  rc |= set_lds(attn16_bwd_dq_k<1, H, TM>, fwd_lds<TM>());
+  if constexpr (TM == TMAX) {
+    rc |= set_lds(attn16_fwd_k<2, H, TM>, fwd_lds<TM>());
+    rc |= set_lds(attn16_bwd_dkv_k<2, H, TM>, bwd_lds<TM>());
+    rc |= set_lds(attn16_bwd_dq_k<2, H, TM>, fwd_lds<TM>());
+  }
+  return rc;
+}
 int init_attrs() {
   static int done = -1;
   if (done >= 0) return done;
-  int rc = 0;
-  rc |= set_lds(attn16_fwd_k<0, false>, FWD_LDS);
-  rc |= set_lds(attn16_fwd_k<1, false>, FWD_LDS);
-  rc |= set_lds(attn16_fwd_k<2, false>, FWD_LDS);
-  rc |= set_lds(attn16_fwd_k<0, true>, FWD_LDS);
-  rc |= set_lds(attn16_fwd_k<1, true>, FWD_LDS);
-  rc |= set_lds(attn16_fwd_k<2, true>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<0, false>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<1, false>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<2, false>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<0, false>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<1, false>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<2, false>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<0, true>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<1, true>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dkv_k<2, true>, BWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<0, true>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<1, true>, FWD_LDS);
-  rc |= set_lds(attn16_bwd_dq_k<2, true>, FWD_LDS);
-  done = rc;
-  return rc;
+  done = init_attrs_t<false, 256>() | init_attrs_t<true, 256>() | init_attrs_t<false, 512>() | init_attrs_t<true, 512>();
+  return done;
 }
 }  // namespace
 
@@ -580,7 +638,8 @@ int attn16_fwd_launch(bool half, const void* qkv16, void* O16, void* Ob16, float
                       int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
                       b2p_stream_t stream) {
   B2P_CHECK_ARG(qkv16 && O16 && lse2, "attn16_fwd: NULL pointer");
-  B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_fwd: needs head size 64 and T <= 256");
+  B2P_CHECK_ARG(dh == DH && T <= 2 * TMAX && T > 0, "attn16_fwd: needs head size 64 and T <= 512");
+  B2P_CHECK_ARG(!mask || T <= TMAX, "attn16_fwd: the stored keep mask covers T <= 256 (pass NULL: the backward rehashes)");
   if (B <= 0) return 0;
   if (init_attrs()) return 2;
   B2P_CHECK_ARG(B * nh * T * (T + (T & 1)) < (1ll << 32), "attn16_fwd: B * heads * T * T must stay below 2^32 "
@@ -589,9 +648,16 @@ int attn16_fwd_launch(bool half, const void* qkv16, void* O16, void* Ob16, float
   const DropCfg dc = drop_cfg(drop_p, drop_seed);
   const int dm = drop_p > 0.f ? (mask ? 2 : 1) : 0;
   auto run = [&](auto dmc, auto hc) {
-    hipLaunchKernelGGL((attn16_fwd_k<decltype(dmc)::value, decltype(hc)::value>), grid, dim3(FWD_NT), FWD_LDS,
-                       (hipStream_t)stream, (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T,
-                       (int)nh, scale, dc, dm == 2 ? mask : (uint32_t*)nullptr);
+    constexpr int DM = decltype(dmc)::value;
+    constexpr bool HH = decltype(hc)::value;
+    if (T <= TMAX)
+      hipLaunchKernelGGL((attn16_fwd_k<DM, HH, TMAX>), grid, dim3(FWD_NT), fwd_lds<TMAX>(), (hipStream_t)stream,
+                         (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T, (int)nh, scale, dc,
+                         dm == 2 ? mask : (uint32_t*)nullptr);
+    else if constexpr (DM != 2)
+      hipLaunchKernelGGL((attn16_fwd_k<DM, HH, 2 * TMAX>), grid, dim3(FWD_NT), fwd_lds<2 * TMAX>(), (hipStream_t)stream,
+                         (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T, (int)nh, scale, dc,
+                         (uint32_t*)nullptr);
   };
   using F = std::false_type;
   using Tr = std::true_type;
@@ -626,7 +692,8 @@ int attn16_bwd_launch(bool half, const void* qkv16, const void* dO16, const floa
                       void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh, float scale, float drop_p,
                       uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream) {
   B2P_CHECK_ARG(qkv16 && dO16 && lse2 && delta_ws && (dqkv || dqkv16), "attn16_bwd: NULL pointer");
-  B2P_CHECK_ARG(dh == DH && T <= TMAX && T > 0, "attn16_bwd: needs head size 64 and T <= 256");
+  B2P_CHECK_ARG(dh == DH && T <= 2 * TMAX && T > 0, "attn16_bwd: needs head size 64 and T <= 512");
+  B2P_CHECK_ARG(!mask || T <= TMAX, "attn16_bwd: the stored keep mask covers T <= 256");
   if (B <= 0) return 0;
   if (init_attrs()) return 2;
   const dim3 grid_q((unsigned)(B * nh * ((T + FWD_QB - 1) / FWD_QB)));
@@ -638,10 +705,17 @@ int attn16_bwd_launch(bool half, const void* qkv16, const void* dO16, const floa
   auto run = [&](auto dm, auto hc) {
     constexpr int DM = decltype(dm)::value;
     constexpr bool HH = decltype(hc)::value;
-    hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH>), grid_q, dim3(256), FWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16,
-                       (int)T, (int)nh, scale, dc, mask);
-    hipLaunchKernelGGL((attn16_bwd_dkv_k<DM, HH>), grid_k, dim3(256), BWD_LDS, st, q, delta_ws, d, lse2, dqkv, d16,
-                       (int)T, (int)nh, scale, dc, mask);
+    if (T <= TMAX) {
+      hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH, TMAX>), grid_q, dim3(256), fwd_lds<TMAX>(), st, q, delta_ws, d, lse2,
+                         dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+      hipLaunchKernelGGL((attn16_bwd_dkv_k<DM, HH, TMAX>), grid_k, dim3(256), bwd_lds<TMAX>(), st, q, delta_ws, d, lse2,
+                         dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+    } else if constexpr (DM != 2) {
+      hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH, 2 * TMAX>), grid_q, dim3(256), fwd_lds<2 * TMAX>(), st, q, delta_ws,
+                         d, lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+      hipLaunchKernelGGL((attn16_bwd_dkv_k<DM, HH, 2 * TMAX>), grid_k, dim3(256), bwd_lds<2 * TMAX>(), st, q, delta_ws,
+                         d, lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+    }
   };
   auto by_dm = [&](auto hc) {
     if (drop_p > 0.f && mask) run(std::integral_constant<int, 2>(), hc);

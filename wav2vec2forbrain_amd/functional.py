@@ -1643,8 +1643,10 @@ def _attn_core_bwd(qkv, P, Pd, dO, B, T, nh, dh, p_attn, seed, want16=False):
 
 
 def attn16_ok(T, dh) -> bool:
-    """The fused bf16 attention kernels (csrc/attn16.hip) cover head size 64 and T' <= 256."""
-    return dh == 64 and 0 < T <= 256
+    """The fused bf16 attention kernels (csrc/attn16.hip) cover head size 64 and T' <= 512 (windows of up
+    to 2,080 bins; the 256-key class keeps the dropout keep bits for the backward, the 512-key class
+    rehashes them)."""
+    return dh == 64 and 0 < T <= 512
 
 
 def _attn16_fwd(qkv16, B, T, nh, dh, p_attn, seed, want_mask=False):
@@ -1653,7 +1655,8 @@ def _attn16_fwd(qkv16, B, T, nh, dh, p_attn, seed, want_mask=False):
     dev = qkv16.device
     O16 = torch.empty(B * T, nh * dh, device=dev, dtype=BF16)
     lse2 = torch.empty(B, nh, T, device=dev)
-    mask = torch.empty(B, nh, T, 8, device=dev, dtype=torch.int32) if (want_mask and p_attn > 0) else None
+    # the stored keep mask covers T' <= 256 (32 bytes a row); longer windows rehash in the backward
+    mask = torch.empty(B, nh, T, 8, device=dev, dtype=torch.int32) if (want_mask and p_attn > 0 and T <= 256) else None
     _lib.call("b2p_attn16_fwd", _p(qkv16), _p(O16), _p(lse2), B, T, nh, dh, float(dh ** -0.5), float(p_attn),
               seed, None if mask is None else mask.data_ptr(), _st())
     return (O16, lse2, mask) if want_mask else (O16, lse2)
@@ -1674,7 +1677,7 @@ def _attn16_fwd_f16(qkvh, B, T, nh, dh, p_attn, seed):
     Oh = torch.empty(B * T, nh * dh, device=dev, dtype=torch.float16)
     Ob = torch.empty(B * T, nh * dh, device=dev, dtype=BF16)
     lse2 = torch.empty(B, nh, T, device=dev)
-    mask = torch.empty(B, nh, T, 8, device=dev, dtype=torch.int32) if p_attn > 0 else None
+    mask = torch.empty(B, nh, T, 8, device=dev, dtype=torch.int32) if (p_attn > 0 and T <= 256) else None
     _lib.call("b2p_attn16_fwd_f16", _p(qkvh), _p(Oh), _p(Ob), _p(lse2), B, T, nh, dh, float(dh ** -0.5),
               float(p_attn), seed, None if mask is None else mask.data_ptr(), _st())
     return Oh, Ob, lse2, mask
