@@ -269,9 +269,7 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     const float inv_s = DROP ? inv * dc.scale : inv;   // keys >= T already hold exp2(-inf) = 0
     const uint32_t rowlo = (uint32_t)((((uint32_t)b * (uint32_t)nh + (uint32_t)h) * (uint32_t)T + (uint32_t)(qok ? q : 0)) *
                                       (uint32_t)TP);
-    // O^T (d x q) = V^T (d x keys) . P_d^T (keys x q), 32 keys per k-step, on the UNNORMALISED
-    // probabilities exp2(s - max) in [0, 1] (same relative rounding in the 16-bit operand): the row's
-    // 1 / sum and the dropout scale multiply the 16 outputs per lane instead of the 64 scores
+    // O^T (d x q) = V^T (d x keys) . P_d^T (keys x q), 32 keys per k-step
     f32x4 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -283,9 +281,10 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
         const int key0 = (2 * c + half) * 16 + 4 * g;
         const uint32_t kb = DROP ? keep4_bits(rowlo + (uint32_t)key0, k32, thr16) : 0xFu;
         if (DM == 2) mbits[c >> 2] |= kb << (8 * (c & 3) + 4 * half);
-        if (DROP) {
 #pragma unroll
-          for (int i = 0; i < 4; ++i) s[2 * c + half][i] = ((kb >> i) & 1u) ? s[2 * c + half][i] : 0.f;
+        for (int i = 0; i < 4; ++i) {
+          const float pv = s[2 * c + half][i] * inv_s;
+          s[2 * c + half][i] = (DROP && !((kb >> i) & 1u)) ? 0.f : pv;
         }
       }
       const bf16x8 bp = pack_acc_t<H>(s[2 * c], s[2 * c + 1]);
@@ -298,10 +297,6 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     if (DM == 2 && qok)
       *reinterpret_cast<uint2*>(maskw + (((int64_t)b * nh + h) * T + q) * 8 + 2 * g) = make_uint2(mbits[0], mbits[1]);
     const int64_t orow = (row0 + q) * D + h * DH;
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) o[dt][i] *= inv_s;
     if (qok) {
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
