@@ -455,3 +455,56 @@ def test_scalar_epilogue_odd_n():
     pre16 = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     with pytest.raises(RuntimeError):
         Fn.gemm(M, N, K, Fn.op(a16, 0, K, True), Fn.op(w16, 0, K, True), None, N, pre16=pre16, C16=c16)
+
+
+_SPLITK_CASES = [(3072, 768, 7968, "ab", 1.0, 1), (768, 768, 7968, "ab", 0.0, 1), (4096, 1024, 7968, "ab", 1.0, 1),
+                 (1000, 520, 4200, "AB", 0.0, 1), (520, 776, 4160, "ab", 1.0, 2)]
+
+
+def test_splitk_fixup_in_kernel_matches_reduce_launch():
+    """The opt-in in-kernel split-K fix-up (B2P_SPLITK_FUSED=1, read once per process: one subprocess
+    runs every case) against the reduce launch, bitwise (_check_splitk_fixup)."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, B2P_SPLITK_FUSED="1")
+    code = "import tests.test_gemm_gpu as t\nfor c in t._SPLITK_CASES: t._check_splitk_fixup(*c)\n"
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", code], env=env, cwd=root, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+
+
+def _check_splitk_fixup(M, N, K, lay, beta, nz):
+    """Split-K weight-gradient shapes: the in-kernel fix-up (the last K-slice workgroup of each tile sums
+    the slabs, gemm16_impl.inc splitk_fixup) against the separate reduce launch (splitk_reduce4): the
+    same slice order, so C must be bitwise equal; both against torch fp32 (beta = 1 accumulates into C,
+    as the frozen weights' .grad). Ping-pong (4096 x 1024) and 128 x 128 (the rest) kernels, batched."""
+    Fn = _fn()
+    torch.manual_seed(9)
+    bf = torch.bfloat16
+    if lay == "ab":
+        a = torch.randn(nz, K, M, device="cuda").to(bf)
+        b = torch.randn(nz, K, N, device="cuda").to(bf)
+        A, Bo = Fn.op(a, 0, M, False, bs1=K * M), Fn.op(b, 0, N, False, bs1=K * N)
+        ref = a.double().transpose(1, 2) @ b.double()
+    else:
+        a = torch.randn(nz, M, K, device="cuda").to(bf)
+        b = torch.randn(nz, N, K, device="cuda").to(bf)
+        A, Bo = Fn.op(a, 0, K, True, bs1=M * K), Fn.op(b, 0, K, True, bs1=N * K)
+        ref = a.double() @ b.double().transpose(1, 2)
+    c0 = torch.randn(nz, M, N, device="cuda")
+    outs = []
+    old = Fn._SPLITK_CTR[0]
+    try:
+        for fused in (True, False):
+            Fn._SPLITK_CTR[0] = fused
+            c = c0.clone()
+            Fn.gemm(M, N, K, A, Bo, c, N, cbs1=M * N, nz1=nz, beta=beta)
+            outs.append(c)
+        torch.cuda.synchronize()
+    finally:
+        Fn._SPLITK_CTR[0] = old
+    assert torch.equal(outs[0], outs[1])
+    want = ref + beta * c0.double()
+    err = float((outs[0].double() - want).abs().max())
+    assert err <= 2e-6 * float(want.abs().max()) * K ** 0.5, err

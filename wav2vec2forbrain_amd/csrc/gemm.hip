@@ -484,7 +484,7 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
     return 1;
   }
   if (rc) return rc;
-  if (d.ksplit > 1) {
+  if (d.ksplit > 1 && !(bf16_ops && gemm16_splitk_fused(d))) {
     const int64_t total = (int64_t)d.nz1 * d.nz2 * d.M * d.N;
     const b2p_epilogue& e = d.ep;
     const bool v4 = d.N % 4 == 0 && e.ldc % 4 == 0 && e.cbs1 % 4 == 0 && e.cbs2 % 4 == 0 &&

@@ -51,11 +51,37 @@ static uint32_t epi_kind(const b2p_gemm_desc& d, const EpiArgs& ea) {
   return k;
 }
 
+// split-K fix-up inside the GEMM (splitk_fixup, gemm16_impl.inc) instead of the reduce launch: the
+// vectorised layouts, a workspace with room for one counter per 128 x 128 output tile behind the
+// slabs (functional.gemm allocates it), B2P_SPLITK_FUSED=1. Off by default: the last workgroup of a
+// tile sums all its slices alone, so the weight-gradient grids (36-144 tiles x 4-7 slices) end in a
+// tail of a few busy CUs: 768x768x7968 38.0 -> 64.5 us, 3072x768x7968 75.6 -> 84.0 us against the
+// reduce launch spread over the chip (profiles/r04w_splitk_fused_ab.txt).
+bool gemm16_splitk_fused(const b2p_gemm_desc& d) {
+  static const int on = getenv("B2P_SPLITK_FUSED") ? atoi(getenv("B2P_SPLITK_FUSED")) : 0;
+  if (!on || d.ksplit <= 1 || !d.workspace) return false;
+  const b2p_epilogue& e = d.ep;
+  const bool v4 = d.N % 4 == 0 && e.ldc % 4 == 0 && e.cbs1 % 4 == 0 && e.cbs2 % 4 == 0 &&
+                  ((uintptr_t)e.C & 15u) == 0 && ((uintptr_t)e.C16 & 7u) == 0 && ((uintptr_t)d.workspace & 15u) == 0;
+  const int64_t nz = (int64_t)d.nz1 * d.nz2;
+  const int64_t need = (int64_t)d.ksplit * nz * d.M * d.N + ((d.M + 127) / 128) * ((d.N + 127) / 128) * nz;
+  return v4 && d.workspace_floats >= need;
+}
+
 static int run(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, unsigned nwg, int tm, int tn, int grp) {
   const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
-  if (AK && BK && !d.A.conv && d.A.dtype == 1) return gemm16_run_nt_bf16(d, st, fam, ek, nwg, tm, tn, grp);
-  if (AK && BK && d.A.dtype == 2) return gemm16_run_nt_f16(d, st, fam, ek, nwg, tm, tn, grp);
-  return gemm16_run_other(d, st, fam, ek, nwg, tm, tn, grp);
+  uint32_t* ctr = nullptr;
+  if (gemm16_splitk_fused(d)) {
+    const int64_t nz = (int64_t)d.nz1 * d.nz2;
+    ctr = reinterpret_cast<uint32_t*>(d.workspace + (int64_t)d.ksplit * nz * d.M * d.N);
+    if (hipMemsetAsync(ctr, 0, (size_t)tm * tn * nz * sizeof(uint32_t), st) != hipSuccess) {
+      b2p_set_error("gemm16: split-K counter reset failed");
+      return 1;
+    }
+  }
+  if (AK && BK && !d.A.conv && d.A.dtype == 1) return gemm16_run_nt_bf16(d, st, fam, ek, nwg, tm, tn, grp, ctr);
+  if (AK && BK && d.A.dtype == 2) return gemm16_run_nt_f16(d, st, fam, ek, nwg, tm, tn, grp, ctr);
+  return gemm16_run_other(d, st, fam, ek, nwg, tm, tn, grp, ctr);
 }
 
 int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {

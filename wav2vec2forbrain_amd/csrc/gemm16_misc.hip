@@ -1,9 +1,11 @@
 // gemm16 instantiations: the other layouts (m/n-contiguous operands, conv views)
 #include "gemm16_impl.inc"
 
-int gemm16_run_other(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, unsigned nwg, int tm, int tn, int grp) {
+int gemm16_run_other(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, unsigned nwg, int tm, int tn, int grp,
+                      uint32_t* ctr) {
   EpiArgs ea = make_epi_args(d);
   ea.rk = ek;   // EK_RUNTIME instantiations read the kind bits at run time
+  ea.tile_ctr = ctr;   // split-K fix-up counters (nullptr: the separate reduce launch)
   const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
   const bool h16 = d.A.dtype == 2;
   if (AK && BK) {   // bf16 with an implicit conv view on A

@@ -1,9 +1,11 @@
 // gemm16 instantiations: bf16 operands, A and B k-contiguous
 #include "gemm16_impl.inc"
 
-int gemm16_run_nt_bf16(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, unsigned nwg, int tm, int tn, int grp) {
+int gemm16_run_nt_bf16(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, unsigned nwg, int tm, int tn, int grp,
+                      uint32_t* ctr) {
   EpiArgs ea = make_epi_args(d);
   ea.rk = ek;   // EK_RUNTIME instantiations read the kind bits at run time
+  ea.tile_ctr = ctr;   // split-K fix-up counters (nullptr: the separate reduce launch)
   if (fam == G16_PP) {
     switch (ek) {
 #define B2P_GO_(K) case K: launch_pp<true, true, false, K>(d, ea, st, nwg, tm, tn, grp); return 0;

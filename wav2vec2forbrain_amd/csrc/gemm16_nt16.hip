@@ -1,9 +1,11 @@
 // gemm16 instantiations: fp16 operands, A and B k-contiguous
 #include "gemm16_impl.inc"
 
-int gemm16_run_nt_f16(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, unsigned nwg, int tm, int tn, int grp) {
+int gemm16_run_nt_f16(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, unsigned nwg, int tm, int tn, int grp,
+                      uint32_t* ctr) {
   EpiArgs ea = make_epi_args(d);
   ea.rk = ek;   // EK_RUNTIME instantiations read the kind bits at run time
+  ea.tile_ctr = ctr;   // split-K fix-up counters (nullptr: the separate reduce launch)
   const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
   if (!(AK && BK)) { b2p_set_error("gemm16: internal dispatch"); return 1; }
   if (fam == G16_PP) {

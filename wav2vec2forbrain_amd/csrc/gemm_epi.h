@@ -31,6 +31,8 @@ struct EpiArgs {
   const uint64_t* epoch;   // graph-replay dropout seed offset (b2p_seed_eff)
   const int32_t* gate;     // LayerDrop gate (b2p_gate): closed -> no K loop
   uint32_t rk;             // gemm16 epilogue kind bits of this launch (EK_RUNTIME instantiations)
+  uint32_t* tile_ctr;      // gemm16 split-K: per-tile arrival counters (zeroed per launch) -> the last
+                           // K-slice workgroup of a tile sums the slabs itself (no reduce launch)
 };
 
 __device__ __forceinline__ void epilogue_store(const EpiArgs& a, int z, int z1, int z2, int m, int n,
@@ -196,6 +198,7 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
   ea.epoch = b2p_seed_epoch();
   ea.gate = b2p_gate();
   ea.rk = 0;
+  ea.tile_ctr = nullptr;
   return ea;
 }
 
@@ -203,3 +206,5 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
 
 // bf16-operand (LDS-DMA) GEMM launcher, gemm16.hip; arguments already validated by b2p_gemm.
 int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st);
+// true when the gemm16 launch of d sums its split-K slabs itself (no reduce launch after it)
+bool gemm16_splitk_fused(const b2p_gemm_desc& d);

@@ -530,7 +530,9 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
             kchunk = -(-kchunk // q) * q
             ks = -(-K // kchunk)
             dev = (C if C is not None else C16).device
-            ws = torch.empty(ks * nz1 * nz2 * M * N, device=dev, dtype=torch.float32)
+            # slabs + one arrival counter per 128 x 128 output tile (the 16-bit kernel's in-kernel fix-up)
+            ctr = -(-M // 128) * -(-N // 128) * nz1 * nz2 if _SPLITK_CTR[0] else 0
+            ws = torch.empty(ks * nz1 * nz2 * M * N + ctr, device=dev, dtype=torch.float32)
             d.ksplit, d.kchunk = ks, kchunk
             d.workspace = ws.data_ptr()
             d.workspace_floats = ws.numel()
@@ -547,6 +549,9 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
                                                             + (2 if aux16 is not None else 4 if aux is not None else 0))))
     _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
 
+
+# split-K fix-up inside the 16-bit GEMM (counters behind the slabs); False: the separate reduce launch
+_SPLITK_CTR = [True]
 
 # tools/gemm_census.py: when a list, every gemm() call appends its shape record
 GEMM_LOG = None
