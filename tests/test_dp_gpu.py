@@ -119,25 +119,43 @@ def test_dp_step_equals_global_batch_step(name, tmp_path):
         assert torch.equal(res[0]["grads"][n], res[1]["grads"][n]), n
 
 
-def _trainer_steps(model, batches, graphs):
+def _trainer_steps(model, batches, graphs, unfreeze="brain_encoder"):
     from wav2vec2forbrain_amd import functional as Fn
     from wav2vec2forbrain_amd.train.train_loop import Trainer
     from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+    info = {}
     with Fn.precision("fp32"):
-        trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+        trainer = Trainer(SyntheticStepExperiment(model, unfreeze=unfreeze, lr=1e-3))
         trainer.use_graphs = graphs
         trainer.capture_after = 1
-        losses = [float(trainer.train_step(b).loss) for b in batches]
+        losses = []
+        for b in batches:
+            if trainer.reducer is not None:
+                trainer.reducer.launch_log.clear()
+                trainer.reducer.launch_tail.clear()
+            losses.append(float(trainer.train_step(b).loss))
     torch.cuda.synchronize()
+    if trainer.reducer is not None:   # the last step's bucket launches (a replay when graphs are on)
+        info.update(launch_log=list(trainer.reducer.launch_log), launch_tail=list(trainer.reducer.launch_tail),
+                    buckets=len(trainer.reducer.buckets))
+    info["segments"] = [g["graph"].segments for g in trainer._graphs.values()]
     counts = (trainer.eager_steps, trainer.graph_steps)
     trainer.release_graphs()
     Fn.set_deferred_wgrad([])
-    return losses, counts
+    return losses, counts, info
 
 
-def _trainer_worker(rank, name, port, out_dir):
+def _optimised(model, unfreeze):
+    from wav2vec2forbrain_amd.train.ddp import unused_param_names
+    if unfreeze == "brain_encoder":
+        return _trainable(model)
+    skip = unused_param_names(model)
+    return [(n, p) for n, p in model.named_parameters() if n not in skip and p.requires_grad]
+
+
+def _trainer_worker(rank, name, port, out_dir, unfreeze="brain_encoder", bucket_mb="64", eager_too=False):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), B2P_DP_BUCKET_MB=bucket_mb)
     dist.init_process_group("gloo", rank=rank, world_size=WORLD)
     try:
         cfg = _cfg(name)
@@ -146,10 +164,17 @@ def _trainer_worker(rank, name, port, out_dir):
         model.sync_metrics = False
         per = cfg["B"] // WORLD
         b = _batch(cfg, (rank * per, (rank + 1) * per))
-        losses, counts = _trainer_steps(model, [b] * 3, graphs=True)
-        torch.save({"losses": losses, "counts": counts,
-                    "params": {n: p.detach().cpu() for n, p in _trainable(model)}},
-                   os.path.join(out_dir, f"trainer_rank{rank}.pt"))
+        losses, counts, info = _trainer_steps(model, [b] * 3, graphs=True, unfreeze=unfreeze)
+        rec = {"losses": losses, "counts": counts, "info": info,
+               "params": {n: p.detach().cpu() for n, p in _optimised(model, unfreeze)},
+               "bufs": {n: b.detach().cpu() for n, b in model.named_buffers() if b.is_floating_point()}}
+        if eager_too:   # the same data-parallel steps without graphs, from the same initial model
+            model = build_model(cfg)
+            model.train()
+            model.sync_metrics = False
+            rec["eager_losses"] = _trainer_steps(model, [b] * 3, graphs=False, unfreeze=unfreeze)[0]
+            rec["eager_params"] = {n: p.detach().cpu() for n, p in _optimised(model, unfreeze)}
+        torch.save(rec, os.path.join(out_dir, f"trainer_rank{rank}.pt"))
     finally:
         dist.destroy_process_group()
 
@@ -164,7 +189,7 @@ def test_dp_replayed_trainer_steps_equal_global_batch_steps(tmp_path):
     cfg = _cfg(name)
     ref = build_model(cfg)
     ref.train()
-    ref_losses, _ = _trainer_steps(ref, [_batch(cfg, (0, cfg["B"]))] * 3, graphs=False)
+    ref_losses, _, _ = _trainer_steps(ref, [_batch(cfg, (0, cfg["B"]))] * 3, graphs=False)
     params = {n: p.detach().cpu() for n, p in _trainable(ref)}
 
     ctx = mp.get_context("spawn")
@@ -186,3 +211,63 @@ def test_dp_replayed_trainer_steps_equal_global_batch_steps(tmp_path):
             d = float((r["params"][n] - p).norm())
             assert d <= 1e-4 * float(p.norm()) + 1e-6, (n, d)
         assert torch.equal(res[0]["params"][n], res[1]["params"][n]), n
+
+
+def test_dp_replayed_syncbn_full_ft_steps_equal_global_batch_steps(tmp_path):
+    """The Conformer with synchronised BatchNorm, fully fine-tuned (unfreeze=brain_encoder+w2v), under
+    data-parallel replays: the step is captured in segments split at every SyncBN statistics
+    all-reduce (forward and backward) and at every gradient-bucket launch (train/step_graph.py), and a
+    replay issues those collectives between the segments. Three steps of two ranks on half batches
+    give the parameters and BatchNorm running statistics of three single-process steps on the whole
+    batch, steps 2-3 are replays, and the replay launched gradient buckets with captured backward
+    still to run after them (the exchange overlapped the backward)."""
+    import torch.multiprocessing as mp
+    name, unfreeze = "tiny_conf", "brain_encoder+w2v"
+    cfg = _cfg(name)
+    ref = build_model(cfg)
+    ref.train()
+    ref_losses, _, _ = _trainer_steps(ref, [_batch(cfg, (0, cfg["B"]))] * 3, graphs=False, unfreeze=unfreeze)
+    params = {n: p.detach().cpu() for n, p in _optimised(ref, unfreeze)}
+    bufs = {n: b.detach().cpu() for n, b in ref.named_buffers() if b.is_floating_point()}
+
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_trainer_worker, args=(r, name, port, str(tmp_path), unfreeze, "0.01", True))
+             for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [torch.load(tmp_path / f"trainer_rank{r}.pt", weights_only=True) for r in range(WORLD)]
+    for r in res:
+        assert tuple(r["counts"]) == (1, 2), r["counts"]
+        info = r["info"]
+        nconv = sum(1 for n in bufs if n.endswith("running_mean"))
+        # 3 SyncBN all-reduces per conv module (2 forward, 1 backward) + the bucket launch points
+        assert info["segments"][0] >= 3 * nconv + 2, (info["segments"], nconv)
+        assert info["buckets"] >= 3, info
+        assert sorted(info["launch_log"]) == list(range(info["buckets"])), info
+        assert max(info["launch_tail"]) > 0, info   # some bucket went out before the backward ended
+    for k in range(3):
+        glob = (res[0]["losses"][k] + res[1]["losses"][k]) / 2
+        assert abs(glob - ref_losses[k]) <= 2e-5 * abs(ref_losses[k]), (k, glob, ref_losses[k])
+    # the key-projection bias has no true gradient (softmax over keys ignores it): its gradient is
+    # reduction noise that Adam normalises to +-lr, so it is compared replay-vs-eager only
+    noise = [n for n in params if n.endswith("linear_k.bias")]
+    glob, rep = {}, {}
+    for n, p in params.items():
+        for r in res:
+            glob[n] = max(glob.get(n, 0.0), float((r["params"][n] - p).norm()) / float(p.norm()))
+            rep[n] = max(rep.get(n, 0.0), float((r["params"][n] - r["eager_params"][n]).norm()) / float(p.norm()))
+        assert torch.equal(res[0]["params"][n], res[1]["params"][n]), n
+    print("rel param diff, replayed DP vs global batch:", sorted(glob.items(), key=lambda kv: -kv[1])[:6])
+    print("rel param diff, replayed DP vs eager DP:", sorted(rep.items(), key=lambda kv: -kv[1])[:6])
+    for n in params:
+        assert rep[n] <= 1e-5, (n, rep[n])
+        if n not in noise:
+            assert glob[n] <= 2e-4, (n, glob[n])
+    for n, b in bufs.items():
+        for r in res:
+            d = float((r["bufs"][n] - b).norm())
+            assert d <= 1e-4 * float(b.norm()) + 1e-6, (n, d)

@@ -207,6 +207,11 @@ def set_deferred_wgrad(params) -> None:
     _FROZEN_PTR.update({p.data_ptr(): p for p in params if p is not None and p.is_cuda})
 
 
+def deferred_wgrad_active() -> bool:
+    """Some parameter's gradient work is deferred to the side streams (set_deferred_wgrad)."""
+    return bool(_Deferred.ids)
+
+
 def _defer_ok(p) -> bool:
     return p is not None and id(p) in _Deferred.ids
 
@@ -367,14 +372,44 @@ def flush_wgrad(after=None) -> None:
     _Deferred.pending = True
 
 
-def join_wgrad() -> None:
-    """Flush, then make the current stream wait for the side streams."""
-    flush_wgrad()
+def _join_sides() -> None:
+    """The current stream waits for the work already flushed to the side streams (the queue stays)."""
     if _Deferred.pending:
         cur = torch.cuda.current_stream()
         for sd in _Deferred.sides:
             cur.wait_stream(sd)
         _Deferred.pending = False
+
+
+def join_wgrad() -> None:
+    """Flush, then make the current stream wait for the side streams."""
+    flush_wgrad()
+    _join_sides()
+
+
+class _Segments:
+    """The segmented capture in progress (train/step_graph.py _SegmentedCapture) and, while a replay
+    runs the host calls between its segments, how many segments follow the current call."""
+    active = None
+    remaining = 0
+
+
+def collective(fn) -> None:
+    """A host-issued collective (a torch.distributed call) at this point of the step. Eager: fn()
+    now. Inside a segmented capture: the captured segment ends here (its side-stream forks joined, as
+    a graph requires), and every replay calls fn() between this segment and the next — a collective is
+    never captured, the segments around it are."""
+    seg = _Segments.active
+    if seg is None:
+        fn()
+        return
+    _join_sides()
+    seg.split(fn)
+
+
+def segments_remaining() -> int:
+    """Inside a host call between the segments of a replayed step: the segments still to run."""
+    return _Segments.remaining
 
 
 def set_precision(mode: str) -> None:
@@ -2576,12 +2611,12 @@ def _bn_fwd_sync(c, gamma, beta, run_mean, run_var, y, pre, mean, rstd, M, C, ep
     import torch.distributed as dist
     count = M * dist.get_world_size(group)
     _lib.call("b2p_batchnorm_stats", _p(c), None, _p(mean), M, C, _p(ws), _st())
-    dist.all_reduce(mean, group=group)
+    collective(lambda: dist.all_reduce(mean, group=group))
     _lib.call("b2p_batchnorm_finalize", _p(mean), None, None, None, None, C, count, float(eps), float(momentum), 0,
               _st())
     sq = torch.empty(C, device=c.device)
     _lib.call("b2p_batchnorm_stats", _p(c), _p(mean), _p(sq), M, C, _p(ws), _st())
-    dist.all_reduce(sq, group=group)
+    collective(lambda: dist.all_reduce(sq, group=group))
     _lib.call("b2p_batchnorm_finalize", _p(mean), _p(sq), _p(rstd), _p(run_mean), _p(run_var), C, count, float(eps),
               float(momentum), 1, _st())
     _lib.call("b2p_batchnorm_apply", _p(c), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(y), _p(pre), M, C, act,
@@ -2598,7 +2633,7 @@ def _bn_bwd_sync(dy, pre, c, mean, rstd, gamma, dx, dgamma, dbeta, M, C, act, ws
     _lib.call("b2p_batchnorm_bwd_sums", _p(dy), _p(pre), _p(c), _p(mean), _p(rstd), _p(g), _p(dbeta), _p(dgamma), M,
               C, act, _p(ws), _st())
     sums = torch.cat([dbeta, dgamma])
-    dist.all_reduce(sums, group=group)
+    collective(lambda: dist.all_reduce(sums, group=group))
     _lib.call("b2p_batchnorm_bwd_dx", _p(g), _p(c), _p(mean), _p(rstd), _p(gamma), _p(sums), _p(sums, C), _p(dx), M, C,
               count, _st())
 

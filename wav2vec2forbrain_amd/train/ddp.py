@@ -17,10 +17,13 @@ RCCL spreads one large all-reduce over all links with multiple channels, so fewe
 (default 64 MB) amortise the per-collective latency while still leaving several buckets to overlap
 for the full-fine-tune gradient sets (424 MB base, 2.47 GB Conformer-large).
 
-Graph-replayed steps (bench.py N>1, overlap=False): backward is captured and finish() exchanges the
-buckets after the replay. Under unfreeze=brain_encoder (BASELINE configs 1-4) every trainable
-gradient is produced at the very end of backward (GRU, front end), so there is no backward left to
-overlap with; the exchange is the 64 MB brain-encoder set, ~0.1 ms on 7 links.
+Graph-replayed steps: a bucket's launch goes through functional.collective(), so inside a segmented
+capture (train/step_graph.py) it splits the captured step there and each replay issues the bucket's
+all-reduce between the segments, beside the rest of the backward (full fine-tuning, config 5).
+Under unfreeze=brain_encoder (BASELINE configs 1-4) every trainable gradient is produced at the very
+end of backward (GRU, front end), beside the side-stream frozen-weight gradients a split would have
+to join, so the Trainer captures those with overlap=False and finish() exchanges the buckets after
+the replay: the 64 MB brain-encoder set, ~0.1 ms on 7 links.
 """
 from __future__ import annotations
 
@@ -28,6 +31,8 @@ from typing import Iterable
 
 import torch
 import torch.distributed as dist
+
+from .. import functional as Fn
 
 
 class GradBucketReducer:
@@ -68,6 +73,8 @@ class GradBucketReducer:
                 off += p.numel()
             self.flat.append(flat)
         self.launch_log: list[int] = []     # bucket indices in the order their collectives were issued
+        # per launch: the captured segments a replay still ran after it (> 0: overlapped the backward)
+        self.launch_tail: list[int] = []
         # "used by some rank this step" per parameter (int32, MAX-reduced in finish()): the gates
         # HipAdam's device form reads (opt.gates = reducer.gates), so a parameter no rank used —
         # every rank's LayerDrop dropped its layer — is left untouched, as torch.optim.Adam leaves a
@@ -171,11 +178,21 @@ class GradBucketReducer:
         op = dist.ReduceOp.AVG if self.avg_op else dist.ReduceOp.SUM
         self.works[bi] = dist.all_reduce(self.flat[bi], op=op, group=self.pg, async_op=True)
         self.launch_log.append(bi)
+        self.launch_tail.append(Fn.segments_remaining())
+
+    def _launch_all(self, bis):
+        for bi in bis:
+            self._launch(bi)
+        self.next_launch = max(self.next_launch, bis[-1] + 1)
 
     def _launch_ready(self):
+        ready = []
         while self.next_launch < len(self.buckets) and self.pending[self.next_launch] == 0:
-            self._launch(self.next_launch)
+            ready.append(self.next_launch)
             self.next_launch += 1
+        if ready:
+            # eager: now; segmented capture: between the segments of every replay
+            Fn.collective(lambda: self._launch_all(ready))
 
     def _hook(self, p):
         self._seen.add(id(p))

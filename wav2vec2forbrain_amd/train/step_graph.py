@@ -15,6 +15,14 @@ call. What stays live across replays:
     (copy_) before a replay.
 Gradients of parameters that the optimizer does not own (the frozen wav2vec2 weights, as in the
 reference) keep accumulating in their .grad buffers across replays, exactly as in eager steps.
+
+Segmented capture (segmented=True, the data-parallel step): a collective cannot live inside a graph,
+so every host collective the step issues through functional.collective() — the SyncBN statistics
+all-reduces of the Conformer's conv modules (forward and backward) and the gradient-bucket all-reduces
+as buckets complete — ends the graph captured so far and starts the next. The segments share one
+memory pool (replayed in capture order, as the pool requires); a replay runs segment 0, the first
+collective, segment 1, ... so a bucket's RCCL all-reduce (async) runs beside the rest of the
+backward.
 """
 from __future__ import annotations
 
@@ -58,8 +66,55 @@ def _capture_stream(dev, prio: bool):
     return s
 
 
+class _SegmentedCapture:
+    """Graphs captured back to back on one stream and one memory pool, split at host collectives."""
+
+    def __init__(self, stream):
+        self.stream = stream
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs: list = []
+        self.calls: list = []
+        self.cur = None
+
+    def begin(self) -> None:
+        g = torch.cuda.CUDAGraph()
+        # relaxed: a split inside the backward begins the next segment on autograd's worker thread
+        # and the main thread ends it (the other modes tie a capture to the thread that began it)
+        with torch.cuda.stream(self.stream):
+            g.capture_begin(pool=self.pool, capture_error_mode="relaxed")
+        self.cur = g
+
+    def end(self) -> None:
+        with torch.cuda.stream(self.stream):
+            self.cur.capture_end()
+        self.graphs.append(self.cur)
+        self.cur = None
+
+    def split(self, fn) -> None:
+        self.end()
+        self.calls.append(fn)
+        self.begin()
+
+    def replay(self) -> None:
+        n = len(self.graphs)
+        for i, g in enumerate(self.graphs):
+            g.replay()
+            if i < len(self.calls):
+                Fn._Segments.remaining = n - 1 - i
+                try:
+                    self.calls[i]()
+                finally:
+                    Fn._Segments.remaining = 0
+
+    def reset(self) -> None:
+        for g in self.graphs:
+            g.reset()
+        self.graphs, self.calls = [], []
+
+
 class StepGraph:
-    def __init__(self, step_fn, optimizer=None, warmup: int = 2, warm_replays: int = 2, epoch=None):
+    def __init__(self, step_fn, optimizer=None, warmup: int = 2, warm_replays: int = 2, epoch=None,
+                 segmented: bool = False):
         """step_fn() runs one step on the current stream and returns the loss tensor (no host
         syncs inside: model.sync_metrics must be False). Pass the optimizer when step_fn includes
         its update (captured); without it the update runs eagerly after each replay (the data-
@@ -73,6 +128,7 @@ class StepGraph:
         self.graph = None
         self.loss = None
         self.epoch = epoch
+        self.segmented = segmented
 
     def capture(self) -> None:
         live = live_graph_nodes()
@@ -104,9 +160,26 @@ class StepGraph:
         # optimizer's host step counters as they were (after_replay advances them per replay)
         steps = ({p: st["step"].clone() for p, st in self.opt.state.items() if "step" in st}
                  if self.opt is not None else {})
-        g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
-            self.loss = self._one()
+        if self.segmented:
+            g = _SegmentedCapture(s)
+            Fn._Segments.active = g
+            g.begin()
+            try:
+                with torch.cuda.stream(s):
+                    self.loss = self._one()
+            except BaseException:
+                Fn._Segments.active = None
+                try:
+                    g.end()
+                finally:
+                    g.reset()
+                raise
+            Fn._Segments.active = None
+            g.end()
+        else:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g, stream=s):
+                self.loss = self._one()
         torch.cuda.synchronize()
         for p, t in steps.items():
             self.opt.state[p]["step"] = t
@@ -124,10 +197,17 @@ class StepGraph:
         """One training step; returns the (static) loss tensor — clone it to keep the value."""
         if self.opt is not None:
             self.opt.prepare_replay()
-        self.graph.replay()
+        self.graph.replay()     # a CUDAGraph, or a _SegmentedCapture (segments and the collectives between)
         if self.opt is not None:
             self.opt.after_replay()
         return self.loss
+
+    @property
+    def segments(self) -> int:
+        """Graphs one replay runs (1 unless segmented)."""
+        if self.graph is None:
+            return 0
+        return len(self.graph.graphs) if self.segmented else 1
 
     def release(self) -> None:
         """Back to eager semantics (the seed counter is no longer mixed in); the executable graph and

@@ -47,7 +47,7 @@ class Trainer:
         if dist.is_initialized() and dist.get_world_size() > 1:
             skip = unused_param_names(self.model)
             params = [p for n, p in self.model.named_parameters() if id(p) in opt_ids and n not in skip]
-            self.reducer = GradBucketReducer(params)
+            self.reducer = GradBucketReducer(params, bucket_mb=float(os.environ.get("B2P_DP_BUCKET_MB", "64")))
             if hasattr(self.optimizer, "make_capturable"):
                 # device-form update gated per parameter by "some rank used it" (LayerDrop: a
                 # parameter no rank used keeps its value and moments, as with grad=None)
@@ -66,6 +66,9 @@ class Trainer:
                            and hasattr(self.optimizer, "make_capturable"))
         self.graph_cache_size = int(os.environ.get("B2P_TRAINER_GRAPHS", "4"))
         self.capture_after = int(os.environ.get("B2P_TRAINER_CAPTURE_AFTER", "1"))
+        # data-parallel replays capture the step in segments split at its collectives (SyncBN
+        # statistics, gradient buckets); 0: one graph, SyncBN steps eager, buckets after the replay
+        self.segmented = os.environ.get("B2P_SEGMENTED_CAPTURE", "1") != "0"
         self._graphs: dict = {}
         self._shape_seen: dict = {}
         self._epoch_counter = None
@@ -84,14 +87,17 @@ class Trainer:
 
     def _sync_bn(self) -> bool:
         """Data-parallel with synchronised BatchNorm statistics (the Conformer's sync_batchnorm): the
-        statistics all-reduce runs inside the forward, which a captured step cannot hold (no collective
-        is captured), so such steps stay eager. With sync_batchnorm off each rank normalises over its
-        own micro-batch (torch DDP's default semantics) in eager and replayed steps alike."""
+        statistics all-reduces run inside the forward and backward. A captured step cannot hold a
+        collective, so the data-parallel step is captured in segments split at each of them
+        (train/step_graph.py); B2P_SEGMENTED_CAPTURE=0 keeps such steps eager instead. With
+        sync_batchnorm off each rank normalises over its own micro-batch (torch DDP's default
+        semantics) in eager and replayed steps alike."""
         return self.reducer is not None and any(getattr(m, "sync_batchnorm", False) for m in self.model.modules())
 
     def _graphable(self, batch) -> bool:
         return (self.use_graphs and self.model.training and batch.input.is_cuda and batch.target is not None
-                and getattr(batch, "target_lens", None) is not None and not Fn.capturing() and not self._sync_bn())
+                and getattr(batch, "target_lens", None) is not None and not Fn.capturing()
+                and (self.segmented or not self._sync_bn()))
 
     def _capture(self, batch):
         """Captures one whole step for this batch shape (train/step_graph.py) on static copies of the
@@ -117,11 +123,16 @@ class Trainer:
 
         if self._epoch_counter is None:
             self._epoch_counter = torch.zeros(1, dtype=torch.int64, device=batch.input.device)
+        seg = dp and self.segmented
         if dp:
-            self.reducer.overlap = False   # no collective inside the capture: exchanged after each replay
+            # bucket all-reduces between the segments of the backward only when no frozen-weight
+            # gradient work runs on the side streams (full fine-tuning): a split joins those streams,
+            # which would serialise them with the GRU backward they are meant to run beside.
+            # Otherwise every bucket is exchanged after the replay (finish()).
+            self.reducer.overlap = seg and not Fn.deferred_wgrad_active()
         try:
             sg = StepGraph(step, None if dp else self.optimizer, warmup=0, warm_replays=0,
-                           epoch=self._epoch_counter)
+                           epoch=self._epoch_counter, segmented=seg)
             sg.capture()
         finally:
             if dp:
