@@ -233,10 +233,10 @@ def timed_run(kind, args, world, rank, device, use_graph):
     model = build(cfg, device)
     model.train()
     if world > 1 and hasattr(model, "sync_batchnorm"):
-        # the Conformer under DP: per-rank BatchNorm statistics (torch DDP's default semantics) so the
-        # step replays as a graph; SyncBN (the statistics all-reduce inside the forward) keeps a DP
-        # step eager (Trainer._sync_bn)
-        model.sync_batchnorm = False
+        # the Conformer under DP: BatchNorm statistics over the global batch (SyncBN, the default); the
+        # replayed step is captured in segments split at those all-reduces (train/step_graph.py).
+        # B2P_BENCH_SYNCBN=0: per-rank statistics (torch DDP's default semantics), one graph
+        model.sync_batchnorm = os.environ.get("B2P_BENCH_SYNCBN", "1") != "0"
     # the reference reads ctc_loss.item() inside forward (w2v_custom_feat_extractor.py:94): a host sync
     # per step. The bench keeps the loss on the device and reads every step's value into pinned host
     # memory (stream-ordered) instead, and reads them all after the timed region.

@@ -877,3 +877,30 @@ def test_conformer_16bit_producers():
     refm = a16.float() @ w16.float().t()
     assert _rel(c32.cpu(), refm.cpu()) < 1e-5
     assert torch.equal(c16, c32.half())
+
+
+@pytest.mark.parametrize("act", [3, 1])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("NT,D,F", [(300, 128, 512), (7968, 1024, 4096)])
+def test_ffn1_epilogue_bf16_copy_equals_recompute(act, p, NT, D, F):
+    """The FFN1 GEMM's second 16-bit output (C16b: bf16(dropout(act(pre))) beside the fp16 forward
+    operand) against the backward's recompute of the same operand from the fp32 pre-activation
+    (b2p_act_dropout_cast16): bitwise equal, for SiLU (the Conformer) and GELU, with and without
+    dropout, on the small-tile and the ping-pong kernels."""
+    Fn = _fn()
+    torch.manual_seed(5)
+    h16 = torch.randn(NT, D, device="cuda").half()
+    w1 = torch.randn(F, D, device="cuda") / math.sqrt(D)
+    b1 = torch.randn(F, device="cuda") * 0.1
+    pre = torch.empty(NT, F, device="cuda")
+    f = torch.empty(NT, F, device="cuda", dtype=torch.float16)
+    fb = torch.empty(NT, F, device="cuda", dtype=torch.bfloat16)
+    seed = 1234 if p > 0 else 0
+    with Fn.precision("bf16"), Fn.forward_f16(True):
+        _, w1op = Fn._w_op16(w1, True)
+        Fn.gemm(NT, F, D, Fn.op(h16, 0, D, True), w1op, None, F, bias=b1, pre_out=pre, act=act, drop_p=p, seed=seed,
+                C16=f, c16_fp16=True, C16b=fb)
+        ref = Fn._act_dropout_cast16(pre, act, p, seed)
+    torch.cuda.synchronize()
+    d = (fb.float() - ref.float()).abs()
+    assert torch.equal(fb, ref), (int((d > 0).sum()), float(d.max()))

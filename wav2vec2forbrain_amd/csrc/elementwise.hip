@@ -229,7 +229,9 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
   // software-pipelined rows: row rr+1's dy / x are in flight while row rr is reduced and written
   // (one wave per row: without the prefetch each row paid a full load latency before any math)
   const int64_t row_base = (int64_t)blockIdx.x * LN_BWD_ROWS + wave * (LN_BWD_ROWS / 4);
-  float4 nd[LN_MAXV], nx[LN_MAXV];
+  // the residual gradient dx_accum is fetched with dy / x (read at the store, it cost a full load
+  // latency per row)
+  float4 nd[LN_MAXV], nx[LN_MAXV], na[LN_MAXV];
   auto fetch = [&](int64_t r) {
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
@@ -237,20 +239,28 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
       if (c < nv && r < rows) {
         nd[i] = reinterpret_cast<const float4*>(dy + r * cols)[c];
         nx[i] = reinterpret_cast<const float4*>(x + r * cols)[c];
+        if (dx_accum) na[i] = reinterpret_cast<const float4*>(dx_accum + r * cols)[c];
       }
     }
   };
   fetch(row_base);
+  float4 gk[LN_MAXV];   // gamma, loaded once per wave (was re-read for every row)
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) gk[i] = g4[c];
+  }
   for (int rr = 0; rr < LN_BWD_ROWS / 4; ++rr) {
     const int64_t row = row_base + rr;
     if (row >= rows) break;
     const float mu = mean[row], rs = rstd[row];
     if (!PF && rr > 0) fetch(row);
-    float4 cd[LN_MAXV], cx[LN_MAXV];
+    float4 cd[LN_MAXV], cx[LN_MAXV], ca[LN_MAXV];
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
       cd[i] = nd[i];
       cx[i] = nx[i];
+      ca[i] = na[i];
     }
     if (PF && rr + 1 < LN_BWD_ROWS / 4) fetch(row + 1);
     float4 xh[LN_MAXV], gg[LN_MAXV];
@@ -269,7 +279,7 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
           d.z = kk[2] ? d.z * dscale : 0.f;
           d.w = kk[3] ? d.w * dscale : 0.f;
         }
-        const float4 xv = cx[i], g = g4[c];
+        const float4 xv = cx[i], g = gk[i];
         xh[i] = make_float4((xv.x - mu) * rs, (xv.y - mu) * rs, (xv.z - mu) * rs, (xv.w - mu) * rs);
         gg[i] = make_float4(d.x * g.x, d.y * g.y, d.z * g.z, d.w * g.w);
         s1 += gg[i].x + gg[i].y + gg[i].z + gg[i].w;
@@ -281,7 +291,6 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
     s1 = warp_sum(s1) / cols;
     s2 = warp_sum(s2) / cols;
     float4* dxr = reinterpret_cast<float4*>(dx + row * cols);
-    const float4* acc = dx_accum ? reinterpret_cast<const float4*>(dx_accum + row * cols) : nullptr;
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
       const int c = lane + 64 * i;
@@ -291,7 +300,13 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
         o.y = rs * (gg[i].y - s1 - xh[i].y * s2);
         o.z = rs * (gg[i].z - s1 - xh[i].z * s2);
         o.w = rs * (gg[i].w - s1 - xh[i].w * s2);
-        if (acc) { const float4 a = acc[c]; o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w; }
+        if (dx_accum) {
+          // the residual add stays a separate rounding (no fused multiply-add with the rs product):
+          // the same bits as when the add sat behind its own load
+          asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(o.w));
+          const float4 a = ca[i];
+          o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
+        }
         dxr[c] = o;
         if (d16 && !dxd) reinterpret_cast<uint2*>(d16 + row * cols)[c] = b2p_pack_bf16x4(o);
         if (dxd) {   // gradient of the dropout that produced this LN's input (residual branch)

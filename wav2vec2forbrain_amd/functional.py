@@ -2274,6 +2274,9 @@ def _act_dropout_cast16(pre, act, p, seed):
     return out
 
 
+_FFN_F16B = [os.environ.get("B2P_FFN_F16B", "1") != "0"]
+
+
 @_gate_aware
 @_prec_follow
 class _FFNBlock(torch.autograd.Function):
@@ -2292,8 +2295,9 @@ class _FFNBlock(torch.autograd.Function):
         pre = torch.empty(NT, F, device=dev)
         if bf16_mode():
             # 16-bit operands written by their producers (LayerNorm, FFN1 epilogue): no cast passes;
-            # fp16 under forward_f16, else bf16. f exists only as that operand copy (the backward
-            # recomputes its bf16 form from pre)
+            # fp16 under forward_f16, else bf16. Under forward_f16 the FFN1 epilogue also writes f's
+            # bf16 copy, the backward's weight-gradient operand (kept instead of the fp16 one; it was
+            # recomputed from pre, a 195 MB pass per FFN at Conformer-large bs=32)
             half = _state.fwd16
             if half:   # h kept only as the bf16 weight-gradient operand of the backward (no fp32 copy)
                 _, h16, mean, rstd, h = _ln_fwd_x16(x2, g, b, eps, half, want32=False, want_b16=True)
@@ -2301,14 +2305,17 @@ class _FFNBlock(torch.autograd.Function):
                 _, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half, want32=False)
                 h = h16
             f = torch.empty(NT, F, device=dev, dtype=torch.float16 if half else BF16)
+            fb = torch.empty(NT, F, device=dev, dtype=BF16) if half and _FFN_F16B[0] else None
             w1b, w1op = _w_op16(w1, half)
             gemm(NT, F, D, op(h16, 0, D, True), w1op, None, F, bias=b1, pre_out=pre, act=act, drop_p=p_act,
-                 seed=s_act, C16=f, c16_fp16=half)
+                 seed=s_act, C16=f, c16_fp16=half, C16b=fb)
             del h16, w1b
             w2b, w2op = _w_op16(w2, half)
             gemm(NT, D, F, op(f, 0, F, True), w2op, y, D, alpha=scale, bias=bs, drop_p=p_hid, seed=s_hid,
                  residual=x2)
             del w2b
+            if fb is not None:
+                f = fb
         else:
             h, mean, rstd = _ln_fwd(x2, g, b, eps)
             f = torch.empty(NT, F, device=dev)
