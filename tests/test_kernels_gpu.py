@@ -904,3 +904,55 @@ def test_ffn1_epilogue_bf16_copy_equals_recompute(act, p, NT, D, F):
     torch.cuda.synchronize()
     d = (fb.float() - ref.float()).abs()
     assert torch.equal(fb, ref), (int((d > 0).sum()), float(d.max()))
+
+
+def test_conv_module_vector_paths_bitwise_equal_scalar_paths():
+    """The float4 forms of the Conformer conv-module kernels (BatchNorm apply / backward passes, GLU,
+    depthwise-conv LDS staging) against their scalar forms, which the library takes for operands that
+    are not 16-B aligned: bitwise equal outputs (same per-element arithmetic)."""
+    Fn = _fn()
+    from wav2vec2forbrain_amd import _lib
+    lib = _lib.load()
+    P = Fn._p
+    torch.manual_seed(11)
+    B, T, C, K = 3, 150, 256, 31
+    M = B * T
+
+    def buf(n, fill=None):   # [16-B aligned, 4-B offset] views, one allocation each
+        a, b = torch.empty(n + 4, device="cuda"), torch.empty(n + 4, device="cuda")
+        if fill is not None:
+            a[:n].copy_(fill)
+            b[1:n + 1].copy_(fill)
+        return a[:n], b[1:n + 1]
+
+    st = Fn._st()
+    x = torch.randn(M * C, device="cuda") * 2 + 0.3
+    dy = torch.randn(M * C, device="cuda")
+    a2 = torch.randn(M * 2 * C, device="cuda")
+    gamma, beta = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+    mean, rstd = torch.randn(C, device="cuda") * 0.1, torch.rand(C, device="cuda") + 0.5
+    w = torch.randn(C * K, device="cuda") * 0.2
+    outs = []
+    sums_ref = None
+    for al in (0, 1):
+        xs, dys, a2s = buf(M * C, x)[al], buf(M * C, dy)[al], buf(M * 2 * C, a2)[al]
+        y, pre, g, dx, u, cv, dcv, du = (buf(M * C)[al] for _ in range(8))
+        ws = torch.empty(int(lib.b2p_batchnorm_workspace(M, C)) + 4, device="cuda")
+        sums = torch.empty(2 * C, device="cuda")
+        _lib.call("b2p_batchnorm_apply", P(xs), P(mean), P(rstd), P(gamma), P(beta), P(y), P(pre), M, C, 3, st)
+        _lib.call("b2p_batchnorm_bwd_sums", P(dys), P(pre), P(xs), P(mean), P(rstd), P(g), P(sums), P(sums, C), M, C, 3,
+                  P(ws), st)
+        # the column sums themselves take another reduction order on unaligned rows: dx from one set
+        sums_ref = sums if sums_ref is None else sums_ref
+        _lib.call("b2p_batchnorm_bwd_dx", P(g), P(xs), P(mean), P(rstd), P(gamma), P(sums_ref), P(sums_ref, C), P(dx), M,
+                  C, M, st)
+        _lib.call("b2p_glu_fwd", P(a2s), P(u), M, C, st)
+        _lib.call("b2p_dwconv_fwd", P(u), P(w), P(cv), B, T, C, K, st)
+        wsd = torch.empty(int(lib.b2p_dwconv_bwd_workspace(B, T, C, K)) + 4, device="cuda")
+        ddw = torch.empty(C * K, device="cuda")
+        _lib.call("b2p_dwconv_bwd", P(u), P(w), P(dys), P(du), P(ddw), B, T, C, K, P(wsd), st)
+        torch.cuda.synchronize()
+        outs.append([t.clone() for t in (y, pre, g, ws[:M * C], dx, u, cv, du, ddw)])
+    names = ("bn y", "bn pre", "bn g", "bn g*xhat", "bn dx", "glu", "dwconv", "dwconv dx", "dwconv dw")
+    for n, p, q in zip(names, outs[0], outs[1]):
+        assert torch.equal(p, q), (n, float((p - q).abs().max()))
