@@ -956,3 +956,75 @@ def test_conv_module_vector_paths_bitwise_equal_scalar_paths():
     names = ("bn y", "bn pre", "bn g", "bn g*xhat", "bn dx", "glu", "dwconv", "dwconv dx", "dwconv dw")
     for n, p, q in zip(names, outs[0], outs[1]):
         assert torch.equal(p, q), (n, float((p - q).abs().max()))
+
+
+@pytest.mark.parametrize("M,N,batch,ld_pad,mode", [
+    (7968, 1024, 1, 0, 0), (7968, 3 * 768, 1, 0, 0), (1000, 130, 1, 0, 0), (257, 64, 3, 0, 0),
+    (5000, 300, 2, 3, 0), (4099, 96, 1, 0, 1), (3000, 200, 2, 0, 2), (2048, 1024, 1, 0, 3), (1, 5, 1, 0, 0)])
+def test_colsum_one_launch(M, N, batch, ld_pad, mode):
+    """Column sums in one launch (csrc/elementwise.hip colsum_fold*: the last-arriving row block of a
+    column strip sums the strip's sc1 partials and resets its counter) against an fp64 torch sum:
+    ragged M / N, batched, padded ld, every mode, accumulate, repeated launches (counter reuse), a
+    captured graph replayed 3 times and two launches on concurrent streams."""
+    from wav2vec2forbrain_amd import _lib
+    Fn = _fn()
+    torch.manual_seed(M + N)
+    ld = N + ld_pad
+    X = torch.randn(batch, M, ld, device="cuda") + 0.25
+    Y = torch.randn(batch, M, ld, device="cuda")
+    C = torch.randn(batch, N, device="cuda")
+    Xd, Yd, Cd = X[..., :N].double(), Y[..., :N].double(), C.double()
+    ref = {0: Xd.sum(1), 1: (Xd * Xd).sum(1), 2: (Xd * Yd).sum(1), 3: ((Xd - Cd[:, None, :]) ** 2).sum(1)}[mode]
+    yarg = Y if mode == 2 else (C if mode == 3 else None)
+
+    def run(out, acc=0, stream=None):
+        ws = torch.empty(max(int(_lib.load().b2p_colsum_workspace(M, N)) * batch, 1), device="cuda")
+        st = ctypes_stream(stream)
+        _lib.call("b2p_colsum_batched", Fn._p(X), Fn._p(yarg), batch, M, N, ld, M * ld, mode, Fn._p(out), acc,
+                  Fn._p(ws), st)
+        return ws
+
+    tol = 2e-6 * max(1.0, math.sqrt(M))
+    outs = []
+    for _ in range(3):
+        o = torch.empty(batch, N, device="cuda")
+        run(o)
+        outs.append(o)
+    torch.cuda.synchronize()
+    for o in outs:
+        assert torch.equal(o, outs[0])
+        assert _rel(o.double(), ref) < tol
+    o = outs[0].clone()
+    run(o, acc=1)
+    assert _rel(o.double(), 2 * ref) < tol
+    # graph replay: the counters are reset by each launch's last block
+    g = torch.cuda.CUDAGraph()
+    og = torch.zeros(batch, N, device="cuda")
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s):
+            keep = run(og)
+    for _ in range(3):
+        og.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(og, outs[0])
+    del keep
+    # two streams at once
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    o1, o2 = torch.empty(batch, N, device="cuda"), torch.empty(batch, N, device="cuda")
+    torch.cuda.synchronize()
+    with torch.cuda.stream(s1):
+        k1 = run(o1, stream=s1)
+    with torch.cuda.stream(s2):
+        k2 = run(o2, stream=s2)
+    torch.cuda.synchronize()
+    assert torch.equal(o1, outs[0]) and torch.equal(o2, outs[0])
+    del k1, k2
+
+
+def ctypes_stream(stream=None):
+    s = torch.cuda.current_stream() if stream is None else stream
+    import ctypes
+    return ctypes.c_void_p(s.cuda_stream)

@@ -313,12 +313,15 @@ __global__ void dw_transpose_k(const float* __restrict__ kc, float* __restrict__
 // ---- BatchNorm1d (training statistics over M rows, per channel)
 __global__ void bn_finalize_k(const float* __restrict__ sum, const float* __restrict__ sqdev, const float* __restrict__ mean,
                               float* __restrict__ rstd, float* __restrict__ run_mean, float* __restrict__ run_var,
-                              int64_t C, int64_t count, float eps, float momentum) {
+                              int64_t C, int64_t count, float eps, float momentum, const int32_t* __restrict__ gate) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const float mu = mean[c];
   const float var = sqdev[c] / (float)count;
   rstd[c] = rsqrtf(var + eps);
+  // LayerDrop: a replay that skips this layer leaves the running statistics untouched (the reference
+  // never runs the layer), so the captured step needs no snapshot / restore of them
+  if (b2p_gated_off(gate)) return;
   if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
   if (run_var) {
     const float unb = count > 1 ? sqdev[c] / (float)(count - 1) : var;
@@ -659,7 +662,7 @@ extern "C" int b2p_batchnorm_fwd(const float* x, const float* gamma, const float
   hipLaunchKernelGGL(scale_k, dim3(nblk(C)), dim3(256), 0, st, mean, C, 1.f / (float)M);
   if (colsum_impl(x, mean, 1, M, C, C, 0, 3, sqdev, 0, part, st)) return 1;
   hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sqdev, mean, rstd,
-                     running_mean, running_var, C, M, eps, momentum);
+                     running_mean, running_var, C, M, eps, momentum, b2p_gate());
   bn_apply_launch(x, mean, rstd, gamma, beta, y, pre, M, C, act, st);
   B2P_CHECK_LAUNCH();
   return 0;
@@ -676,7 +679,7 @@ extern "C" int b2p_batchnorm_eval(const float* x, const float* gamma, const floa
   float* sq = workspace + C;
   B2P_CHECK_HIP(hipMemcpyAsync(sq, running_var, C * sizeof(float), hipMemcpyDeviceToDevice, st));
   hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sq, running_mean, rstd,
-                     (float*)nullptr, (float*)nullptr, C, (int64_t)1, eps, 0.f);
+                     (float*)nullptr, (float*)nullptr, C, (int64_t)1, eps, 0.f, (const int32_t*)nullptr);
   bn_apply_launch(x, running_mean, rstd, gamma, beta, y, nullptr, M, C, act, st);
   B2P_CHECK_LAUNCH();
   return 0;
@@ -719,7 +722,8 @@ extern "C" int b2p_batchnorm_finalize(float* sum_or_mean, const float* sqdev, fl
   } else {
     B2P_CHECK_ARG(sqdev && rstd, "batchnorm_finalize: phase 1 needs sqdev and rstd");
     hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sqdev,
-                       (const float*)sum_or_mean, rstd, running_mean, running_var, C, count, eps, momentum);
+                       (const float*)sum_or_mean, rstd, running_mean, running_var, C, count, eps, momentum,
+                       b2p_gate());
   }
   B2P_CHECK_LAUNCH();
   return 0;

@@ -3,6 +3,7 @@
 // All fp32, float4-vectorised along the contiguous dimension where the layout allows.
 #include "common.h"
 #include <stdlib.h>
+#include <atomic>
 #include "../../include/b2p_hip.h"
 
 namespace {
@@ -98,6 +99,164 @@ __global__ void __launch_bounds__(256) colsum_p2(const float* __restrict__ part,
   }
 }
 
+// ---- one-launch column sums: phase 2 folded into the last-arriving row block of each column strip.
+// Every row block stores its partial row write-through (sc1), drains (vmcnt(0) + barrier) and counts
+// itself in with one relaxed agent-scope atomic on its strip's counter; the block that draws nblk-1
+// reads the strip's partials with sc1 loads (placement-independent: cdna_hip_programming.md §6
+// Guideline 16, R1 / the counter form of the split-K hand-off), sums them in a fixed order and resets
+// the counter to 0 for the next launch. Counters: a zero-initialised device pool; each launch takes a
+// fresh range (host-side rotation), so launches on different streams / graph branches never share one.
+// Replaces the separate colsum_p2 launch (~5 us of ramp for ~16-64 KB of partials) per reduction.
+constexpr int kCtrPool = 1 << 16;
+__device__ uint32_t g_colsum_ctr[kCtrPool];
+
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+__device__ __forceinline__ rsrc_t mkres_cs(const void* p, uint64_t bytes) {
+  const uint32_t n = bytes >= 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)bytes;
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, n, 0x00020000);
+}
+
+// returns true in every thread of the block that arrived last at counter `ctr` (nblk arrivals)
+__device__ __forceinline__ bool colsum_arrive(uint32_t* ctr, int nblk, int* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this block's sc1 partial stores have landed
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == (uint32_t)(nblk - 1);
+    if (last) __hip_atomic_store(ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");   // keeps the sc1 loads below the count
+  return last;
+}
+
+// colsum_p1v + fold: 128 columns x 8 row lanes per block, as colsum_p1v
+__global__ void __launch_bounds__(256) colsum_fold_v(const float* __restrict__ X, int64_t M, int64_t N, int64_t ld,
+                                                     int64_t bstride, float* __restrict__ part, int nblk,
+                                                     float* __restrict__ out, int accumulate, uint32_t ctr0) {
+  __shared__ float4 red[9][32];   // rows 0-7: the reduction; red[8][0]: the "arrived last" flag
+  const int c4 = threadIdx.x & 31, rl = threadIdx.x >> 5;
+  const int64_t n = (int64_t)blockIdx.x * 128 + 4 * c4;
+  const int blk = blockIdx.y, b = blockIdx.z;
+  const int64_t m0 = (int64_t)blk * kColsumRows;
+  const int64_t m1 = m0 + kColsumRows < M ? m0 + kColsumRows : M;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n < N) {
+    const float* xp = X + b * bstride + n;
+#pragma unroll 4
+    for (int64_t m = m0 + rl; m < m1; m += 8) {
+      const float4 x = *reinterpret_cast<const float4*>(xp + m * ld);
+      s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+    }
+  }
+  red[rl][c4] = s;
+  __syncthreads();
+  float* pb = part + (int64_t)b * nblk * N;
+  const rsrc_t rp = mkres_cs(pb, (uint64_t)nblk * N * 4);
+  if (rl == 0 && n < N) {
+    float4 t = red[0][c4];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) {
+      const float4 u = red[r][c4];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(__attribute__((ext_vector_type(4))) unsigned, t), rp,
+                                           (uint32_t)(((int64_t)blk * N + n) * 4), 0, 16);
+  }
+  if (!colsum_arrive(g_colsum_ctr + ctr0 + (uint32_t)b * gridDim.x + blockIdx.x, nblk,
+                     reinterpret_cast<int*>(&red[8][0])))
+    return;
+  float4 t = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (n < N) {
+    for (int i = rl; i < nblk; i += 8) {
+      const float4 u = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(
+                                                      rp, (uint32_t)(((int64_t)i * N + n) * 4), 0, 16));
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+  }
+  red[rl][c4] = t;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    float4 v = red[0][c4];
+#pragma unroll
+    for (int r = 1; r < 8; ++r) {
+      const float4 u = red[r][c4];
+      v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+    }
+    float4* o = reinterpret_cast<float4*>(out + (int64_t)b * N + n);
+    if (accumulate) {
+      const float4 w = *o;
+      v.x += w.x; v.y += w.y; v.z += w.z; v.w += w.w;
+    }
+    *o = v;
+  }
+}
+
+// colsum_p1 + fold: 64 columns x 4 row lanes per block, every mode, any alignment
+__global__ void __launch_bounds__(256) colsum_fold(const float* __restrict__ X, const float* __restrict__ Y,
+                                                   int64_t M, int64_t N, int64_t ld, int64_t bstride, int mode,
+                                                   float* __restrict__ part, int nblk, float* __restrict__ out,
+                                                   int accumulate, uint32_t ctr0) {
+  __shared__ float red[5][64];    // rows 0-3: the reduction; red[4][0]: the "arrived last" flag
+  const int c = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int64_t n = (int64_t)blockIdx.x * 64 + c;
+  const int blk = blockIdx.y, b = blockIdx.z;
+  const int64_t m0 = (int64_t)blk * kColsumRows;
+  const int64_t m1 = m0 + kColsumRows < M ? m0 + kColsumRows : M;
+  float s = 0.f;
+  if (n < N) {
+    const float* xp = X + b * bstride + n;
+    const float* yp = (Y && mode == 2) ? Y + b * bstride + n : nullptr;
+    const float yc = (Y && mode == 3) ? Y[(int64_t)b * N + n] : 0.f;
+#pragma unroll 8
+    for (int64_t m = m0 + rl; m < m1; m += 4) {
+      const float x = xp[m * ld];
+      const float dxc = x - yc;
+      s += mode == 0 ? x : (mode == 1 ? x * x : (mode == 2 ? x * yp[m * ld] : dxc * dxc));
+    }
+  }
+  red[rl][c] = s;
+  __syncthreads();
+  float* pb = part + (int64_t)b * nblk * N;
+  const rsrc_t rp = mkres_cs(pb, (uint64_t)nblk * N * 4);
+  if (rl == 0 && n < N)
+    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(unsigned, red[0][c] + red[1][c] + red[2][c] + red[3][c]),
+                                          rp, (uint32_t)(((int64_t)blk * N + n) * 4), 0, 16);
+  if (!colsum_arrive(g_colsum_ctr + ctr0 + (uint32_t)b * gridDim.x + blockIdx.x, nblk,
+                     reinterpret_cast<int*>(&red[4][0])))
+    return;
+  float t = 0.f;
+  if (n < N)
+    for (int i = rl; i < nblk; i += 4)
+      t += __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rp, (uint32_t)(((int64_t)i * N + n) * 4), 0,
+                                                                          16));
+  red[rl][c] = t;
+  __syncthreads();
+  if (rl == 0 && n < N) {
+    const float v = (red[0][c] + red[1][c]) + (red[2][c] + red[3][c]);
+    float* o = out + (int64_t)b * N + n;
+    *o = accumulate ? *o + v : v;
+  }
+}
+
+// first counter of a fresh range of n (n <= kCtrPool / 4), or -1 when the one-launch form is off
+int64_t colsum_ctr_range(int64_t n) {
+  static const bool on = [] {
+    const char* e = getenv("B2P_COLSUM_FOLD");
+    return !(e && e[0] == '0');
+  }();
+  if (!on || n > kCtrPool / 4) return -1;
+  static std::atomic<uint32_t> next{0};
+  uint32_t cur = next.load(std::memory_order_relaxed), base, nxt;
+  do {
+    base = cur + (uint32_t)n <= (uint32_t)kCtrPool ? cur : 0u;
+    nxt = base + (uint32_t)n;
+  } while (!next.compare_exchange_weak(cur, nxt, std::memory_order_relaxed));
+  return base;
+}
+
 }  // namespace
 
 // out[b][n] (+)= sum_m f(X[b][m][n]); mode 0: x, 1: x^2, 2: x*Y[b][m][n], 3: (x - Y[b][n])^2
@@ -106,7 +265,20 @@ int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   const int nblk = (int)((M + kColsumRows - 1) / kColsumRows);
   const bool vec = mode == 0 && N % 4 == 0 && ld % 4 == 0 && bstride % 4 == 0 && ((uintptr_t)X & 15u) == 0 &&
-                   ((uintptr_t)part & 15u) == 0;
+                   ((uintptr_t)part & 15u) == 0 && ((uintptr_t)out & 15u) == 0;
+  const int64_t gx = vec ? (N + 127) / 128 : (N + 63) / 64;
+  const int64_t ctr0 = nblk * N < ((int64_t)1 << 30) ? colsum_ctr_range(gx * batch) : -1;
+  if (ctr0 >= 0) {
+    dim3 g((unsigned)gx, nblk, (unsigned)batch);
+    if (vec)
+      hipLaunchKernelGGL(colsum_fold_v, g, dim3(256), 0, st, X, M, N, ld, bstride, part, nblk, out, accumulate,
+                         (uint32_t)ctr0);
+    else
+      hipLaunchKernelGGL(colsum_fold, g, dim3(256), 0, st, X, Y, M, N, ld, bstride, mode, part, nblk, out,
+                         accumulate, (uint32_t)ctr0);
+    B2P_CHECK_LAUNCH();
+    return 0;
+  }
   if (vec) {
     dim3 g1((unsigned)((N + 127) / 128), nblk, (unsigned)batch);
     hipLaunchKernelGGL(colsum_p1v, g1, dim3(256), 0, st, X, M, N, ld, bstride, part, nblk);

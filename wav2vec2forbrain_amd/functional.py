@@ -1477,6 +1477,12 @@ def layerdrop_layer(layer, x, p):
     if LAYERDROP_LOG is not None:
         LAYERDROP_LOG.append(seed)
     bufs = [b for b in layer.buffers() if b.is_floating_point() and b.numel() % 4 == 0]
+    if LAYERDROP_GATE:
+        # BatchNorm running statistics are updated by bn_finalize_k, which reads the gate itself and
+        # leaves them untouched in a replay that skips the layer: no snapshot / restore launches
+        bn = {id(t) for m in layer.modules() if isinstance(m, torch.nn.modules.batchnorm._BatchNorm)
+              for t in (m.running_mean, m.running_var) if t is not None}
+        bufs = [b for b in bufs if id(b) not in bn]
     olds = [b.clone() for b in bufs]
     y = None
     flag = torch.empty(1, dtype=torch.int32, device=x.device)
