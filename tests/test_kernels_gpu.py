@@ -960,7 +960,8 @@ def test_conv_module_vector_paths_bitwise_equal_scalar_paths():
 
 @pytest.mark.parametrize("M,N,batch,ld_pad,mode", [
     (7968, 1024, 1, 0, 0), (7968, 3 * 768, 1, 0, 0), (1000, 130, 1, 0, 0), (257, 64, 3, 0, 0),
-    (5000, 300, 2, 3, 0), (4099, 96, 1, 0, 1), (3000, 200, 2, 0, 2), (2048, 1024, 1, 0, 3), (1, 5, 1, 0, 0)])
+    (5000, 300, 2, 3, 0), (4099, 96, 1, 0, 1), (3000, 200, 2, 0, 2), (2048, 1024, 1, 0, 3), (1, 5, 1, 0, 0),
+    (1000, 130, 1, 1, 3), (999, 66, 2, 2, 2), (777, 40, 1, 1, 1)])
 def test_colsum_one_launch(M, N, batch, ld_pad, mode):
     """Column sums in one launch (csrc/elementwise.hip colsum_fold*: the last-arriving row block of a
     column strip sums the strip's sc1 partials and resets its counter) against an fp64 torch sum:
