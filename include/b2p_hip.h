@@ -470,6 +470,12 @@ int b2p_adam_gated_recs(const int64_t* recs, int ntensors, const float* lr_dev, 
  * frozen parameters into their .grad (src/train/train_loop.py:44,66 never zeroes them), one launch
  * instead of one elementwise add per tensor. */
 int b2p_accum_recs(const int64_t* recs, int ntensors, b2p_stream_t stream);
+/* row-summing form: records {dst, src, numel, nrows, set} (5 x int64 each):
+ * dst[i] (set ? = : +=) sum_{r < nrows} src[r * numel + i], rows summed in order (nrows >= 1). Takes
+ * column sums still held as per-tile partial rows (b2p_gemm colsum_part, b2p_drop_cast_colsum) and
+ * finishes them inside the batched accumulation (replaces b2p_colsum_parts + the add); reference: the
+ * bias gradients torch autograd accumulates into .grad (TF w2v / conf Linear layers). */
+int b2p_accum_rows_recs(const int64_t* recs, int ntensors, b2p_stream_t stream);
 
 /* dropout with an extra output scale: y = x * keep(seed, i) * scale / (1-p) (macaron half-step) */
 int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t seed, float scale,

@@ -1029,3 +1029,26 @@ def ctypes_stream(stream=None):
     s = torch.cuda.current_stream() if stream is None else stream
     import ctypes
     return ctypes.c_void_p(s.cuda_stream)
+
+
+def test_accum_rows_recs():
+    """b2p_accum_rows_recs (csrc/adam.hip accum_rec_k): records {dst, src, numel, nrows, set} in one
+    launch — plain accumulation (nrows 1), column sums of partial rows written (set) or accumulated,
+    more records than one launch holds — against torch."""
+    import ctypes
+    from wav2vec2forbrain_amd import _lib
+    torch.manual_seed(5)
+    cases = [(1000, 1, 0), (4096, 125, 1), (768, 63, 0), (3, 7, 1), (1024, 32, 0)] * 14   # 70 records
+    dsts, srcs, refs, recs = [], [], [], []
+    for n, r, st in cases:
+        d = torch.randn(n, device="cuda")
+        s = torch.randn(r, n, device="cuda")
+        refs.append((s.double().sum(0) + (0 if st else d.double())).float())
+        dsts.append(d)
+        srcs.append(s)
+        recs += [d.data_ptr(), s.data_ptr(), n, r, st]
+    arr = (ctypes.c_int64 * len(recs))(*recs)
+    _lib.call("b2p_accum_rows_recs", arr, len(cases), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    for d, ref in zip(dsts, refs):
+        assert _rel(d, ref) < 1e-5

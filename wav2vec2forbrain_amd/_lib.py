@@ -120,6 +120,7 @@ _SIGS = {
     "b2p_adam_multi_dev": (c_i32, [c_p, c_i32, c_i64, c_p, c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_p]),
     "b2p_cast16_2d": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_p]),
     "b2p_accum_recs": (c_i32, [c_p, c_i32, c_p]),
+    "b2p_accum_rows_recs": (c_i32, [c_p, c_i32, c_p]),
     "b2p_adam_recs": (c_i32, [c_p, c_i32, c_f32, c_f64, c_f64, c_f32, c_f32, c_f32, c_f32, c_p, c_p, c_p, c_p]),
     "b2p_adam_gated_recs": (c_i32, [c_p, c_i32, c_p, c_f64, c_f64, c_f32, c_f32, c_p, c_p]),
     "b2p_set_seed_epoch": (c_i32, [c_p]),

@@ -112,19 +112,64 @@ __global__ void __launch_bounds__(NTH) adam_gated_k(const GatedAdamRecs recs, fl
              reinterpret_cast<float*>(rec[3]), rec[4], h.x, b1, b2, eps, wd, h.y, h.z);
 }
 
-// gradient accumulation dst[i] += src[i] over many small tensors in one launch (records by value:
-// capturable, nothing uploaded). blockIdx.y = record, blockIdx.x strides its elements.
-constexpr int ACC_MAXR = 96;
+// gradient accumulation over many small tensors in one launch (records by value: capturable, nothing
+// uploaded). blockIdx.y = record, blockIdx.x strides its elements. Record {dst, src, numel, nrows,
+// set}: dst[i] (set ? = : +=) sum_{r < nrows} src[r * numel + i], rows summed in order — nrows 1 is
+// the plain accumulation; nrows > 1 takes column sums still held as per-tile partial rows (a GEMM
+// epilogue's or b2p_drop_cast_colsum's) and finishes them here, on the side stream.
+constexpr int ACC_MAXR = 64;
 struct AccRecs {
-  int64_t r[ACC_MAXR][3];   // dst, src, numel
+  int64_t r[ACC_MAXR][5];   // dst, src, numel, nrows, set
 };
 __global__ void __launch_bounds__(NTH) accum_rec_k(const AccRecs recs) {
   const int64_t* rec = recs.r[blockIdx.y];
   float* __restrict__ dst = reinterpret_cast<float*>(rec[0]);
   const float* __restrict__ src = reinterpret_cast<const float*>(rec[1]);
-  const int64_t n = rec[2];
+  const int64_t n = rec[2], nrows = rec[3];
+  const bool set = rec[4] != 0;
   const int64_t stride = (int64_t)gridDim.x * NTH;
-  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += stride) dst[i] += src[i];
+  for (int64_t i = (int64_t)blockIdx.x * NTH + threadIdx.x; i < n; i += stride) {
+    // rows in order, 8 loads in flight per step (the partial rows are ~60-130 deep)
+    float v = src[i];
+    int64_t r = 1;
+    for (; r + 8 <= nrows; r += 8) {
+      float q[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) q[k] = src[(r + k) * n + i];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v += q[k];
+    }
+    for (; r < nrows; ++r) v += src[r * n + i];
+    dst[i] = set ? v : dst[i] + v;
+  }
+}
+
+int accum_launch(const int64_t* recs, int width, int ntensors, hipStream_t st) {
+  for (int c0 = 0; c0 < ntensors; c0 += ACC_MAXR) {
+    const int nc = ntensors - c0 < ACC_MAXR ? ntensors - c0 : ACC_MAXR;
+    AccRecs a;
+    int64_t maxn = 0, maxr = 1;
+    for (int i = 0; i < nc; ++i) {
+      const int64_t* q = recs + (int64_t)width * (c0 + i);
+      a.r[i][0] = q[0];
+      a.r[i][1] = q[1];
+      a.r[i][2] = q[2];
+      a.r[i][3] = width == 5 ? q[3] : 1;
+      a.r[i][4] = width == 5 ? q[4] : 0;
+      B2P_CHECK_ARG(a.r[i][2] <= 0 || (a.r[i][0] && a.r[i][1]), "accum_recs: NULL tensor in a record");
+      B2P_CHECK_ARG(a.r[i][3] >= 1, "accum_recs: nrows must be >= 1");
+      maxn = a.r[i][2] > maxn ? a.r[i][2] : maxn;
+      maxr = a.r[i][3] > maxr ? a.r[i][3] : maxr;
+    }
+    if (maxn <= 0) continue;
+    // row-summing records: one element per thread (their cost is the row loop, not the width)
+    const int64_t per = maxr > 1 ? 1 : PER_THREAD;
+    int64_t bx = (maxn + (int64_t)NTH * per - 1) / ((int64_t)NTH * per);
+    if (bx > 1024) bx = 1024;
+    hipLaunchKernelGGL(accum_rec_k, dim3((unsigned)bx, (unsigned)nc), dim3(NTH), 0, st, a);
+  }
+  B2P_CHECK_LAUNCH();
+  return 0;
 }
 }  // namespace
 
@@ -229,20 +274,11 @@ extern "C" int b2p_adam_multi(const int64_t* table, int ntensors, int64_t max_nu
 extern "C" int b2p_accum_recs(const int64_t* recs, int ntensors, b2p_stream_t stream) {
   B2P_CHECK_ARG(recs != nullptr || ntensors == 0, "accum_recs: NULL records");
   B2P_CHECK_ARG(ntensors >= 0, "accum_recs: bad tensor count");
-  for (int c0 = 0; c0 < ntensors; c0 += ACC_MAXR) {
-    const int nc = ntensors - c0 < ACC_MAXR ? ntensors - c0 : ACC_MAXR;
-    AccRecs a;
-    int64_t maxn = 0;
-    for (int i = 0; i < nc; ++i) {
-      for (int k = 0; k < 3; ++k) a.r[i][k] = recs[3 * (c0 + i) + k];
-      B2P_CHECK_ARG(a.r[i][2] <= 0 || (a.r[i][0] && a.r[i][1]), "accum_recs: NULL tensor in a record");
-      maxn = a.r[i][2] > maxn ? a.r[i][2] : maxn;
-    }
-    if (maxn <= 0) continue;
-    int64_t bx = (maxn + (int64_t)NTH * PER_THREAD - 1) / ((int64_t)NTH * PER_THREAD);
-    if (bx > 1024) bx = 1024;
-    hipLaunchKernelGGL(accum_rec_k, dim3((unsigned)bx, (unsigned)nc), dim3(NTH), 0, (hipStream_t)stream, a);
-  }
-  B2P_CHECK_LAUNCH();
-  return 0;
+  return accum_launch(recs, 3, ntensors, (hipStream_t)stream);
+}
+
+extern "C" int b2p_accum_rows_recs(const int64_t* recs, int ntensors, b2p_stream_t stream) {
+  B2P_CHECK_ARG(recs != nullptr || ntensors == 0, "accum_rows_recs: NULL records");
+  B2P_CHECK_ARG(ntensors >= 0, "accum_rows_recs: bad tensor count");
+  return accum_launch(recs, 5, ntensors, (hipStream_t)stream);
 }

@@ -132,11 +132,8 @@ __device__ __forceinline__ bool colsum_arrive(uint32_t* ctr, int nblk, int* flag
   return last;
 }
 
-// colsum_p1v + fold: 128 columns x 8 row lanes per block, as colsum_p1v; every mode (MODE 3: the
-// per-column center Y[b][n .. n+3] held in registers)
-template <int MODE>
-__global__ void __launch_bounds__(256) colsum_fold_v(const float* __restrict__ X, const float* __restrict__ Y,
-                                                     int64_t M, int64_t N, int64_t ld,
+// colsum_p1v + fold: 128 columns x 8 row lanes per block, as colsum_p1v
+__global__ void __launch_bounds__(256) colsum_fold_v(const float* __restrict__ X, int64_t M, int64_t N, int64_t ld,
                                                      int64_t bstride, float* __restrict__ part, int nblk,
                                                      float* __restrict__ out, int accumulate, uint32_t ctr0) {
   __shared__ float4 red[9][32];   // rows 0-7: the reduction; red[8][0]: the "arrived last" flag
@@ -148,20 +145,9 @@ __global__ void __launch_bounds__(256) colsum_fold_v(const float* __restrict__ X
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (n < N) {
     const float* xp = X + b * bstride + n;
-    const float* yp = MODE == 2 ? Y + b * bstride + n : nullptr;
-    const float4 yc = MODE == 3 ? *reinterpret_cast<const float4*>(Y + (int64_t)b * N + n) : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll 4
     for (int64_t m = m0 + rl; m < m1; m += 8) {
-      float4 x = *reinterpret_cast<const float4*>(xp + m * ld);
-      if (MODE == 1) {
-        x.x *= x.x; x.y *= x.y; x.z *= x.z; x.w *= x.w;
-      } else if (MODE == 2) {
-        const float4 y = *reinterpret_cast<const float4*>(yp + m * ld);
-        x.x *= y.x; x.y *= y.y; x.z *= y.z; x.w *= y.w;
-      } else if (MODE == 3) {
-        x.x -= yc.x; x.y -= yc.y; x.z -= yc.z; x.w -= yc.w;
-        x.x *= x.x; x.y *= x.y; x.z *= x.z; x.w *= x.w;
-      }
+      const float4 x = *reinterpret_cast<const float4*>(xp + m * ld);
       s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
     }
   }
@@ -278,21 +264,16 @@ int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_
                 int64_t bstride, int mode, float* out, int accumulate, float* part, hipStream_t st) {
   if (M <= 0 || N <= 0 || batch <= 0) return 0;
   const int nblk = (int)((M + kColsumRows - 1) / kColsumRows);
-  const bool aligned = N % 4 == 0 && ld % 4 == 0 && bstride % 4 == 0 && ((uintptr_t)X & 15u) == 0 &&
-                       ((uintptr_t)part & 15u) == 0;
-  const bool vec = mode == 0 && aligned;
-  // the one-launch form vectorises every mode (Y of mode 2 / 3 aligned like X)
-  const bool fvec = aligned && ((uintptr_t)out & 15u) == 0 && (mode == 0 || mode == 1 || (Y && ((uintptr_t)Y & 15u) == 0));
-  const int64_t gx = fvec ? (N + 127) / 128 : (N + 63) / 64;
+  const bool vec = mode == 0 && N % 4 == 0 && ld % 4 == 0 && bstride % 4 == 0 && ((uintptr_t)X & 15u) == 0 &&
+                   ((uintptr_t)part & 15u) == 0 && ((uintptr_t)out & 15u) == 0;
+  const int64_t gx = vec ? (N + 127) / 128 : (N + 63) / 64;
   const int64_t ctr0 = nblk * N < ((int64_t)1 << 30) ? colsum_ctr_range(gx * batch) : -1;
   if (ctr0 >= 0) {
     dim3 g((unsigned)gx, nblk, (unsigned)batch);
-    if (fvec) {
-      auto k = mode == 0 ? colsum_fold_v<0> : mode == 1 ? colsum_fold_v<1> : mode == 2 ? colsum_fold_v<2>
-                                                                                      : colsum_fold_v<3>;
-      hipLaunchKernelGGL(k, g, dim3(256), 0, st, X, Y, M, N, ld, bstride, part, nblk, out, accumulate,
+    if (vec)
+      hipLaunchKernelGGL(colsum_fold_v, g, dim3(256), 0, st, X, M, N, ld, bstride, part, nblk, out, accumulate,
                          (uint32_t)ctr0);
-    } else
+    else
       hipLaunchKernelGGL(colsum_fold, g, dim3(256), 0, st, X, Y, M, N, ld, bstride, mode, part, nblk, out,
                          accumulate, (uint32_t)ctr0);
     B2P_CHECK_LAUNCH();

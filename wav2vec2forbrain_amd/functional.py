@@ -228,6 +228,8 @@ def _defer_acc(p, g) -> None:
     accumulations go out as ONE multi-tensor launch, b2p_accum_recs)."""
     if _DIAG_SKIP_ACC:
         return
+    if not _LAZY_COLSUM:
+        g = _mat(g)
     _Deferred.accs.append((p, g))
 
 
@@ -240,6 +242,8 @@ def _defer_small(prms, grads):
         if g is not None and _defer_ok(p):
             _defer_acc(p, g)
             out[k] = None
+        else:
+            out[k] = _mat(g)
     return out
 
 
@@ -249,18 +253,32 @@ def _flush_accs(sd) -> None:
     recs, n = [], 0
     with torch.cuda.stream(sd):
         for p, g in _Deferred.accs:
+            if isinstance(g, ColsumParts):   # partial rows: summed (and accumulated) in the batched launch
+                parts = g.parts
+                parts.record_stream(sd)
+                ok = (p.grad is None or (p.grad.is_contiguous() and p.grad.dtype == torch.float32
+                                          and p.grad.numel() == parts.shape[1]))
+                if not ok:
+                    p.grad.add_(g.materialize().view_as(p.grad))
+                    continue
+                st = p.grad is None
+                if st:
+                    p.grad = torch.empty(p.shape, device=parts.device)
+                recs += [p.grad.data_ptr(), parts.data_ptr(), parts.shape[1], parts.shape[0], int(st)]
+                n += 1
+                continue
             g.record_stream(sd)
             if p.grad is None:
                 p.grad = g
             elif (p.grad.is_contiguous() and g.is_contiguous() and p.grad.dtype == g.dtype == torch.float32
                   and p.grad.numel() == g.numel() and p.grad.device == g.device):
-                recs += [p.grad.data_ptr(), g.data_ptr(), g.numel()]
+                recs += [p.grad.data_ptr(), g.data_ptr(), g.numel(), 1, 0]
                 n += 1
             else:
                 p.grad.add_(g)
         if n:
             arr = (ctypes.c_int64 * len(recs))(*recs)
-            _lib.call("b2p_accum_recs", arr, n, _st())
+            _lib.call("b2p_accum_rows_recs", arr, n, _st())
     _Deferred.accs.clear()
 
 
@@ -684,6 +702,28 @@ def colsum_parts_buf(M, N, device):
 def colsum_from_parts(parts, out):
     _lib.call("b2p_colsum_parts", _p(parts), parts.shape[0], parts.shape[1], _p(out), 0, _st())
     return out
+
+
+class ColsumParts:
+    """Column sums still held as per-tile partial rows (a GEMM epilogue's colsum_part or
+    b2p_drop_cast_colsum's): a frozen parameter's deferred accumulation finishes them inside the
+    side stream's batched launch (b2p_accum_rows_recs), everything else calls materialize()."""
+    __slots__ = ("parts",)
+
+    def __init__(self, parts):
+        self.parts = parts
+
+    def materialize(self):
+        return colsum_from_parts(self.parts, torch.empty(self.parts.shape[1], device=self.parts.device))
+
+
+def _mat(g):
+    return g.materialize() if isinstance(g, ColsumParts) else g
+
+
+# B2P_LAZY_COLSUM=0 (A/B): deferred bias gradients are finished by a colsum_p2 launch on the main
+# stream, as before, instead of inside the side stream's batched accumulation
+_LAZY_COLSUM = os.environ.get("B2P_LAZY_COLSUM", "1") != "0"
 
 
 def colsum(x2d_ptr_tensor, M, N, out, ld=None, accumulate=False):
@@ -2003,7 +2043,7 @@ class _EncoderLayer16(torch.autograd.Function):
             else:
                 dw1 = torch.empty_like(w1)
                 gemm(F, D, NT, op(dpre16, 0, F, False), op(x1_16, 0, D, False), dw1, D)
-        db1 = colsum_from_parts(parts, torch.empty(F, device=dev)) if ng[13] else None
+        db1 = ColsumParts(parts) if ng[13] else None   # finished below (deferred) or materialised
         # dx1 = dpre W1 + dy2
         dx1 = torch.empty(NT, D, device=dev)
         gemm(NT, D, F, op(dpre16, 0, F, True), op(w1t16, 0, F, True), dx1, D, residual=dy2)
@@ -2064,6 +2104,8 @@ class _EncoderLayer16(torch.autograd.Function):
             if g is not None and _defer_ok(prm[6 + k]):
                 _defer_acc(prm[6 + k], g)
                 rest[k] = None
+            else:
+                rest[k] = _mat(g)
         return (dx, None, *grads_w, *rest)
 
 
@@ -2229,15 +2271,18 @@ def _dropout_scaled(x, p, seed, scale):
     return y
 
 
-def _drop_cast_colsum(dy, p, seed, scale, want_colsum):
-    """(bf16(dropout(dy) * scale), its column sums or None) in one pass over dy (M x N, fp32)."""
+def _drop_cast_colsum(dy, p, seed, scale, want_colsum, lazy=False):
+    """(bf16(dropout(dy) * scale), its column sums or None) in one pass over dy (M x N, fp32); lazy:
+    the column sums as ColsumParts (for a gradient that goes through _defer_small)."""
     M, N = dy.shape
     y16 = torch.empty(M, N, device=dy.device, dtype=BF16)
     parts = None
     if want_colsum:
         parts = torch.empty(int(_lib.load().b2p_drop_cast_colsum_parts(M)), N, device=dy.device)
     _lib.call("b2p_drop_cast_colsum", _p(dy), _p(y16), _p(parts), M, N, float(p), seed, float(scale), _st())
-    return y16, (colsum_from_parts(parts, torch.empty(N, device=dy.device)) if want_colsum else None)
+    if not want_colsum:
+        return y16, None
+    return y16, (ColsumParts(parts) if lazy else colsum_from_parts(parts, torch.empty(N, device=dy.device)))
 
 
 def _ln_fwd_x16(x2d, g, b, eps, half, want32=True, want_b16=False):
@@ -2380,7 +2425,7 @@ class _FFNBlock(torch.autograd.Function):
         F = w1.shape[0]
         dev = x2.device
         ng = ctx.needs_input_grad
-        dz16, db2 = _drop_cast_colsum(dy, p_hid, s_hid, scale, ctx.has_b[1] and ng[6])
+        dz16, db2 = _drop_cast_colsum(dy, p_hid, s_hid, scale, ctx.has_b[1] and ng[6], lazy=True)
         db1 = None
         f16 = f if f.dtype == BF16 else _act_dropout_cast16(pre, act, p_act, s_act)
         dw2 = _wgrad16(w2, ng[5], dz16, D, f16, F, NT)
@@ -2390,7 +2435,7 @@ class _FFNBlock(torch.autograd.Function):
         gemm(NT, F, D, op(dz16, 0, D, True), op(weight16t(w2), 0, D, True), None, F, drop_p=p_act, seed=s_act,
              act_bwd=act, aux=pre, C16=dpre16, colsum_part=parts)
         if parts is not None:
-            db1 = colsum_from_parts(parts, torch.empty(F, device=dev))
+            db1 = ColsumParts(parts)   # finished by _defer_small (side-stream launch or materialised)
         dw1 = _wgrad16(w1, ng[3], dpre16, F, h if h.dtype == BF16 else cast16(h), D, NT)
         dh = torch.empty(NT, D, device=dev)
         gemm(NT, D, F, op(dpre16, 0, F, True), op(weight16t(w1), 0, F, True), dh, D)
@@ -2567,7 +2612,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
         NT, hd = B * T, D // nh
         dev = x2.device
         ng = ctx.needs_input_grad
-        dz16, dbo = _drop_cast_colsum(dy, p_out, seeds[1], 1.0, ctx.has_b[3] and ng[10])
+        dz16, dbo = _drop_cast_colsum(dy, p_out, seeds[1], 1.0, ctx.has_b[3] and ng[10], lazy=True)
         dwo = _wgrad16(wo, ng[9], dz16, D, O if ctx.fused else cast16(O), D, NT)
         if ctx.fused:
             # qkv / P / Pd / O hold qkv16, lse2, the dropout keep bits and O16 (forward)
