@@ -97,16 +97,21 @@ def host_cpu_info():
     except OSError:
         pass
     n_phys = len(phys) or (os.cpu_count() or 1)
-    caps = [n_phys, len(os.sched_getaffinity(0))]
+    caps = {"physical_cores": n_phys, "affinity": len(os.sched_getaffinity(0))}
     try:
         q, per = open("/sys/fs/cgroup/cpu.max").read().split()
         if q != "max":
-            caps.append(max(1, int(int(q) / int(per))))
+            caps["cgroup_quota"] = max(1, int(int(q) / int(per)))
     except (OSError, ValueError):
         pass
     if os.environ.get("OMP_NUM_THREADS", "").isdigit():
-        caps.append(int(os.environ["OMP_NUM_THREADS"]))
-    return min(caps), n_phys, model
+        caps["OMP_NUM_THREADS"] = int(os.environ["OMP_NUM_THREADS"])
+    HOST_CAPS.clear()
+    HOST_CAPS.update(caps)
+    return min(caps.values()), n_phys, model
+
+
+HOST_CAPS: dict = {}   # the thread caps host_cpu_info() saw (recorded beside the CPU baseline)
 
 
 
@@ -145,8 +150,10 @@ def oracle_steps(cfg, sd, steps, train_dropouts, lr=1e-3):
 
 def cpu_record(times, threads, n_phys, model_name, sample):
     med = sorted(times)[len(times) // 2]
+    bound = sorted(k for k, v in HOST_CAPS.items() if v == threads)
     return {"value": round(1.0 / med, 5), "unit": "steps/s", "cores": threads, "kind": "port",
             "host_physical_cores": n_phys, "cpu_model": model_name,
+            "thread_caps": dict(HOST_CAPS), "bound_by": bound,
             "sample": f"{sample}: median {med:.2f} s/step (all: {', '.join(f'{t:.2f}' for t in times)})"}
 
 
@@ -222,14 +229,36 @@ def log(msg):
     print(f"bench: {msg}", file=sys.stderr, flush=True)
 
 
-def timed_run(kind, args, world, rank, device, use_graph):
+# BASELINE configs[4] per GPU (global batch 64 over 8 GPUs): the Conformer-large with the whole encoder
+# trained (unfreeze_strategy=brain_encoder+w2v: two param groups, w2v lr 1e-4, L2 weight decay 1e-5,
+# b2t_gru_w2v_conformer_experiment.py:87-123)
+FT = dict(bs=8, lr=1e-3, w2v_lr=1e-4, wd=1e-5)
+
+
+def experiment_for(kind, model):
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+    if kind == "conformer_ft":
+        return SyntheticStepExperiment(model, unfreeze="brain_encoder+w2v", lr=FT["lr"], w2v_lr=FT["w2v_lr"],
+                                       weight_decay=FT["wd"])
+    return SyntheticStepExperiment(model, lr=1e-3)
+
+
+def timed_run(kind, args, world, rank, device, use_graph, steps=None, warmup=None, evaluator=None, roofline=None):
     """W warm-up steps + K timed steps of the Trainer's training step (train/train_loop.py, the step
     run.py executes) on the workload, then the GEMM-timing pass. Graph mode: the first W steps run
     eagerly, the next one captures the step (untimed), the K timed steps are replays."""
+    import argparse as _ap
     from wav2vec2forbrain_amd import functional as Fn, _lib
     from wav2vec2forbrain_amd.train.train_loop import Trainer
-    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
-    cfg = make_config(args.bs, args.seq, kind)
+    args = _ap.Namespace(**vars(args))
+    args.steps = steps or args.steps
+    args.warmup = args.warmup if warmup is None else warmup
+    args.evaluator = args.evaluator if evaluator is None else evaluator
+    args.no_roofline = args.no_roofline if roofline is None else not roofline
+    if kind == "conformer_ft":
+        cfg = make_config(FT["bs"], args.seq, "conformer")
+    else:
+        cfg = make_config(args.bs, args.seq, kind)
     model = build(cfg, device)
     model.train()
     if world > 1 and hasattr(model, "sync_batchnorm"):
@@ -243,9 +272,10 @@ def timed_run(kind, args, world, rank, device, use_graph):
     for m in model.modules():
         if hasattr(m, "sync_metrics"):
             m.sync_metrics = False
-    trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+    trainer = Trainer(experiment_for(kind, model))
     trainer.use_graphs = use_graph and trainer.use_graphs
     trainer.capture_after = args.warmup
+    prec = trainer.step_precision() or "bf16"
     batch = batch_on(cfg, device)
 
     def metrics(out):
@@ -283,8 +313,9 @@ def timed_run(kind, args, world, rank, device, use_graph):
         Fn.set_gemm_timing(True)
         if trainer.reducer is not None:
             trainer.reducer.use_layer_gates(None)
-        for _ in range(args.steps):
-            trainer._eager_body(batch)
+        with Fn.precision(prec):
+            for _ in range(args.steps):
+                trainer._eager_body(batch)
         torch.cuda.synchronize()
         Fn.set_gemm_timing(False)
         gemm = ctypes_read_timing()
@@ -293,7 +324,7 @@ def timed_run(kind, args, world, rank, device, use_graph):
         t = torch.tensor([dt], device=device)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = t.item()
-    res = dict(cfg=cfg, dt=dt, losses=loss_host[:, 0].tolist(),
+    res = dict(cfg=cfg, dt=dt, losses=loss_host[:, 0].tolist(), precision=prec, steps=args.steps, warmup=args.warmup,
                wers=loss_host[:, 1].tolist() if args.evaluator else None, gemm=gemm,
                step_mode=("hip-graph replay" if replayed == args.steps else
                           "eager" if replayed == 0 else f"mixed ({replayed}/{args.steps} replayed)"))
@@ -336,6 +367,8 @@ def main():
                     help="skip the eager GEMM-timing pass after the timed region (profiling runs)")
     ap.add_argument("--no-conformer", action="store_true",
                     help="N=1 base runs: skip the nested Conformer-large (configs[2], the north-star target) record")
+    ap.add_argument("--no-extra", action="store_true",
+                    help="N=1 base runs: skip the nested configs[3] / configs[4] / evaluator / fp32-mode records")
     ap.add_argument("--evaluator", action="store_true",
                     help="include the train evaluator's greedy CTC decode + WER (on the device) in every step")
     ap.add_argument("--graph", type=int, default=None,
@@ -420,6 +453,14 @@ def main():
         res["vs_cpu"] = round(res["value"] / res["cpu_baseline"]["value"], 1)
     if world == 1 and args.config == "base" and not args.no_conformer:
         res["conformer_large"] = conformer_record(args, device)
+    if world == 1 and args.config == "base" and not args.no_extra:
+        res["train_evaluator_record"] = evaluator_record(args, device)
+        log("base: exact-fp32 mode steps")
+        res["fp32_mode"] = fp32_mode_record("base", args, device)
+        if "cpu_baseline" in res:
+            res["fp32_mode"]["vs_cpu"] = round(res["fp32_mode"]["value"] / res["cpu_baseline"]["value"], 1)
+        res["large960"] = large_record(args, device)
+        res["conformer_large_ft"] = ft_record(args, device)
     print(json.dumps(res), flush=True)
     if world > 1:
         dist.destroy_process_group()
@@ -455,6 +496,117 @@ def conformer_record(args, device):
     rec["fp32_mode"] = fp32_mode_record("conformer", args, device)
     if "cpu_baseline" in rec:
         rec["fp32_mode"]["vs_cpu"] = round(rec["fp32_mode"]["value"] / rec["cpu_baseline"]["value"], 1)
+    return rec
+
+
+def fixture_parity(name, device):
+    """The CTC losses of the Trainer's deterministic steps on a golden fixture's model and batch
+    (tests/golden/<name>.npz: the reference's own modules and torch.optim.Adam produced that trajectory,
+    tests/golden/make_golden.py) under the Trainer's precision policy, the first step eager and the rest
+    replays, against the reference's losses."""
+    import numpy as np
+    from tests.golden.configs import CONFIGS, make_batch as fixture_batch
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    from wav2vec2forbrain_amd.train.train_loop import Trainer
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment, build_model
+    cfg = {c["name"]: c for c in CONFIGS}[name]
+    a = cfg["adam"]
+    ref = [float(v) for v in np.load(os.path.join(ROOT, "tests", "golden", f"{name}.npz"))["adam_losses"]]
+    model = build_model(cfg, device=device)
+    model.train()
+    exp = SyntheticStepExperiment(model, unfreeze="brain_encoder+w2v" if a["w2v_lr"] is not None else "brain_encoder",
+                                  lr=a["lr"], w2v_lr=a["w2v_lr"], weight_decay=a["wd"])
+    x, day, il, tgt, tl = fixture_batch(cfg)
+    batch = make_b2t_batch(x, tgt, day, il, tl).cuda()
+    trainer = Trainer(exp)
+    trainer.capture_after = 1
+    losses = [float(trainer.train_step(batch).loss) for _ in range(a["steps"])]
+    prec = trainer.step_precision() or "bf16"
+    trainer.release_graphs()
+    Fn.set_deferred_wgrad([])
+    del trainer, model, exp, batch
+    free_device()
+    rel = [abs(g - r) / abs(r) for g, r in zip(losses, ref)]
+    return {"mode": f"deterministic Trainer steps ({prec}; step 1 eager, then replays) vs the reference's own "
+                    f"trajectory (tests/golden/{name}.npz)", "precision": prec,
+            "reference_ctc_loss": [round(v, 6) for v in ref], "hip_ctc_loss": [round(v, 6) for v in losses],
+            "rel_err": [float(f"{r:.3e}") for r in rel], "max_rel_err": float(f"{max(rel):.3e}"),
+            "tolerance": 1e-3, "pass": max(rel) <= 1e-3}
+
+
+def nested(r, metric, kind_text, extra=None):
+    sps = r["steps"] / r["dt"]
+    rec = {"metric": metric, "value": round(sps, 4), "unit": "steps/s",
+           "ms_per_step": round(r["dt"] / r["steps"] * 1e3, 3), "steps": r["steps"], "warmup": r["warmup"],
+           "dtype": r["precision"], "config": dict(kind_text), "step_mode": r["step_mode"],
+           "ctc_loss": round(r["losses"][-1], 5)}
+    rec.update(extra or {})
+    return rec
+
+
+def evaluator_record(args, device):
+    """the headline workload with the reference-equivalent train evaluator in every step
+    (reference src/train/train_loop.py:79 -> src/train/evaluator.py:163-229: greedy CTC decode + WER of
+    the step's logits; here on the device, its value read with the loss)."""
+    log("base + train evaluator: timed Trainer steps")
+    r = timed_run("base", args, 1, 0, device, True if args.graph is None else bool(args.graph), evaluator=True,
+                  roofline=False)
+    return nested(r, "train steps/sec, b2p2t_gru+w2v bs=32 seq=1024 with the train evaluator (greedy decode + WER)",
+                  {"workload": WORKLOAD_TEXT["base"] + ", on-device greedy CTC decode + WER every step",
+                   "per_gpu_batch": args.bs, "seq_len": args.seq, "parallelism": "dp1"},
+                  {"word_error_rate": round(r["wers"][-1], 4)})
+
+
+def large_record(args, device):
+    """BASELINE configs[3] per GPU (global 256 over 8 GPUs = bs 32 each): wav2vec2-large-960h, timed
+    Trainer steps + the 2-step Adam trajectory of the reference on its fixture (large960_bs32)."""
+    log("large960 (configs[3] per GPU): timed Trainer steps")
+    r = timed_run("large", args, 1, 0, device, True if args.graph is None else bool(args.graph), steps=10, warmup=3)
+    rec = nested(r, "train steps/sec + CTC loss, b2p2t_gru+w2v wav2vec2-large-960h bs=32 seq=1024 (configs[3] per GPU)",
+                 {"workload": WORKLOAD_TEXT["large"], "per_gpu_batch": args.bs, "seq_len": args.seq,
+                  "parallelism": "dp1 (configs[3] is dp8, global 256)"},
+                 {"roofline": roofline_record(r["gemm"], "large"),
+                  "step_mfma_frac": round(STEP_TFLOP["large"] * r["steps"] / r["dt"] / BF16_DENSE_PEAK_TFLOPS, 4)})
+    log("large960: fixture trajectory")
+    rec["parity"] = fixture_parity("large960_bs32", device)
+    return rec
+
+
+def ft_record(args, device):
+    """BASELINE configs[4] per GPU (global 64 over 8 GPUs = bs 8 each): the Conformer-large with the whole
+    encoder trained (two param groups), timed Trainer steps in the Trainer's precision policy (bf16x3:
+    split-bf16 GEMMs), its 3-step trajectory against the reference's
+    (conformer_large_ft_bs8), and the same step with the policy off (pure bf16 / fp16 operands) for the
+    cost / accuracy trade."""
+    graph = True if args.graph is None else bool(args.graph)
+    log("conformer_large_ft (configs[4] per GPU): timed Trainer steps")
+    r = timed_run("conformer_ft", args, 1, 0, device, graph, steps=10, warmup=3)
+    x3 = r["precision"] == "bf16x3"
+    roof = roofline_record(r["gemm"], "conformer_ft")
+    if x3:   # three bf16 MFMA products per algorithmic multiply-add
+        roof.update(mfma_work_per_flop=3, mfma_frac=round(3 * roof["frac"], 4))
+    rec = nested(r, "train steps/sec + CTC loss, b2p2t_gru+w2v_conformer-large unfreeze=brain_encoder+w2v bs=8 "
+                    "seq=1024 (configs[4] per GPU)",
+                 {"workload": WORKLOAD_TEXT["conformer"].replace("unfreeze=brain_encoder", "unfreeze=brain_encoder+w2v "
+                                                                 "(w2v lr 1e-4, L2 weight decay 1e-5)"),
+                  "per_gpu_batch": FT["bs"], "seq_len": args.seq, "parallelism": "dp1 (configs[4] is dp8, global 64)"},
+                 {"roofline": roof})
+    log("conformer_large_ft: fixture trajectory")
+    rec["parity"] = fixture_parity("conformer_large_ft_bs8", device)
+    old = os.environ.get("B2P_TRAIN_PRECISION")
+    os.environ["B2P_TRAIN_PRECISION"] = "keep"
+    try:
+        log("conformer_large_ft: policy off (bf16 / fp16 operands)")
+        r2 = timed_run("conformer_ft", args, 1, 0, device, graph, steps=10, warmup=3, roofline=False)
+        rec["policy_off"] = {"dtype": r2["precision"], "value": round(r2["steps"] / r2["dt"], 4),
+                             "ms_per_step": round(r2["dt"] / r2["steps"] * 1e3, 3),
+                             "parity": fixture_parity("conformer_large_ft_bs8", device)}
+    finally:
+        if old is None:
+            os.environ.pop("B2P_TRAIN_PRECISION")
+        else:
+            os.environ["B2P_TRAIN_PRECISION"] = old
     return rec
 
 

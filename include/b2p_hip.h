@@ -110,7 +110,9 @@ typedef struct {
   b2p_epilogue ep;
   int32_t precision;          /* 0 = bf16 MFMA, 1 = fp32 MFMA (parity mode), 2 = fp16 MFMA
                                * (fp32 operands converted while staged; forward of the 24-layer
-                               * Conformer, whose CTC loss bf16 rounding noise biases)          */
+                               * Conformer, whose CTC loss bf16 rounding noise biases), 3 = split
+                               * bf16 (fp32 operands only: x = hi + lo, hi*hi + hi*lo + lo*hi on bf16
+                               * MFMA, ~16 significant bits per product; the bf16x3 mode)       */
   int32_t timing_family;      /* tag for b2p_timing_* (0 = untagged)                          */
   double flops;               /* algorithmic FLOPs of this launch (for timing)                */
   /* split-K (deterministic): ksplit > 1 slices K into kchunk-sized ranges (multiple of 32) whose
@@ -150,6 +152,16 @@ int b2p_colsum_batched(const float* X, const float* Y, int64_t batch, int64_t M,
                        int64_t bstride, int mode, float* out, int accumulate, float* partial,
                        b2p_stream_t stream);
 
+/* One-launch column sums take their arrival counters from a device pool, a fresh range per launch.
+ * The ranges allocated between b2p_colsum_pin_begin and b2p_colsum_pin_end (a graph capture: the graph
+ * replays those launches for as long as it lives) stay reserved until b2p_colsum_unpin(id); no later
+ * launch is handed a reserved counter (when nothing free fits, it takes the two-launch form).
+ * b2p_colsum_pool_state: the allocation cursor (set_cursor >= 0 moves it: tests) and the reserved
+ * counter count. Replaces nothing in the reference (bookkeeping of the fused bias-gradient sums). */
+int b2p_colsum_pin_begin(void);
+int64_t b2p_colsum_pin_end(void);
+int b2p_colsum_unpin(int64_t id);
+int64_t b2p_colsum_pool_state(int64_t set_cursor, int64_t* reserved);
 /* out[n] (+)= sum_t part[t][n] over ntiles rows of a b2p_epilogue.colsum_part buffer */
 int b2p_colsum_parts(const float* part, int64_t ntiles, int64_t N, float* out, int accumulate,
                      b2p_stream_t stream);

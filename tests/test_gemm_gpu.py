@@ -6,7 +6,7 @@ import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 
-TOL = {"fp32": (2e-5, 2e-5), "bf16": (2e-2, 2e-2)}
+TOL = {"fp32": (2e-5, 2e-5), "bf16": (2e-2, 2e-2), "bf16x3": (1e-4, 1e-4)}
 
 
 def _fn():
@@ -21,7 +21,7 @@ def _close(out, ref, mode, scale=None):
     assert err <= atol * scale + rtol * 0, f"max err {err} vs scale {scale} ({mode})"
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("mode", ["fp32", "bf16", "bf16x3"])
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (130, 70, 37), (1, 33, 5), (300, 257, 96), (64, 48, 6144)])
 def test_nt_nn_tn(mode, M, N, K):
     Fn = _fn()
@@ -48,7 +48,28 @@ def test_nt_nn_tn(mode, M, N, K):
         _close(out3[:, :N], at[:, :M].t() @ b[:, :N], mode)
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+def test_split_bf16_accuracy():
+    """precision 3 (split bf16, the bf16x3 mode): the relative error of a K = 4096 product against an fp64
+    reference is within a few 2^-16 (the bf16 mode's is ~2^-9); K >= 2048 on 4 output tiles makes it a
+    split-K launch (slabs summed in slice order); operands span 1e-6 .. 1e2 (bf16 keeps fp32's range)."""
+    Fn = _fn()
+    torch.manual_seed(3)
+    M, N, K = 256, 192, 4096
+    a = torch.randn(M, K, device="cuda") * torch.logspace(-6, 2, K, device="cuda")[torch.randperm(K, device="cuda")]
+    w = torch.randn(N, K, device="cuda")
+    ref = a.double() @ w.double().t()
+    errs = {}
+    for mode in ("bf16", "bf16x3"):
+        with Fn.precision(mode):
+            out = torch.empty(M, N, device="cuda")
+            Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), out, N)
+        errs[mode] = float((out.double() - ref).norm() / ref.norm())
+    print(errs)
+    assert errs["bf16x3"] <= 3e-5, errs
+    assert errs["bf16x3"] * 50 <= errs["bf16"], errs
+
+
+@pytest.mark.parametrize("mode", ["fp32", "bf16", "bf16x3"])
 def test_epilogue(mode):
     Fn = _fn()
     torch.manual_seed(1)

@@ -1052,3 +1052,64 @@ def test_accum_rows_recs():
     torch.cuda.synchronize()
     for d, ref in zip(dsts, refs):
         assert _rel(d, ref) < 1e-5
+
+
+def test_colsum_pinned_counters_survive_pool_wrap():
+    """Counter ranges of captured graphs stay reserved (b2p_colsum_pin_begin / _end / _unpin, as
+    StepGraph.capture does): two captured graphs, then the allocation cursor moved to just before each
+    graph's range so that the rotation wraps across them, then eager launches on a concurrent stream
+    racing the replays of both graphs. Every result equals the fp64 sum; no eager launch was handed a
+    reserved counter; unpinning frees the ranges."""
+    import ctypes
+    from wav2vec2forbrain_amd import _lib
+    Fn = _fn()
+    lib = _lib.load()
+    torch.manual_seed(5)
+    M, N, batch = 3000, 1000, 4
+    X = torch.randn(batch, M, N, device="cuda") + 0.25
+    ref = X.double().sum(1)
+
+    def run(out, stream=None):
+        ws = torch.empty(int(lib.b2p_colsum_workspace(M, N)) * batch, device="cuda")
+        _lib.call("b2p_colsum_batched", Fn._p(X), None, batch, M, N, N, M * N, 0, Fn._p(out), 0, Fn._p(ws),
+                  ctypes_stream(stream))
+        return ws
+
+    res = ctypes.c_int64()
+    lib.b2p_colsum_pool_state(-1, ctypes.byref(res))
+    reserved0 = res.value
+    graphs, outs, keep, pins, starts = [], [], [], [], []
+    s = torch.cuda.Stream()
+    for _ in range(2):
+        g = torch.cuda.CUDAGraph()
+        o = torch.zeros(batch, N, device="cuda")
+        s.wait_stream(torch.cuda.current_stream())
+        starts.append(lib.b2p_colsum_pool_state(-1, None))
+        _lib.check(lib.b2p_colsum_pin_begin(), "pin_begin")
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                keep.append(run(o))
+        pins.append(lib.b2p_colsum_pin_end())
+        graphs.append(g)
+        outs.append(o)
+    lib.b2p_colsum_pool_state(-1, ctypes.byref(res))
+    assert res.value - reserved0 >= 2 * ((N + 127) // 128) * batch, res.value
+    side = torch.cuda.Stream()
+    for start in starts:
+        lib.b2p_colsum_pool_state(start, None)        # the next eager range would overlap this graph's
+        eager = [torch.empty(batch, N, device="cuda") for _ in range(4)]
+        torch.cuda.synchronize()
+        with torch.cuda.stream(side):
+            ks = [run(e, stream=side) for e in eager]
+        for g, o in zip(graphs, outs):
+            o.zero_()
+            g.replay()
+        torch.cuda.synchronize()
+        for o in outs + eager:
+            assert _rel(o.double(), ref) < 2e-6 * math.sqrt(M)
+        del ks
+    for p in pins:
+        lib.b2p_colsum_unpin(p)
+    lib.b2p_colsum_pool_state(-1, ctypes.byref(res))
+    assert res.value == reserved0, (res.value, reserved0)
+    del keep

@@ -69,6 +69,10 @@ _SIGS = {
     "b2p_colsum": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i32, c_p, c_p]),
     "b2p_colsum_batched": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32, c_p, c_p]),
     "b2p_colsum_parts": (c_i32, [c_p, c_i64, c_i64, c_p, c_i32, c_p]),
+    "b2p_colsum_pin_begin": (c_i32, []),
+    "b2p_colsum_pin_end": (c_i64, []),
+    "b2p_colsum_unpin": (c_i32, [c_i64]),
+    "b2p_colsum_pool_state": (c_i64, [c_i64, ctypes.POINTER(c_i64)]),
     "b2p_dropout": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_p]),
     "b2p_layernorm_fwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_u64, c_p]),
     "b2p_layernorm_bwd_workspace": (c_i64, [c_i64, c_i64]),

@@ -85,6 +85,11 @@ def ensure_built() -> str:
 def _build_locked(verbose: bool, jobs: int | None) -> str:
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
     hmt = _headers_mtime()
+    # a library newer than every source, header and kernel template is current even without the
+    # objects (a snapshot that carries the built .so but not build/)
+    newest_src = max([hmt] + [max(os.path.getmtime(s), _inc_mtime(s)) for s in srcs])
+    if os.path.exists(LIB) and os.path.getmtime(LIB) >= newest_src:
+        return LIB
     # the GPU box reports the whole machine's CPUs; its share is 16
     jobs = jobs or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:

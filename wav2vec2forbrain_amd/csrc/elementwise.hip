@@ -4,6 +4,10 @@
 #include "common.h"
 #include <stdlib.h>
 #include <atomic>
+#include <map>
+#include <mutex>
+#include <utility>
+#include <vector>
 #include "../../include/b2p_hip.h"
 
 namespace {
@@ -107,7 +111,7 @@ __global__ void __launch_bounds__(256) colsum_p2(const float* __restrict__ part,
 // the counter to 0 for the next launch. Counters: a zero-initialised device pool; each launch takes a
 // fresh range (host-side rotation), so launches on different streams / graph branches never share one.
 // Replaces the separate colsum_p2 launch (~5 us of ramp for ~16-64 KB of partials) per reduction.
-constexpr int kCtrPool = 1 << 16;
+constexpr int kCtrPool = 1 << 18;
 __device__ uint32_t g_colsum_ctr[kCtrPool];
 
 typedef __amdgpu_buffer_rsrc_t rsrc_t;
@@ -241,6 +245,48 @@ __global__ void __launch_bounds__(256) colsum_fold(const float* __restrict__ X, 
   }
 }
 
+// Counter allocation. Every launch takes a fresh range by host-side rotation over the pool. A captured
+// graph replays its launches' ranges for as long as it lives, so the ranges allocated while a capture
+// records (b2p_colsum_pin_begin .. _end) stay reserved until b2p_colsum_unpin: later launches (eager,
+// or another graph, possibly on a concurrent stream) skip them and never share a counter with a live
+// graph. When no free range fits, the launch falls back to the two-launch form (no counter at all).
+struct CtrPool {
+  std::mutex mu;
+  uint32_t cursor = 0;
+  bool recording = false;
+  int64_t next_id = 1;
+  std::vector<std::pair<uint32_t, uint32_t>> rec;                            // ranges of the recording
+  std::map<int64_t, std::vector<std::pair<uint32_t, uint32_t>>> pins;        // id -> reserved ranges
+
+  // first start >= base at which [start, start + n) misses every reserved range (or kCtrPool)
+  uint32_t fit(uint32_t base, uint32_t n) const {
+    bool moved = true;
+    while (moved && base + n <= (uint32_t)kCtrPool) {
+      moved = false;
+      for (const auto& kv : pins)
+        for (const auto& r : kv.second)
+          if (base < r.second && r.first < base + n) { base = r.second; moved = true; }
+    }
+    return base;
+  }
+  int64_t alloc(uint32_t n) {
+    std::lock_guard<std::mutex> g(mu);
+    uint32_t b = fit(cursor, n);
+    if (b + n > (uint32_t)kCtrPool) b = fit(0, n);    // wrap once
+    if (b + n > (uint32_t)kCtrPool) return -1;        // everything left is reserved by live graphs
+    cursor = b + n;
+    if (recording) {
+      if (!rec.empty() && rec.back().second == b) rec.back().second = b + n;
+      else rec.emplace_back(b, b + n);
+    }
+    return b;
+  }
+};
+CtrPool& ctr_pool() {
+  static CtrPool p;
+  return p;
+}
+
 // first counter of a fresh range of n (n <= kCtrPool / 4), or -1 when the one-launch form is off
 int64_t colsum_ctr_range(int64_t n) {
   static const bool on = [] {
@@ -248,16 +294,50 @@ int64_t colsum_ctr_range(int64_t n) {
     return !(e && e[0] == '0');
   }();
   if (!on || n > kCtrPool / 4) return -1;
-  static std::atomic<uint32_t> next{0};
-  uint32_t cur = next.load(std::memory_order_relaxed), base, nxt;
-  do {
-    base = cur + (uint32_t)n <= (uint32_t)kCtrPool ? cur : 0u;
-    nxt = base + (uint32_t)n;
-  } while (!next.compare_exchange_weak(cur, nxt, std::memory_order_relaxed));
-  return base;
+  return ctr_pool().alloc((uint32_t)n);
 }
 
 }  // namespace
+
+extern "C" int b2p_colsum_pin_begin(void) {
+  CtrPool& p = ctr_pool();
+  std::lock_guard<std::mutex> g(p.mu);
+  B2P_CHECK_ARG(!p.recording, "colsum_pin_begin: a recording is already open");
+  p.recording = true;
+  p.rec.clear();
+  return 0;
+}
+
+extern "C" int64_t b2p_colsum_pin_end(void) {
+  CtrPool& p = ctr_pool();
+  std::lock_guard<std::mutex> g(p.mu);
+  if (!p.recording) { b2p_set_error("colsum_pin_end: no recording is open"); return -1; }
+  p.recording = false;
+  const int64_t id = p.next_id++;
+  p.pins[id] = p.rec;
+  p.rec.clear();
+  return id;
+}
+
+extern "C" int b2p_colsum_unpin(int64_t id) {
+  CtrPool& p = ctr_pool();
+  std::lock_guard<std::mutex> g(p.mu);
+  p.pins.erase(id);
+  return 0;
+}
+
+extern "C" int64_t b2p_colsum_pool_state(int64_t set_cursor, int64_t* reserved) {
+  CtrPool& p = ctr_pool();
+  std::lock_guard<std::mutex> g(p.mu);
+  if (set_cursor >= 0 && set_cursor < kCtrPool) p.cursor = (uint32_t)set_cursor;
+  if (reserved) {
+    int64_t r = 0;
+    for (const auto& kv : p.pins)
+      for (const auto& q : kv.second) r += q.second - q.first;
+    *reserved = r;
+  }
+  return p.cursor;
+}
 
 // out[b][n] (+)= sum_m f(X[b][m][n]); mode 0: x, 1: x^2, 2: x*Y[b][m][n], 3: (x - Y[b][n])^2
 int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_t N, int64_t ld,

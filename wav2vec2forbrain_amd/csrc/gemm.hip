@@ -44,12 +44,26 @@ template <int KB> struct Prec<2, KB> {   // fp16 MFMA (same rate as bf16, 3 more
   typedef _Float16 T;
   static constexpr int LDS_STRIDE = KB + 8;
 };
+// split bf16 ("bf16x3"): x = hi + lo with hi = bf16(x), lo = bf16(x - hi), two LDS planes; the
+// product is hi*hi + hi*lo + lo*hi on bf16 MFMA (the dropped lo*lo is ~2^-18 relative): about 16
+// significant bits per product at a third of the bf16 MFMA rate, five times the exact-fp32 MFMA rate
+template <int KB> struct Prec<3, KB> {
+  typedef __bf16 T;
+  static constexpr int LDS_STRIDE = KB + 8;
+};
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 template <int PREC, int KB>
-__device__ __forceinline__ void st4(typename Prec<PREC, KB>::T* dst, float a, float b, float c, float d) {
-  if constexpr (PREC == 0) {
+__device__ __forceinline__ void st4(typename Prec<PREC, KB>::T* dst, float a, float b, float c, float d,
+                                    int plane = 0) {
+  if constexpr (PREC == 3) {
+    bf16x4 h = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+    bf16x4 l = {(__bf16)(a - (float)h[0]), (__bf16)(b - (float)h[1]), (__bf16)(c - (float)h[2]),
+                (__bf16)(d - (float)h[3])};
+    *reinterpret_cast<bf16x4*>(dst) = h;
+    *reinterpret_cast<bf16x4*>(dst + plane) = l;
+  } else if constexpr (PREC == 0) {
     bf16x4 v = {(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
     *reinterpret_cast<bf16x4*>(dst) = v;
   } else if constexpr (PREC == 2) {
@@ -189,13 +203,13 @@ struct Loader {
     }
   }
 
-  __device__ __forceinline__ void store(typename Prec<PREC, KB>::T* lds, int tid) {
+  __device__ __forceinline__ void store(typename Prec<PREC, KB>::T* lds, int tid, int plane = 0) {
     constexpr int LS = Prec<PREC, KB>::LDS_STRIDE;
     if constexpr (INNER_K) {
 #pragma unroll
       for (int i = 0; i < NV; ++i) {
         const int row = tid / CPR + RPP * i;
-        st4<PREC, KB>(lds + row * LS + (tid % CPR) * 4, v[i].x, v[i].y, v[i].z, v[i].w);
+        st4<PREC, KB>(lds + row * LS + (tid % CPR) * 4, v[i].x, v[i].y, v[i].z, v[i].w, plane);
       }
     } else {
       if (!active) return;
@@ -205,10 +219,10 @@ struct Loader {
         const int c = bidx % NC, g = bidx / NC;
         typename Prec<PREC, KB>::T* d = lds + (4 * c) * LS + 4 * g;
         const float4* w = v + 4 * q;
-        st4<PREC, KB>(d + 0 * LS, w[0].x, w[1].x, w[2].x, w[3].x);
-        st4<PREC, KB>(d + 1 * LS, w[0].y, w[1].y, w[2].y, w[3].y);
-        st4<PREC, KB>(d + 2 * LS, w[0].z, w[1].z, w[2].z, w[3].z);
-        st4<PREC, KB>(d + 3 * LS, w[0].w, w[1].w, w[2].w, w[3].w);
+        st4<PREC, KB>(d + 0 * LS, w[0].x, w[1].x, w[2].x, w[3].x, plane);
+        st4<PREC, KB>(d + 1 * LS, w[0].y, w[1].y, w[2].y, w[3].y, plane);
+        st4<PREC, KB>(d + 2 * LS, w[0].z, w[1].z, w[2].z, w[3].z, plane);
+        st4<PREC, KB>(d + 3 * LS, w[0].w, w[1].w, w[2].w, w[3].w, plane);
       }
     }
   }
@@ -234,7 +248,9 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
   constexpr int LS = Prec<PREC, KB>::LDS_STRIDE;
   constexpr int WM = BM / 2, WN = BN / 2;     // wave tile
   constexpr int TM = WM / 16, TN = WN / 16;   // 16x16 MFMA tiles per wave
-  __shared__ __attribute__((aligned(16))) T smem[2 * (BM + BN) * LS];
+  // split bf16: the lo plane follows the two hi buffers
+  constexpr int PLANE = PREC == 3 ? 2 * (BM + BN) * LS : 0;
+  __shared__ __attribute__((aligned(16))) T smem[(PREC == 3 ? 2 : 1) * 2 * (BM + BN) * LS];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -269,8 +285,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
   const int nk = (K > kbeg && !b2p_gated_off(ea.gate)) ? (K - kbeg + KB - 1) / KB : 0;
   la.load(sa, tid, kbeg, K);
   lb.load(sb, tid, kbeg, K);
-  la.store(AS_(0), tid);
-  lb.store(BS_(0), tid);
+  la.store(AS_(0), tid, PLANE);
+  lb.store(BS_(0), tid, PLANE);
   __syncthreads();
 
   for (int kt = 0; kt < nk; ++kt) {
@@ -297,6 +313,32 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
 #pragma unroll
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+    } else if constexpr (PREC == 3) {
+#pragma unroll
+      for (int kk = 0; kk < KB / 32; ++kk) {
+        bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int o = (wm * WM + i * 16 + (lane & 15)) * LS + 32 * kk + 8 * (lane >> 4);
+          ah[i] = *reinterpret_cast<const bf16x8*>(A_ + o);
+          al[i] = *reinterpret_cast<const bf16x8*>(A_ + PLANE + o);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int o = (wn * WN + j * 16 + (lane & 15)) * LS + 32 * kk + 8 * (lane >> 4);
+          bh[j] = *reinterpret_cast<const bf16x8*>(B_ + o);
+          bl[j] = *reinterpret_cast<const bf16x8*>(B_ + PLANE + o);
+        }
+        // the two correction products first, then the leading one
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+          }
       }
     } else if constexpr (PREC == 2) {
 #pragma unroll
@@ -330,8 +372,8 @@ __global__ void __launch_bounds__(NT) gemm_kernel(const b2p_gemm_desc d, const E
       }
     }
     if (more) {
-      la.store(AS_(cur ^ 1), tid);
-      lb.store(BS_(cur ^ 1), tid);
+      la.store(AS_(cur ^ 1), tid, PLANE);
+      lb.store(BS_(cur ^ 1), tid, PLANE);
     }
     __syncthreads();
   }
@@ -383,6 +425,8 @@ int launch_prec(const b2p_gemm_desc& d, const EpiArgs& ea, hipStream_t st) {
   dim3 grid((unsigned)((d.N + BN - 1) / BN), (unsigned)((d.M + BM - 1) / BM), (unsigned)(d.nz1 * d.nz2 * ks));
   if (d.precision == 1)
     hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKin, ACONV, BCONV, 1>), grid, dim3(NT), 0, st, d, ea);
+  else if (d.precision == 3)
+    hipLaunchKernelGGL((gemm_kernel<BM, BN, 32, AK, BKin, ACONV, BCONV, 3>), grid, dim3(NT), 0, st, d, ea);
   else if (d.precision == 2 && (ks == 1 || d.kchunk % 64 == 0))
     hipLaunchKernelGGL((gemm_kernel<BM, BN, 64, AK, BKin, ACONV, BCONV, 2>), grid, dim3(NT), 0, st, d, ea);
   else if (d.precision == 2)
@@ -427,7 +471,8 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   B2P_CHECK_ARG(d.M >= 0 && d.N >= 0 && d.K >= 0, "gemm: negative size");
   B2P_CHECK_ARG(d.M < (1ll << 31) && d.N < (1ll << 31) && d.K < (1ll << 31), "gemm: size too large");
   B2P_CHECK_ARG(d.nz1 >= 1 && d.nz2 >= 1, "gemm: batch dims must be >= 1");
-  B2P_CHECK_ARG(d.precision >= 0 && d.precision <= 2, "gemm: precision must be 0 (bf16), 1 (fp32) or 2 (fp16)");
+  B2P_CHECK_ARG(d.precision >= 0 && d.precision <= 3,
+                "gemm: precision must be 0 (bf16), 1 (fp32), 2 (fp16) or 3 (split bf16)");
   if (d.M == 0 || d.N == 0) return 0;
   B2P_CHECK_ARG(d.ep.C != nullptr || d.ep.C16 != nullptr, "gemm: C and C16 are NULL");
   B2P_CHECK_ARG(d.ep.C != nullptr || d.ep.beta == 0.f, "gemm: beta != 0 needs C");

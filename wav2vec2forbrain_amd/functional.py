@@ -90,15 +90,20 @@ def _gate_aware(cls):
 _FLUSH_PER_BLOCK = os.environ.get("B2P_WGRAD_FLUSH", "gru") == "block"
 
 
+PRECISION_MODES = {"bf16": 0, "fp32": 1, "bf16x3": 3}   # GemmDesc.precision of each mode's fp32-operand GEMMs
+
+
 def _prec() -> int:
     return _state.prec
 
 
 @contextlib.contextmanager
 def precision(mode: str):
-    """'bf16' (default: bf16 MFMA, fp32 accumulate) or 'fp32' (exact-fp32 MFMA parity mode)."""
+    """'bf16' (default: bf16 / fp16 MFMA, fp32 accumulate), 'fp32' (exact-fp32 MFMA parity mode) or
+    'bf16x3' (the fp32 mode's operators with every GEMM on split-bf16 operands: hi*hi + hi*lo + lo*hi,
+    ~16 significant bits per product, at a third of the bf16 MFMA rate instead of a sixteenth)."""
     old = _prec()
-    _state.prec = {"bf16": 0, "fp32": 1}[mode]
+    _state.prec = PRECISION_MODES[mode]
     try:
         yield
     finally:
@@ -122,6 +127,8 @@ def forward_f16(on: bool = True):
 
 # error attribution (tools/bf16_err.py): blocks listed in B2P_FP32_OPS run their forward in exact fp32
 _FP32_OPS = set(filter(None, os.environ.get("B2P_FP32_OPS", "").split(",")))
+# error attribution (tools/traj_err_ft.py): named precision switches of a diagnostic run
+DIAG_SWITCHES: set = set(filter(None, os.environ.get("B2P_DIAG", "").split(",")))
 
 
 @contextlib.contextmanager
@@ -156,11 +163,14 @@ def _prec_follow(cls):
 
     @functools.wraps(bwd)
     def backward(ctx, *grads):
+        if "bwd32path" in DIAG_SWITCHES:   # diagnostic: fp32-operand backward, GEMMs rounding to fp16 / bf16
+            with forward_f16("bwdf16" in DIAG_SWITCHES):
+                return bwd(ctx, *grads)
         if ctx.block in _FP32_BWD_ONLY and _state.prec != 1:
             with precision("fp32"):
                 return bwd(ctx, *grads)
         if (_BWD_FOLLOWS_FWD[0] or ctx.block in _FP32_BWD_OPS) and ctx.prec_fwd != _state.prec:
-            with precision({0: "bf16", 1: "fp32"}[ctx.prec_fwd]):
+            with precision({v: k for k, v in PRECISION_MODES.items()}[ctx.prec_fwd]):
                 return bwd(ctx, *grads)
         return bwd(ctx, *grads)
 
@@ -249,10 +259,23 @@ def _defer_small(prms, grads):
 
 def _flush_accs(sd) -> None:
     """The queued small-gradient accumulations on side stream sd: a parameter without .grad takes
-    the tensor itself, the rest are batched into b2p_accum_recs records {p.grad, g, numel}."""
-    recs, n = [], 0
+    the tensor itself, the rest are batched into b2p_accum_rows_recs records {p.grad, g, numel}. The
+    records of one launch run in parallel (one per blockIdx.y), so a destination appears at most once
+    per launch: a parameter queued twice in one flush goes into the next launch, after the first."""
+    recs, n, dsts = [], 0, set()
+
+    def launch():
+        nonlocal recs, n
+        if n:
+            arr = (ctypes.c_int64 * len(recs))(*recs)
+            _lib.call("b2p_accum_rows_recs", arr, n, _st())
+        recs, n = [], 0
+        dsts.clear()
+
     with torch.cuda.stream(sd):
         for p, g in _Deferred.accs:
+            if p.grad is not None and p.grad.data_ptr() in dsts:
+                launch()
             if isinstance(g, ColsumParts):   # partial rows: summed (and accumulated) in the batched launch
                 parts = g.parts
                 parts.record_stream(sd)
@@ -265,6 +288,7 @@ def _flush_accs(sd) -> None:
                 if st:
                     p.grad = torch.empty(p.shape, device=parts.device)
                 recs += [p.grad.data_ptr(), parts.data_ptr(), parts.shape[1], parts.shape[0], int(st)]
+                dsts.add(p.grad.data_ptr())
                 n += 1
                 continue
             g.record_stream(sd)
@@ -273,12 +297,11 @@ def _flush_accs(sd) -> None:
             elif (p.grad.is_contiguous() and g.is_contiguous() and p.grad.dtype == g.dtype == torch.float32
                   and p.grad.numel() == g.numel() and p.grad.device == g.device):
                 recs += [p.grad.data_ptr(), g.data_ptr(), g.numel(), 1, 0]
+                dsts.add(p.grad.data_ptr())
                 n += 1
             else:
                 p.grad.add_(g)
-        if n:
-            arr = (ctypes.c_int64 * len(recs))(*recs)
-            _lib.call("b2p_accum_rows_recs", arr, n, _st())
+        launch()
     _Deferred.accs.clear()
 
 
@@ -431,7 +454,7 @@ def segments_remaining() -> int:
 
 
 def set_precision(mode: str) -> None:
-    _state.prec = {"bf16": 0, "fp32": 1}[mode]
+    _state.prec = PRECISION_MODES[mode]
 
 
 _GEMM_TIMING = [0]
@@ -783,6 +806,11 @@ def _ln_bwd(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, s
 BF16 = torch.bfloat16
 _PARAM_EPOCH: dict = {}
 _W16: dict = {}
+
+
+def _bwd16_path() -> bool:
+    """A block backward takes its 16-bit-operand form (not under the bwd32path diagnostic)."""
+    return bf16_mode() and "bwd32path" not in DIAG_SWITCHES
 
 
 def bf16_mode() -> bool:
@@ -2390,7 +2418,7 @@ class _FFNBlock(torch.autograd.Function):
         dev = x2.device
         ng = ctx.needs_input_grad
         dy = dy.contiguous().view(NT, D)
-        if bf16_mode() or h.dtype != torch.float32:
+        if _bwd16_path() or h.dtype != torch.float32:
             return _FFNBlock._backward16(ctx, dy, x2, h, mean, rstd, pre, f, g, w1, w2)
         dz = _dropout_scaled(dy, p_hid, s_hid, scale)
         dw2 = db2 = dw1 = db1 = None
@@ -2564,7 +2592,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
         ng = ctx.needs_input_grad
         hr_ = h if hr is None else hr
         dy = dy.contiguous().view(NT, D)
-        if bf16_mode() or ctx.fused:
+        if _bwd16_path() or ctx.fused:
             return _ConformerAttnBlock._backward16(ctx, dy, x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv,
                                                    wo, cos_t, sin_t)
         dz = _dropout_scaled(dy, p_out, seeds[1], 1.0)
@@ -2776,7 +2804,7 @@ class _ConvModule(torch.autograd.Function):
         dev = x2.device
         ng = ctx.needs_input_grad
         dy = dy.contiguous().view(NT, D)
-        b16 = bf16_mode() or h.dtype != torch.float32   # bf16 operands: each cast once, frozen wgrads deferred
+        b16 = _bwd16_path() or h.dtype != torch.float32   # bf16 operands: each cast once, frozen wgrads deferred
         ds = torch.empty(NT, D, device=dev)
         if b16:
             do16, _ = _drop_cast_colsum(dy, p, seed, 1.0, False)

@@ -120,8 +120,11 @@ class HipAdam(torch.optim.Optimizer):
 
     def add_param_group(self, param_group) -> None:
         """torch.optim.Optimizer.add_param_group; in the device form the new group gets its device lr,
-        step counters and state right away (a replayed update walks every group's device record)."""
+        step counters and state right away. A step captured BEFORE this call holds update records for
+        the old groups only: `generation` advances, and the Trainer re-captures its cached steps when it
+        sees a new generation (train_loop.Trainer.train_step)."""
         super().add_param_group(param_group)
+        self.generation = getattr(self, "generation", 0) + 1
         if getattr(self, "capturable", False):
             self.capturable = False
             dev, self._dev = self._dev, []

@@ -29,6 +29,8 @@ from __future__ import annotations
 
 from typing import Iterable
 
+from collections import deque
+
 import torch
 import torch.distributed as dist
 
@@ -72,9 +74,10 @@ class GradBucketReducer:
                 self.views[p] = flat[off:off + p.numel()].view_as(p)
                 off += p.numel()
             self.flat.append(flat)
-        self.launch_log: list[int] = []     # bucket indices in the order their collectives were issued
+        # diagnostics (bounded: a long run issues ~40 bucket launches per step)
+        self.launch_log: deque = deque(maxlen=4096)    # bucket indices in the order their collectives were issued
         # per launch: the captured segments a replay still ran after it (> 0: overlapped the backward)
-        self.launch_tail: list[int] = []
+        self.launch_tail: deque = deque(maxlen=4096)
         # "used by some rank this step" per parameter (int32, MAX-reduced in finish()): the gates
         # HipAdam's device form reads (opt.gates = reducer.gates), so a parameter no rank used —
         # every rank's LayerDrop dropped its layer — is left untouched, as torch.optim.Adam leaves a

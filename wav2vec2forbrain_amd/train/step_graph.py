@@ -85,6 +85,8 @@ class _SegmentedCapture:
         self.cur = g
 
     def end(self) -> None:
+        if self.cur is None:   # an error between a split's end() and its begin(): nothing is capturing
+            return
         with torch.cuda.stream(self.stream):
             self.cur.capture_end()
         self.graphs.append(self.cur)
@@ -129,6 +131,7 @@ class StepGraph:
         self.loss = None
         self.epoch = epoch
         self.segmented = segmented
+        self.pin = None        # the reserved column-sum counter ranges (b2p_colsum_pin_end id)
 
     def capture(self) -> None:
         live = live_graph_nodes()
@@ -160,6 +163,22 @@ class StepGraph:
         # optimizer's host step counters as they were (after_replay advances them per replay)
         steps = ({p: st["step"].clone() for p, st in self.opt.state.items() if "step" in st}
                  if self.opt is not None else {})
+        # the column-sum arrival counters this capture's launches take stay reserved while it lives
+        _lib.check(lib.b2p_colsum_pin_begin(), "b2p_colsum_pin_begin")
+        try:
+            self._capture_graph(s)
+        except BaseException:
+            lib.b2p_colsum_unpin(lib.b2p_colsum_pin_end())
+            raise
+        self.pin = lib.b2p_colsum_pin_end()
+        torch.cuda.synchronize()
+        for p, t in steps.items():
+            self.opt.state[p]["step"] = t
+        for _ in range(self.warm_replays):   # first launches of a new graph pay its upload
+            self.replay()
+        torch.cuda.synchronize()
+
+    def _capture_graph(self, s) -> None:
         if self.segmented:
             g = _SegmentedCapture(s)
             Fn._Segments.active = g
@@ -180,13 +199,7 @@ class StepGraph:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g, stream=s):
                 self.loss = self._one()
-        torch.cuda.synchronize()
-        for p, t in steps.items():
-            self.opt.state[p]["step"] = t
         self.graph = g
-        for _ in range(self.warm_replays):   # first launches of a new graph pay its upload
-            self.replay()
-        torch.cuda.synchronize()
 
     def _one(self):
         _lib.check(_lib.load().b2p_seed_epoch_step(ctypes.c_void_p(self.epoch.data_ptr()),
@@ -216,5 +229,8 @@ class StepGraph:
         if self.graph is not None:
             torch.cuda.synchronize()
             self.graph.reset()
+        if self.pin is not None:
+            _lib.load().b2p_colsum_unpin(self.pin)
+            self.pin = None
         self.graph = None
         self.loss = None

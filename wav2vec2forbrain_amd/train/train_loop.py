@@ -61,6 +61,15 @@ class Trainer:
                 self.frozen_reducer = GradBucketReducer(frozen, overlap=False, grad_views=False, track_used=False)
         # frozen parameters (not optimised): their gradient GEMMs run deferred beside the GRU backward
         Fn.set_deferred_wgrad(frozen)
+        # precision policy of the default (bf16) mode: with the w2v encoder trained (full fine-tuning,
+        # unfreeze_strategy=brain_encoder+w2v) the step runs in the bf16x3 mode. Adam's first updates of
+        # the ~600 M encoder parameters are ~lr * sign(g), and the 16-bit operands' rounding (bf16 or fp16,
+        # forward or backward) moved the 3-step CTC-loss trajectory 1.3e-3 .. 7.4e-3 away from the
+        # reference's; split-bf16 GEMMs hold it at 1.3e-4 (tools/traj_err_ft.py).
+        # B2P_TRAIN_PRECISION: auto (this policy) | keep (the ambient mode as it is)
+        enc = getattr(self.model, "w2v_encoder", None)
+        self.encoder_trained = enc is not None and any(id(p) in opt_ids for p in enc.parameters())
+        self.precision_policy = os.environ.get("B2P_TRAIN_PRECISION", "auto")
         # replayed steps (see train_step): a cache of captured steps keyed by the batch shape
         self.use_graphs = (os.environ.get("B2P_TRAINER_GRAPH", "1") != "0" and torch.cuda.is_available()
                            and hasattr(self.optimizer, "make_capturable"))
@@ -70,6 +79,7 @@ class Trainer:
         # statistics, gradient buckets); 0: one graph, SyncBN steps eager, buckets after the replay
         self.segmented = os.environ.get("B2P_SEGMENTED_CAPTURE", "1") != "0"
         self._graphs: dict = {}
+        self._opt_generation = getattr(self.optimizer, "generation", 0)
         self._shape_seen: dict = {}
         self._epoch_counter = None
         self.graph_steps = 0
@@ -180,7 +190,30 @@ class Trainer:
             g["graph"].release()
         self._graphs.clear()
 
+    def step_precision(self) -> str | None:
+        """The precision mode this Trainer's steps run in under the policy (None: the ambient mode)."""
+        if self.precision_policy == "auto" and self.encoder_trained and Fn.bf16_mode():
+            return "bf16x3"
+        return None
+
     def train_step(self, batch: SampleBatch):
+        gen = getattr(self.optimizer, "generation", 0)
+        if gen != self._opt_generation:
+            # the optimizer gained a param group (HipAdam.add_param_group): steps captured before hold
+            # update records for the old groups only, so they are dropped and captured again
+            self.release_graphs()
+            self._opt_generation = gen
+            opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
+            Fn.set_deferred_wgrad([p for p in self.model.parameters() if p.requires_grad and id(p) not in opt_ids])
+            enc = getattr(self.model, "w2v_encoder", None)
+            self.encoder_trained = enc is not None and any(id(p) in opt_ids for p in enc.parameters())
+        mode = self.step_precision()
+        if mode is None:
+            return self._train_step(batch)
+        with Fn.precision(mode):
+            return self._train_step(batch)
+
+    def _train_step(self, batch: SampleBatch):
         """One training step. The first `capture_after` steps of a batch shape run eagerly; then the
         whole step is captured once as a HIP graph and replayed for every later batch of that shape
         (at most graph_cache_size shapes; other shapes keep running eagerly). Replayed and eager steps
