@@ -158,6 +158,17 @@ int b2p_colsum_batched(const float* X, const float* Y, int64_t batch, int64_t M,
  * launch is handed a reserved counter (when nothing free fits, it takes the two-launch form).
  * b2p_colsum_pool_state: the allocation cursor (set_cursor >= 0 moves it: tests) and the reserved
  * counter count. Replaces nothing in the reference (bookkeeping of the fused bias-gradient sums). */
+/* Per-member LayerDrop gates of a batched GEMM launch (nz1 members; the frozen weight gradients of several
+ * layers in one launch): dev_gate_ptrs = device int64[nz1] of device int32* flags (0 = open), NULL to
+ * clear; while set, b2p_gemm gates member z1 by its own flag instead of b2p_set_gate's. */
+int b2p_set_gate_batch(const int64_t* dev_gate_ptrs);
+/* dst[0 .. n) = vals[0 .. n), n <= 64, by a kernel launch carrying the values (graph-capturable): the
+ * pointer / offset tables of batched launches. */
+int b2p_i64_fill(int64_t* dst, const int64_t* vals, int n, b2p_stream_t stream);
+/* Kernel family of the 256 x 256 GEMM launches (a tuning knob, tools/gemm_ab.py A/B): 0 = the 2-buffer
+ * 64-deep ping-pong kernel, 1 = the 4-stage 32-deep ring; v < 0 only reads. Returns the previous value.
+ * Default from B2P_GEMM16_P4. */
+int b2p_gemm16_variant(int v);
 int b2p_colsum_pin_begin(void);
 int64_t b2p_colsum_pin_end(void);
 int b2p_colsum_unpin(int64_t id);

@@ -30,6 +30,10 @@ def main():
     shapes = [("nt", NT, D, D), ("nt", NT, F, D), ("nt", NT, D, F), ("nt", NT, 3 * D, D),
               ("nn", NT, D, F), ("nn", NT, F, D), ("tn", D, F, NT), ("tn", F, D, NT), ("tn", D, D, NT),
               ("nt", 4096, 4096, 4096), ("nt", 8192, 8192, 8192)]
+    # the Conformer-large step's shapes (D 1024, F 4096)
+    Dc, Fc = 1024, 4096
+    shapes += [("nt", NT, Fc, Dc), ("nt", NT, Dc, Fc), ("nt", NT, 3 * Dc, Dc), ("nt", NT, Dc, Dc), ("nn", NT, Dc, Fc),
+               ("nn", NT, Fc, Dc), ("tn", Dc, Fc, NT), ("tn", Fc, Dc, NT), ("tn", Dc, Dc, NT)]
     if os.environ.get("GVB_SWEEP"):
         shapes = [("nt", 8192, 2048, k) for k in (256, 512, 1024, 2048, 4096, 8192)] + \
                  [("nt", 4096, 4096, k) for k in (768, 4096)] + [("nt", 7968, 3072, 768)]

@@ -59,6 +59,8 @@ const uint64_t* b2p_seed_epoch();
 // LayerDrop gate set by b2p_set_gate (lib.cpp): GEMMs under a closed gate skip their K loop (acc = 0,
 // epilogue still runs, so every output stays finite), fused attention skips its work
 const int32_t* b2p_gate();
+// per-member gates of a batched launch (b2p_set_gate_batch): device int64[nz1] of int32* (0 = open)
+const int64_t* b2p_gate_batch();
 __device__ __forceinline__ bool b2p_gated_off(const int32_t* gate) { return gate && *gate == 0; }
 void b2p_set_error(const char* fmt, ...);
 

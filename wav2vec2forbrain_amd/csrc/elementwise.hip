@@ -299,6 +299,28 @@ int64_t colsum_ctr_range(int64_t n) {
 
 }  // namespace
 
+namespace {
+struct I64Vals {
+  int64_t v[64];
+};
+__global__ void i64_fill_k(int64_t* __restrict__ dst, I64Vals vals, int n) {
+  const int i = threadIdx.x;
+  if (i < n) dst[i] = vals.v[i];
+}
+}  // namespace
+
+// dst[0 .. n) = vals (n <= 64) by a kernel whose arguments carry the values: stream-ordered and
+// capturable into a graph (no host-to-device copy); small index / pointer tables of batched launches
+extern "C" int b2p_i64_fill(int64_t* dst, const int64_t* vals, int n, b2p_stream_t stream) {
+  B2P_CHECK_ARG(dst && vals && n >= 0 && n <= 64, "i64_fill: n must be 0 .. 64 with non-NULL pointers");
+  if (n == 0) return 0;
+  I64Vals v;
+  for (int i = 0; i < n; ++i) v.v[i] = vals[i];
+  hipLaunchKernelGGL(i64_fill_k, dim3(1), dim3(64), 0, (hipStream_t)stream, dst, v, n);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int b2p_colsum_pin_begin(void) {
   CtrPool& p = ctr_pool();
   std::lock_guard<std::mutex> g(p.mu);

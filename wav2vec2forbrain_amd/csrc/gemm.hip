@@ -479,6 +479,7 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   if (check_operand(d.A, "A") || check_operand(d.B, "B")) return 1;
   B2P_CHECK_ARG(d.A.dtype == d.B.dtype, "gemm: operands must share a dtype");
   const bool bf16_ops = d.A.dtype != 0;   // 16-bit operands: the LDS-DMA kernel (gemm16.hip)
+  B2P_CHECK_ARG(!b2p_gate_batch() || bf16_ops, "gemm: per-member gates (b2p_set_gate_batch) need 16-bit operands");
   if (bf16_ops) {
     B2P_CHECK_ARG(d.precision == (d.A.dtype == 1 ? 0 : 2), "gemm: bf16 operands need precision 0, fp16 precision 2");
     B2P_CHECK_ARG(!(d.A.inner_is_k || d.B.inner_is_k) || d.K % 8 == 0,

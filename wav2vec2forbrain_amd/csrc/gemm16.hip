@@ -68,6 +68,17 @@ bool gemm16_splitk_fused(const b2p_gemm_desc& d) {
   return v4 && d.workspace_floats >= need;
 }
 
+static int g_gemm16_variant = -1;
+int b2p_gemm16_variant_get() {
+  if (g_gemm16_variant < 0) g_gemm16_variant = getenv("B2P_GEMM16_P4") ? atoi(getenv("B2P_GEMM16_P4")) : 0;
+  return g_gemm16_variant;
+}
+extern "C" int b2p_gemm16_variant(int v) {
+  const int old = b2p_gemm16_variant_get();
+  if (v >= 0) g_gemm16_variant = v;
+  return old;
+}
+
 static int run(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t ek, unsigned nwg, int tm, int tn, int grp) {
   const bool AK = d.A.inner_is_k != 0, BK = d.B.inner_is_k != 0;
   uint32_t* ctr = nullptr;
@@ -94,6 +105,10 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   const int64_t nz = (int64_t)d.nz1 * d.nz2 * ks;
   const bool h16 = d.A.dtype == 2;
   const uint32_t ek = epi_kind(d, ea);
+  if (ea.gates && !(ek == K_F || ek == K_FB || ek == K_SLAB)) {
+    b2p_set_error("gemm16: per-member gates need a plain (C or beta) epilogue");
+    return 1;
+  }
   if (h16 && d.A.conv) {
     b2p_set_error("gemm16: fp16 operands support plain (non-conv) views only");
     return 1;

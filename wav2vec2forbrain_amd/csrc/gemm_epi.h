@@ -30,6 +30,7 @@ struct EpiArgs {
   int32_t vec4;   // every C-shaped tensor allows 16-B (C16: 8-B) accesses at n % 4 == 0
   const uint64_t* epoch;   // graph-replay dropout seed offset (b2p_seed_eff)
   const int32_t* gate;     // LayerDrop gate (b2p_gate): closed -> no K loop
+  const int64_t* gates;    // per batch member z1: the member's gate pointer (b2p_gate_batch; 0 = open), or NULL
   uint32_t rk;             // gemm16 epilogue kind bits of this launch (EK_RUNTIME instantiations)
   uint32_t* tile_ctr;      // gemm16 split-K: per-tile arrival counters (zeroed per launch) -> the last
                            // K-slice workgroup of a tile sums the slabs itself (no reduce launch)
@@ -197,6 +198,7 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
   ea.vec4 = v ? 1 : 0;
   ea.epoch = b2p_seed_epoch();
   ea.gate = b2p_gate();
+  ea.gates = b2p_gate_batch();
   ea.rk = 0;
   ea.tile_ctr = nullptr;
   return ea;

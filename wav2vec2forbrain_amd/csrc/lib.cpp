@@ -33,6 +33,12 @@ extern "C" int b2p_set_gate(const int32_t* dev_flag) {
   g_gate = dev_flag;
   return 0;
 }
+static const int64_t* g_gate_batch = nullptr;
+const int64_t* b2p_gate_batch() { return g_gate_batch; }
+extern "C" int b2p_set_gate_batch(const int64_t* dev_gate_ptrs) {
+  g_gate_batch = dev_gate_ptrs;
+  return 0;
+}
 extern "C" int b2p_version(void) { return 1; }
 extern "C" int b2p_abi_sizes(int64_t* out3) {
   if (!out3) {

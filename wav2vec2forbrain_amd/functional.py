@@ -356,7 +356,7 @@ def _defer_wgemm_rows(ps, fn, *tensors) -> None:
                     r += n
         finally:
             _state.prec = old
-    _Deferred.queue.append((_gate_wrap(run), tensors, id(ps[0])))
+    _Deferred.queue.append((_gate_wrap(run), tensors, id(ps[0]), None))
 
 
 def _defer_wgemm(p, fn, *tensors) -> None:
@@ -374,7 +374,124 @@ def _defer_wgemm(p, fn, *tensors) -> None:
                 fn(p.grad, 1.0)
         finally:
             _state.prec = old
-    _Deferred.queue.append((_gate_wrap(run), tensors, id(p)))
+    _Deferred.queue.append((_gate_wrap(run), tensors, id(p), None))
+
+
+class _WSpec:
+    """A deferred frozen weight gradient dW[M][N] = a[:, a_off:a_off+M]^T b (K = tokens, both 16-bit
+    operands m/n-contiguous): ps are the parameters whose .grad are consecutive row blocks of dW."""
+    __slots__ = ("ps", "M", "N", "K", "a", "a_off", "lda", "b", "ldb", "gate", "prec")
+
+    def __init__(self, ps, M, N, K, a, a_off, lda, b, ldb):
+        self.ps, self.M, self.N, self.K = tuple(ps), M, N, K
+        self.a, self.a_off, self.lda, self.b, self.ldb = a, a_off, lda, b, ldb
+        self.gate, self.prec = _state.gate, _prec()
+
+    def key(self):
+        return (self.M, self.N, self.K, self.lda, self.ldb, self.a.dtype, self.b.dtype, self.prec,
+                tuple(tuple(p.shape) for p in self.ps))
+
+
+# B2P_WGRAD_BATCH=0: every deferred frozen weight gradient is its own (split-K) launch
+_WGRAD_BATCH = [os.environ.get("B2P_WGRAD_BATCH", "1") != "0"]
+
+
+def _defer_wspec(ps, M, N, K, a, a_off, lda, b, ldb) -> None:
+    """Queue a frozen weight gradient as a spec: flush_wgrad batches the same-shape gradients of all
+    layers into one launch (nz1 = layers, the operands gathered per layer, the gradients as views of one
+    buffer, a LayerDrop gate per layer); a lone spec runs as the single launch below."""
+    spec = _WSpec(ps, M, N, K, a, a_off, lda, b, ldb)
+    fn = lambda o, bt: gemm(M, N, K, op(a, a_off, lda, False), op(b, 0, ldb, False), o, N, beta=bt)
+    if len(ps) == 1:
+        _defer_wgemm(ps[0], fn, a, b)
+    else:
+        _defer_wgemm_rows(ps, fn, a, b)
+    fn_, ts, key, _ = _Deferred.queue[-1]
+    _Deferred.queue[-1] = (fn_, ts, key, spec)
+
+
+def _i64_dev(vals, dev):
+    """A device int64 tensor holding vals, written by a kernel launch (graph-capturable)."""
+    t = torch.empty(len(vals), dtype=torch.int64, device=dev)
+    arr = (ctypes.c_int64 * len(vals))(*vals)
+    _lib.call("b2p_i64_fill", _p(t), arr, len(vals), _st())
+    return t
+
+
+def _gathered_op(ts, offs, ld, dtype):
+    """One m/n-contiguous 16-bit Operand over several tensors: base = the lowest address, member z1 at
+    gather1[z1] * 8 elements (every address 16-byte aligned)."""
+    addrs = [t.data_ptr() + 2 * o for t, o in zip(ts, offs)]
+    base = min(addrs)
+    if any((x - base) % 16 for x in addrs):
+        return None, None
+    idx = _i64_dev([(x - base) // 16 for x in addrs], ts[0].device)
+    o = Operand()
+    o.ptr = base
+    o.ld = ld
+    o.bs1, o.bs2 = 8, 0
+    o.gather1 = idx.data_ptr()
+    o.inner_is_k = 0
+    o.conv = 0
+    o.dtype = 1 if dtype == BF16 else 2
+    return o, idx
+
+
+def _run_wspecs(specs) -> bool:
+    """One batched launch for same-shape weight-gradient specs (on the current side stream); False when
+    their .grad state does not allow it (mixed None / set, or set gradients that are not equally spaced
+    views of one buffer in member order): the caller then runs them one by one."""
+    s0 = specs[0]
+    M, N, K, n = s0.M, s0.N, s0.K, len(specs)
+    if n > 64:
+        return False
+    dev = s0.a.device
+    grads = [p.grad for sp in specs for p in sp.ps]
+    if all(g is None for g in grads):
+        buf = torch.empty(n, M, N, device=dev)
+        for i, sp in enumerate(specs):
+            r = 0
+            for p in sp.ps:
+                rows = p.shape[0]
+                p.grad = buf[i, r:r + rows].view(p.shape)
+                r += rows
+        C, beta = buf, 0.0
+    elif all(g is not None for g in grads):
+        C, beta = specs[0].ps[0].grad, 1.0
+        base = C.data_ptr()
+        for i, sp in enumerate(specs):
+            r = 0
+            for p in sp.ps:
+                g = p.grad
+                if (g.dtype != torch.float32 or not g.is_contiguous()
+                        or g.data_ptr() != base + 4 * (i * M * N + r * N)):
+                    return False
+                r += p.shape[0]
+    else:
+        return False
+    A, ia = _gathered_op([sp.a for sp in specs], [sp.a_off for sp in specs], s0.lda, s0.a.dtype)
+    B, ib = _gathered_op([sp.b for sp in specs], [0] * n, s0.ldb, s0.b.dtype)
+    if A is None or B is None:
+        return False
+    gates = [sp.gate for sp in specs]
+    gp = _i64_dev([0 if g is None else g.data_ptr() for g in gates], dev) if any(g is not None for g in gates) else None
+    old_prec, old_split = _state.prec, _state.nosplit
+    _state.prec = s0.prec
+    # the members' tiles fill the chip: no K split (no fp32 slabs, no reduce pass)
+    _state.nosplit = old_split or -(-M // 128) * -(-N // 128) * n >= 256
+    try:
+        with _gated(None):
+            if gp is not None:
+                _lib.call("b2p_set_gate_batch", gp.data_ptr())
+            try:
+                gemm(M, N, K, A, B, C, N, cbs1=M * N, nz1=n, beta=beta)
+            finally:
+                if gp is not None:
+                    _lib.call("b2p_set_gate_batch", None)
+    finally:
+        _state.prec, _state.nosplit = old_prec, old_split
+    del ia, ib, gp
+    return True
 
 
 def flush_wgrad(after=None) -> None:
@@ -398,13 +515,35 @@ def flush_wgrad(after=None) -> None:
     old = _state.nosplit
     _state.nosplit = not _Deferred.split
     try:
-        for fn, ts, key in _Deferred.queue:
-            k = _Deferred.lane.setdefault(key, len(_Deferred.lane) % len(sides))
-            sd = sides[k]
+        # same-shape frozen weight gradients of the layers: one batched launch per shape (one side
+        # stream keeps every parameter's work on one stream, as the lanes below do)
+        batch = _WGRAD_BATCH[0] and len(sides) == 1
+        groups, order = {}, []
+        for ent in _Deferred.queue:
+            spec = ent[3]
+            if batch and spec is not None:
+                k = spec.key()
+                if k not in groups:
+                    groups[k] = []
+                    order.append(("g", k))
+                groups[k].append(ent)
+            else:
+                order.append(("s", ent))
+        for kind, x in order:
+            ents = groups[x] if kind == "g" else [x]
+            sd = sides[_Deferred.lane.setdefault(ents[0][2], len(_Deferred.lane) % len(sides))]
             with torch.cuda.stream(sd):
-                fn()
-            for t in ts:
-                t.record_stream(sd)
+                nch = -(-len(ents) // 64)   # at most 64 members per launch, in equal chunks
+                step = -(-len(ents) // nch)
+                for c in range(0, len(ents), step):
+                    part = ents[c:c + step]
+                    if not (len(part) > 1 and _run_wspecs([e[3] for e in part])):
+                        for fn, _, key, _ in part:
+                            with torch.cuda.stream(sides[_Deferred.lane.setdefault(key, len(_Deferred.lane) % len(sides))]):
+                                fn()
+            for _, ts, key, _ in ents:
+                for t in ts:
+                    t.record_stream(sd if kind == "g" else sides[_Deferred.lane[key]])
         if _Deferred.accs:
             _flush_accs(sides[0])
     finally:
@@ -2051,8 +2190,7 @@ class _EncoderLayer16(torch.autograd.Function):
         dw2 = None
         if ng[14]:
             if _defer_ok(w2):
-                _defer_wgemm(prm[12], lambda o, bt, a=dz2_16, b=f16: gemm(D, F, NT, op(a, 0, D, False), op(b, 0, F, False),
-                                                                        o, F, beta=bt), dz2_16, f16)
+                _defer_wspec((prm[12],), D, F, NT, dz2_16, 0, D, f16, F)
             else:
                 dw2 = torch.empty_like(w2)
                 gemm(D, F, NT, op(dz2_16, 0, D, False), op(f16, 0, F, False), dw2, F)
@@ -2065,9 +2203,7 @@ class _EncoderLayer16(torch.autograd.Function):
         dw1 = None
         if ng[12]:
             if _defer_ok(w1):
-                _defer_wgemm(prm[10], lambda o, bt, a=dpre16, b=x1_16: gemm(F, D, NT, op(a, 0, F, False),
-                                                                          op(b, 0, D, False), o, D, beta=bt),
-                             dpre16, x1_16)
+                _defer_wspec((prm[10],), F, D, NT, dpre16, 0, F, x1_16, D)
             else:
                 dw1 = torch.empty_like(w1)
                 gemm(F, D, NT, op(dpre16, 0, F, False), op(x1_16, 0, D, False), dw1, D)
@@ -2084,8 +2220,7 @@ class _EncoderLayer16(torch.autograd.Function):
         dwo = None
         if ng[8]:
             if _defer_ok(wo):
-                _defer_wgemm(prm[6], lambda o, bt, a=dz1_16, b=O16: gemm(D, D, NT, op(a, 0, D, False), op(b, 0, D, False),
-                                                                       o, D, beta=bt), dz1_16, O16)
+                _defer_wspec((prm[6],), D, D, NT, dz1_16, 0, D, O16, D)
             else:
                 dwo = torch.empty_like(wo)
                 gemm(D, D, NT, op(dz1_16, 0, D, False), op(O16, 0, D, False), dwo, D)
@@ -2101,10 +2236,7 @@ class _EncoderLayer16(torch.autograd.Function):
             del dO
         grads_w = [None] * 6
         if all(_defer_ok(w) for w in (wq, wk, wv)) and ng[2] and ng[4] and ng[6]:
-            _defer_wgemm_rows((prm[0], prm[2], prm[4]),
-                              lambda o, bt, a=dqkv16, b=x16: gemm(3 * D, D, NT, op(a, 0, 3 * D, False),
-                                                                  op(b, 0, D, False), o, D, beta=bt),
-                              dqkv16, x16)
+            _defer_wspec((prm[0], prm[2], prm[4]), 3 * D, D, NT, dqkv16, 0, 3 * D, x16, D)
         elif ng[2] or ng[4] or ng[6]:
             dwqkv = torch.empty(3 * D, D, device=dev)
             gemm(3 * D, D, NT, op(dqkv16, 0, 3 * D, False), op(x16, 0, D, False), dwqkv, D)
@@ -2479,8 +2611,7 @@ def _wgrad16(w, need, dy16, M, x16, N, NT, ldy=None, ldx=None, dy_off=0):
         return None
     ldy, ldx = ldy or M, ldx or N
     if _defer_ok(w):
-        _defer_wgemm(w, lambda o, bt, a=dy16, b=x16: gemm(M, N, NT, op(a, dy_off, ldy, False), op(b, 0, ldx, False),
-                                                          o, N, beta=bt), dy16, x16)
+        _defer_wspec((w,), M, N, NT, dy16, dy_off, ldy, x16, ldx)
         return None
     gw = torch.empty_like(w)
     gemm(M, N, NT, op(dy16, dy_off, ldy, False), op(x16, 0, ldx, False), gw, N)
