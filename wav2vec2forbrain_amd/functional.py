@@ -215,6 +215,7 @@ def set_deferred_wgrad(params) -> None:
     _CAST_CACHE.clear()
     _FROZEN_PTR.clear()
     _FROZEN_PTR.update({p.data_ptr(): p for p in params if p is not None and p.is_cuda})
+    _HOMES.clear()
 
 
 def deferred_wgrad_active() -> bool:
@@ -437,60 +438,145 @@ def _gathered_op(ts, offs, ld, dtype):
     return o, idx
 
 
+_WGRAD_DEBUG = os.environ.get("B2P_WGRAD_DEBUG") == "1"
+
+
+def _wdbg(msg, specs):
+    if _WGRAD_DEBUG:
+        s0 = specs[0]
+        print(f"wgrad batch {s0.M}x{s0.N}x{s0.K} x{len(specs)}: {msg}", flush=True)
+
+
+class _Home:
+    """The gradients of every frozen parameter (tuple) of one weight-gradient shape as slots of one
+    zero-initialised buffer [slots][M][N], sized once for all the frozen parameters of that shape (it is
+    never reallocated, so a captured step can rely on it): p.grad is a view of its slot, and any subset
+    of the layers (LayerDrop skips some in eager steps) is one batched launch over the slots, the
+    absent members under a closed gate."""
+
+    def __init__(self, M, N, cap, dev):
+        self.M, self.N = M, N
+        self.buf = torch.zeros(cap, M, N, device=dev)
+        self.slot = {}        # tuple of parameter ids -> slot
+        self.members = []     # slot -> tuple of parameters
+        self.dirty = []       # slot -> its memory may hold a value (it was bound once)
+
+    def ensure(self, ps):
+        k = tuple(id(p) for p in ps)
+        i = self.slot.get(k)
+        if i is None:
+            if len(self.members) >= self.buf.shape[0]:
+                return None
+            i = self.slot[k] = len(self.members)
+            self.members.append(tuple(ps))
+            self.dirty.append(False)
+        return i
+
+    def view(self, i, p, r):
+        return self.buf[i, r:r + p.shape[0]].view(p.shape)
+
+    def bindable(self, i, ps) -> bool:
+        """Binding slot i needs no zero / copy pass (what a captured step may not contain)."""
+        r = 0
+        for p in ps:
+            g = p.grad
+            if g is None and self.dirty[i]:
+                return False
+            if g is not None and g.data_ptr() != self.view(i, p, r).data_ptr():
+                return False
+            r += p.shape[0]
+        return True
+
+    def bind(self, i, ps) -> None:
+        """p.grad of every parameter of slot i becomes its slot view: a None gradient starts from a zeroed
+        slot, a gradient held elsewhere is moved in."""
+        r = 0
+        for p in ps:
+            v = self.view(i, p, r)
+            g = p.grad
+            if g is None:
+                if self.dirty[i]:
+                    v.zero_()
+                p.grad = v
+            elif g.data_ptr() != v.data_ptr() or g.stride() != v.stride():
+                v.copy_(g)
+                p.grad = v
+            r += p.shape[0]
+        self.dirty[i] = True
+
+
+_HOMES: dict = {}
+_ZERO_GATE: dict = {}   # device -> int32 0 (a closed LayerDrop gate for absent batch members)
+
+
+def _zero_gate(dev):
+    z = _ZERO_GATE.get(str(dev))
+    if z is None:
+        z = _ZERO_GATE[str(dev)] = torch.zeros(1, dtype=torch.int32, device=dev)
+    return z
+
+
 def _run_wspecs(specs) -> bool:
-    """One batched launch for same-shape weight-gradient specs (on the current side stream); False when
-    their .grad state does not allow it (mixed None / set, or set gradients that are not equally spaced
-    views of one buffer in member order): the caller then runs them one by one."""
+    """Batched launches for same-shape frozen weight-gradient specs (on the current side stream), over
+    the slots of their _Home: the members present accumulate (beta 1) into their slot views, the slots
+    of absent layers run under a closed gate (their K loop skipped, += 0). False when the operands do
+    not allow a gathered view (the caller then runs the specs one by one)."""
     s0 = specs[0]
-    M, N, K, n = s0.M, s0.N, s0.K, len(specs)
-    if n > 64:
-        return False
+    M, N, K = s0.M, s0.N, s0.K
     dev = s0.a.device
-    grads = [p.grad for sp in specs for p in sp.ps]
-    if all(g is None for g in grads):
-        buf = torch.empty(n, M, N, device=dev)
-        for i, sp in enumerate(specs):
-            r = 0
-            for p in sp.ps:
-                rows = p.shape[0]
-                p.grad = buf[i, r:r + rows].view(p.shape)
-                r += rows
-        C, beta = buf, 0.0
-    elif all(g is not None for g in grads):
-        C, beta = specs[0].ps[0].grad, 1.0
-        base = C.data_ptr()
-        for i, sp in enumerate(specs):
-            r = 0
-            for p in sp.ps:
-                g = p.grad
-                if (g.dtype != torch.float32 or not g.is_contiguous()
-                        or g.data_ptr() != base + 4 * (i * M * N + r * N)):
-                    return False
-                r += p.shape[0]
-    else:
-        return False
-    A, ia = _gathered_op([sp.a for sp in specs], [sp.a_off for sp in specs], s0.lda, s0.a.dtype)
-    B, ib = _gathered_op([sp.b for sp in specs], [0] * n, s0.ldb, s0.b.dtype)
-    if A is None or B is None:
-        return False
-    gates = [sp.gate for sp in specs]
-    gp = _i64_dev([0 if g is None else g.data_ptr() for g in gates], dev) if any(g is not None for g in gates) else None
+    key = s0.key()[:2] + s0.key()[3:]   # the group key without K (the tokens of this batch shape)
+    home = _HOMES.get(key)
+    cap = capturing()
+    if home is None:
+        if cap:   # a home is allocated (zeroed) outside captures only
+            _wdbg("no home before the capture", specs)
+            return False
+        shape0 = tuple(s0.ps[0].shape)
+        nfrozen = sum(1 for q in _FROZEN_PTR.values() if tuple(q.shape) == shape0)
+        home = _HOMES[key] = _Home(M, N, max(1, -(-nfrozen // len(s0.ps))), dev)
+    at = {}
+    for sp in specs:
+        i = home.ensure(sp.ps)
+        if i is None or (cap and not home.bindable(i, sp.ps)):
+            _wdbg("slot unavailable", specs)
+            return False
+        at[i] = sp
+    for i, sp in at.items():
+        home.bind(i, sp.ps)
+    nslot = len(home.members)
     old_prec, old_split = _state.prec, _state.nosplit
     _state.prec = s0.prec
-    # the members' tiles fill the chip: no K split (no fp32 slabs, no reduce pass)
-    _state.nosplit = old_split or -(-M // 128) * -(-N // 128) * n >= 256
     try:
-        with _gated(None):
-            if gp is not None:
-                _lib.call("b2p_set_gate_batch", gp.data_ptr())
-            try:
-                gemm(M, N, K, A, B, C, N, cbs1=M * N, nz1=n, beta=beta)
-            finally:
+        for c0 in range(0, nslot, 64):
+            c1 = min(nslot, c0 + 64)
+            n = c1 - c0
+            mem = [at.get(i) for i in range(c0, c1)]
+            if all(m is None for m in mem):
+                continue
+            fill = next(m for m in mem if m is not None)
+            A, ia = _gathered_op([(m or fill).a for m in mem], [(m or fill).a_off for m in mem], s0.lda, s0.a.dtype)
+            B, ib = _gathered_op([(m or fill).b for m in mem], [0] * n, s0.ldb, s0.b.dtype)
+            if A is None or B is None:
+                _wdbg("operands not 16-byte aligned", specs)
+                return False
+            zg = _zero_gate(dev)
+            gates = [zg if m is None else m.gate for m in mem]
+            gp = (_i64_dev([0 if g is None else g.data_ptr() for g in gates], dev)
+                  if any(g is not None for g in gates) else None)
+            # the members' tiles fill the chip: no K split (no fp32 slabs, no reduce pass)
+            _state.nosplit = old_split or -(-M // 128) * -(-N // 128) * n >= 256
+            with _gated(None):
                 if gp is not None:
-                    _lib.call("b2p_set_gate_batch", None)
+                    _lib.call("b2p_set_gate_batch", gp.data_ptr())
+                try:
+                    gemm(M, N, K, A, B, home.buf[c0], N, cbs1=M * N, nz1=n, beta=1.0)
+                finally:
+                    if gp is not None:
+                        _lib.call("b2p_set_gate_batch", None)
+            del ia, ib, gp
+            _wdbg(f"batched slots {c0}..{c1} ({sum(m is not None for m in mem)} present)", specs)
     finally:
         _state.prec, _state.nosplit = old_prec, old_split
-    del ia, ib, gp
     return True
 
 
@@ -533,14 +619,10 @@ def flush_wgrad(after=None) -> None:
             ents = groups[x] if kind == "g" else [x]
             sd = sides[_Deferred.lane.setdefault(ents[0][2], len(_Deferred.lane) % len(sides))]
             with torch.cuda.stream(sd):
-                nch = -(-len(ents) // 64)   # at most 64 members per launch, in equal chunks
-                step = -(-len(ents) // nch)
-                for c in range(0, len(ents), step):
-                    part = ents[c:c + step]
-                    if not (len(part) > 1 and _run_wspecs([e[3] for e in part])):
-                        for fn, _, key, _ in part:
-                            with torch.cuda.stream(sides[_Deferred.lane.setdefault(key, len(_Deferred.lane) % len(sides))]):
-                                fn()
+                if not (kind == "g" and _run_wspecs([e[3] for e in ents])):
+                    for fn, _, key, _ in ents:
+                        with torch.cuda.stream(sides[_Deferred.lane.setdefault(key, len(_Deferred.lane) % len(sides))]):
+                            fn()
             for _, ts, key, _ in ents:
                 for t in ts:
                     t.record_stream(sd if kind == "g" else sides[_Deferred.lane[key]])
