@@ -1,0 +1,75 @@
+"""Frozen weight gradients batched per shape (functional._run_wspecs): the reference accumulates the
+gradients of the frozen wav2vec2 weights into .grad every step (src/train/train_loop.py:44,66), and
+the build issues those GEMMs deferred, one batched launch per weight shape over the slots of a
+per-shape buffer (functional._Home). Trainer steps in train mode with LayerDrop 0.5 (eager steps
+skip layers, so a launch covers a changing subset of the slots; replays gate skipped layers on the
+device) must leave exactly the frozen gradients the one-launch-per-gradient path leaves."""
+import pytest
+import torch
+
+from tests.helpers import CFG, build_model, batch_dict
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(name, batched, steps=5, graphs=True, layerdrop=0.5):
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    from wav2vec2forbrain_amd.train.train_loop import Trainer
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+    cfg = CFG[name]
+    Fn._WGRAD_BATCH[0] = batched
+    Fn.SEEDS.reseed(77)
+    Fn.LD_SEEDS.reseed(78)
+    torch.manual_seed(5)
+    model = build_model(cfg, train_dropouts=True)
+    model.train()
+    enc = model.w2v_encoder
+    enc = enc.wav2vec2_conformer.encoder if hasattr(enc, "wav2vec2_conformer") else enc.wav2vec2.encoder
+    enc.config.layerdrop = layerdrop
+    b = batch_dict(cfg)
+    batch = make_b2t_batch(b["x"], b["target"], b["day_idxs"], b["input_lens"], b["target_lens"]).cuda()
+    try:
+        with Fn.precision("bf16"):
+            trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+            trainer.use_graphs = graphs
+            trainer.capture_after = 2
+            for _ in range(steps):
+                trainer.train_step(batch)
+        torch.cuda.synchronize()
+        counts = (trainer.eager_steps, trainer.graph_steps)
+        trainer.release_graphs()
+        grads = {n: (None if p.grad is None else p.grad.detach().clone())
+                 for n, p in model.named_parameters() if n.startswith("w2v_encoder.")}
+        shared = len({p.grad.untyped_storage().data_ptr() for n, p in model.named_parameters()
+                      if n.startswith("w2v_encoder.") and p.grad is not None and p.dim() >= 2})
+    finally:
+        Fn._WGRAD_BATCH[0] = True
+        Fn.set_deferred_wgrad([])
+    return grads, counts, shared
+
+
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_conf"])
+@pytest.mark.parametrize("mode", ["eager_layerdrop", "replays"])
+def test_batched_frozen_wgrads_equal_single_launches(name, mode):
+    """eager_layerdrop: 5 eager steps at LayerDrop 0.5 (each step's launch covers the layers that ran);
+    replays: 2 eager steps, then 3 replays of the captured step (LayerDrop 0, so both paths hold every
+    frozen gradient before the capture; a gradient first created inside a capture is only accumulated
+    across replays by the batched path, whose slots are zeroed outside the capture)."""
+    graphs = mode == "replays"
+    ld = 0.0 if graphs else 0.5
+    g1, c1, shared1 = _run(name, True, graphs=graphs, layerdrop=ld)
+    g0, c0, shared0 = _run(name, False, graphs=graphs, layerdrop=ld)
+    assert c1 == c0 == ((2, 3) if graphs else (5, 0)), (c1, c0)
+    # batched: the matrix gradients of one shape share a buffer (far fewer storages than matrices)
+    assert shared1 < shared0, (shared1, shared0)
+    worst = 0.0
+    for n, a in g0.items():
+        b = g1[n]
+        assert (a is None) == (b is None), n
+        if a is None:
+            continue
+        rel = float((a - b).double().norm() / (a.double().norm() + 1e-30))
+        worst = max(worst, rel)
+        assert rel <= 1e-5, (n, rel)
+    print(f"{name}: worst relative difference of the frozen gradients {worst:.2e}")

@@ -2568,6 +2568,7 @@ def _act_dropout_cast16(pre, act, p, seed):
 
 
 _FFN_F16B = [os.environ.get("B2P_FFN_F16B", "1") != "0"]
+_FFN_PRE16 = [os.environ.get("B2P_FFN_PRE16", "1") != "0"]
 
 
 @_gate_aware
@@ -2585,13 +2586,16 @@ class _FFNBlock(torch.autograd.Function):
         x2 = x.view(NT, D)
         bs = b2 * scale if b2 is not None else None
         y = torch.empty(NT, D, device=dev)
-        pre = torch.empty(NT, F, device=dev)
         if bf16_mode():
             # 16-bit operands written by their producers (LayerNorm, FFN1 epilogue): no cast passes;
             # fp16 under forward_f16, else bf16. Under forward_f16 the FFN1 epilogue also writes f's
             # bf16 copy, the backward's weight-gradient operand (kept instead of the fp16 one; it was
             # recomputed from pre, a 195 MB pass per FFN at Conformer-large bs=32)
             half = _state.fwd16
+            # the pre-activation is read only by the backward's act' (the GEMM epilogue's aux16 operand):
+            # stored in bf16 (B2P_FFN_PRE16=0: fp32), half the bytes written and read back
+            pre16 = _FFN_PRE16[0] and (not half or _FFN_F16B[0])
+            pre = torch.empty(NT, F, device=dev, dtype=BF16 if pre16 else torch.float32)
             if half:   # h kept only as the bf16 weight-gradient operand of the backward (no fp32 copy)
                 _, h16, mean, rstd, h = _ln_fwd_x16(x2, g, b, eps, half, want32=False, want_b16=True)
             else:
@@ -2600,8 +2604,8 @@ class _FFNBlock(torch.autograd.Function):
             f = torch.empty(NT, F, device=dev, dtype=torch.float16 if half else BF16)
             fb = torch.empty(NT, F, device=dev, dtype=BF16) if half and _FFN_F16B[0] else None
             w1b, w1op = _w_op16(w1, half)
-            gemm(NT, F, D, op(h16, 0, D, True), w1op, None, F, bias=b1, pre_out=pre, act=act, drop_p=p_act,
-                 seed=s_act, C16=f, c16_fp16=half, C16b=fb)
+            gemm(NT, F, D, op(h16, 0, D, True), w1op, None, F, bias=b1, pre_out=None if pre16 else pre,
+                 pre16=pre if pre16 else None, act=act, drop_p=p_act, seed=s_act, C16=f, c16_fp16=half, C16b=fb)
             del h16, w1b
             w2b, w2op = _w_op16(w2, half)
             gemm(NT, D, F, op(f, 0, F, True), w2op, y, D, alpha=scale, bias=bs, drop_p=p_hid, seed=s_hid,
@@ -2610,6 +2614,7 @@ class _FFNBlock(torch.autograd.Function):
             if fb is not None:
                 f = fb
         else:
+            pre = torch.empty(NT, F, device=dev)
             h, mean, rstd = _ln_fwd(x2, g, b, eps)
             f = torch.empty(NT, F, device=dev)
             gemm(NT, F, D, op(h, 0, D, True), op(w1, 0, D, True), f, F, bias=b1, pre_out=pre, act=act, drop_p=p_act,
@@ -2675,7 +2680,8 @@ class _FFNBlock(torch.autograd.Function):
         dpre16 = torch.empty(NT, F, device=dev, dtype=BF16)
         parts = colsum_parts_buf(NT, F, dev) if (ctx.has_b[0] and ng[4]) else None
         gemm(NT, F, D, op(dz16, 0, D, True), op(weight16t(w2), 0, D, True), None, F, drop_p=p_act, seed=s_act,
-             act_bwd=act, aux=pre, C16=dpre16, colsum_part=parts)
+             act_bwd=act, aux=None if pre.dtype == BF16 else pre, aux16=pre if pre.dtype == BF16 else None,
+             C16=dpre16, colsum_part=parts)
         if parts is not None:
             db1 = ColsumParts(parts)   # finished by _defer_small (side-stream launch or materialised)
         dw1 = _wgrad16(w1, ng[3], dpre16, F, h if h.dtype == BF16 else cast16(h), D, NT)
