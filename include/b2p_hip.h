@@ -158,6 +158,12 @@ int b2p_colsum_batched(const float* X, const float* Y, int64_t batch, int64_t M,
  * launch is handed a reserved counter (when nothing free fits, it takes the two-launch form).
  * b2p_colsum_pool_state: the allocation cursor (set_cursor >= 0 moves it: tests) and the reserved
  * counter count. Replaces nothing in the reference (bookkeeping of the fused bias-gradient sums). */
+/* bf16x3 mode: the split-bf16 image of an R x C fp32 operand (hi = bf16(x), lo = bf16(x - hi)) as three
+ * blocks, block b = lo when bit b of pattern is set (A: hi, lo, hi = 0b010; B: hi, hi, lo = 0b100), side
+ * by side per row (along_cols, ldy >= 3C) or stacked (ldy >= C): one bf16 GEMM over K' = 3K then sums
+ * hi*hi + lo*hi + hi*lo (replaces the reference's fp32 matmuls at ~16 significant bits per product). */
+int b2p_split3_bf16(const float* x, int64_t R, int64_t C, int64_t ldx, uint16_t* y, int64_t ldy, int pattern,
+                    int along_cols, b2p_stream_t stream);
 /* Per-member LayerDrop gates of a batched GEMM launch (nz1 members; the frozen weight gradients of several
  * layers in one launch): dev_gate_ptrs = device int64[nz1] of device int32* flags (0 = open), NULL to
  * clear; while set, b2p_gemm gates member z1 by its own flag instead of b2p_set_gate's. */

@@ -48,30 +48,43 @@ def test_nt_nn_tn(mode, M, N, K):
         _close(out3[:, :N], at[:, :M].t() @ b[:, :N], mode)
 
 
-def test_split_bf16_accuracy():
+@pytest.mark.parametrize("form", ["kernel", "image"])
+@pytest.mark.parametrize("layout", ["nt", "tn"])
+def test_split_bf16_accuracy(form, layout, monkeypatch):
     """precision 3 (split bf16, the bf16x3 mode): the relative error of a K = 4096 product against an fp64
     reference is within a few 2^-16 (the bf16 mode's is ~2^-9); K >= 2048 on 4 output tiles makes it a
-    split-K launch (slabs summed in slice order); operands span 1e-6 .. 1e2 (bf16 keeps fp32's range)."""
+    split-K launch (slabs summed in slice order); operands span 1e-6 .. 1e2 (bf16 keeps fp32's range).
+    form kernel: the fp32-operand kernel's three MFMAs per k-step (csrc/gemm.hip precision 3); image: the
+    split-bf16 operand images (b2p_split3_bf16) over K' = 3K on the bf16 LDS-DMA kernels."""
     Fn = _fn()
+    monkeypatch.setattr(Fn, "_AUTO16_MIN_FLOP", 0.0 if form == "image" else 1e30)
+    monkeypatch.setattr(Fn, "_X3_SPLIT", [form == "image"])
     torch.manual_seed(3)
     M, N, K = 256, 192, 4096
     a = torch.randn(M, K, device="cuda") * torch.logspace(-6, 2, K, device="cuda")[torch.randperm(K, device="cuda")]
     w = torch.randn(N, K, device="cuda")
     ref = a.double() @ w.double().t()
+    at, wt = a.t().contiguous(), w.t().contiguous()   # K x M, K x N: the weight-gradient layout
     errs = {}
     for mode in ("bf16", "bf16x3"):
         with Fn.precision(mode):
             out = torch.empty(M, N, device="cuda")
-            Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), out, N)
+            if layout == "nt":
+                Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), out, N)
+            else:
+                Fn.gemm(M, N, K, Fn.op(at, 0, M, False), Fn.op(wt, 0, N, False), out, N)
         errs[mode] = float((out.double() - ref).norm() / ref.norm())
     print(errs)
     assert errs["bf16x3"] <= 3e-5, errs
     assert errs["bf16x3"] * 50 <= errs["bf16"], errs
 
 
-@pytest.mark.parametrize("mode", ["fp32", "bf16", "bf16x3"])
-def test_epilogue(mode):
+@pytest.mark.parametrize("mode", ["fp32", "bf16", "bf16x3", "bf16x3-image"])
+def test_epilogue(mode, monkeypatch):
     Fn = _fn()
+    if mode == "bf16x3-image":   # the split-bf16 operand images on the bf16 kernels, every epilogue
+        mode = "bf16x3"
+        monkeypatch.setattr(Fn, "_AUTO16_MIN_FLOP", 0.0)
     torch.manual_seed(1)
     M, N, K = 200, 96, 64
     x = torch.randn(M, K, device="cuda")

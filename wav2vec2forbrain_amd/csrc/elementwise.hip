@@ -1051,6 +1051,60 @@ extern "C" int b2p_cast16_2d(const float* x, int64_t R, int64_t C, int64_t ldx, 
   return 0;
 }
 
+// Split-bf16 operand of the bf16x3 mode: x (R x C fp32, ld ldx) = hi + lo with hi = bf16(x), lo =
+// bf16(x - hi), written as three blocks (block b = lo when bit b of `pattern` is set, else hi), side by
+// side in every row (along_cols: y[r][b*C + c], the k-contiguous operands) or stacked (y[b*R + r][c]).
+// A GEMM over the 3x-deep K of an A image (hi, lo, hi) and a B image (hi, hi, lo) sums hi*hi + lo*hi +
+// hi*lo in one launch on the bf16 MFMA kernels, with its full epilogue.
+__global__ void __launch_bounds__(256) split3_bf16_k(const float* __restrict__ x, int64_t R, int64_t C, int64_t ldx,
+                                                     uint16_t* __restrict__ y, int64_t ldy, int pattern, int along_cols) {
+  const int64_t c4 = (C + 3) / 4;
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= R * c4) return;
+  const int64_t r = i / c4, c = (i - r * c4) * 4;
+  float v[4] = {0.f, 0.f, 0.f, 0.f};
+  const int nv = C - c < 4 ? (int)(C - c) : 4;
+  const float* xs = x + r * ldx + c;
+  if (nv == 4 && ((uintptr_t)xs & 15u) == 0) {
+    const float4 q = *reinterpret_cast<const float4*>(xs);
+    v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
+  } else {
+    for (int j = 0; j < nv; ++j) v[j] = xs[j];
+  }
+  uint16_t hb[4], lb[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const __bf16 h = (__bf16)v[j];
+    const __bf16 l = (__bf16)(v[j] - (float)h);
+    hb[j] = __builtin_bit_cast(uint16_t, h);
+    lb[j] = __builtin_bit_cast(uint16_t, l);
+  }
+  const uint2 hv = make_uint2((uint32_t)hb[0] | ((uint32_t)hb[1] << 16), (uint32_t)hb[2] | ((uint32_t)hb[3] << 16));
+  const uint2 lv = make_uint2((uint32_t)lb[0] | ((uint32_t)lb[1] << 16), (uint32_t)lb[2] | ((uint32_t)lb[3] << 16));
+#pragma unroll
+  for (int b = 0; b < 3; ++b) {
+    uint16_t* ys = along_cols ? y + r * ldy + b * C + c : y + (b * R + r) * ldy + c;
+    const bool lo = (pattern >> b) & 1;
+    if (nv == 4 && ((uintptr_t)ys & 7u) == 0) {
+      *reinterpret_cast<uint2*>(ys) = lo ? lv : hv;
+    } else {
+      for (int j = 0; j < nv; ++j) ys[j] = lo ? lb[j] : hb[j];
+    }
+  }
+}
+
+extern "C" int b2p_split3_bf16(const float* x, int64_t R, int64_t C, int64_t ldx, uint16_t* y, int64_t ldy, int pattern,
+                               int along_cols, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && y, "split3_bf16: NULL pointer");
+  B2P_CHECK_ARG(R >= 0 && C >= 0 && ldx >= C && ldy >= (along_cols ? 3 * C : C), "split3_bf16: bad shape / strides");
+  if (R == 0 || C == 0) return 0;
+  const int64_t n = R * ((C + 3) / 4);
+  hipLaunchKernelGGL(split3_bf16_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, R, C, ldx,
+                     y, ldy, pattern, along_cols);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 // y[c][r] = bf16(x[r][c]) for an R x C fp32 matrix written into columns col0 .. col0+R-1 of a
 // [C][ldy] bf16 matrix (several row blocks stacked side by side: the transposed [Wq; Wk; Wv]):
 // 64 x 64 tiles through LDS, reads and writes coalesced along the rows of x and y

@@ -803,8 +803,17 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
         keep16 = (_cast_operand(A, M, K, h, dev), _cast_operand(B, N, K, h, dev))
         A, B = keep16[0][1], keep16[1][1]
         d.A, d.B = A, B
+    d.flops = 2.0 * M * N * K * nz1 * nz2   # algorithmic (the bf16x3 image below triples the MFMA work)
+    if _X3_SPLIT[0] and _state.prec == 3 and A.dtype == 0 and B.dtype == 0 and _auto16_ok(M, N, K, A, B, nz1, nz2):
+        # bf16x3: split-bf16 images of both operands over K' = 3K, one launch on the bf16 LDS-DMA kernels
+        dev = (C if C is not None else C16).device
+        keep16 = (_split3_operand(A, M, K, 0b010, dev), _split3_operand(B, N, K, 0b100, dev))
+        A, B = keep16[0][1], keep16[1][1]
+        d.A, d.B = A, B
+        K = 3 * K
+        d.K = K
+        d.precision = 0
     d.timing_family = timing or _GEMM_TIMING[0]
-    d.flops = 2.0 * M * N * K * nz1 * nz2
     ws = None
     plain = (bias is None and pre_out is None and act == 0 and act_bwd == 0 and drop_p == 0.0 and residual is None
              and colsum_part is None and pre16 is None and C16b is None)
@@ -845,6 +854,30 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
                                                             + 4 * (residual is not None) + 4 * (beta != 0.0)
                                                             + (2 if aux16 is not None else 4 if aux is not None else 0))))
     _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
+
+
+# bf16x3 mode: large plain fp32-operand GEMMs run as one bf16 GEMM over split-bf16 operand images
+# (B2P_X3_SPLIT=0: the fp32-operand kernel's three-MFMA form, csrc/gemm.hip precision 3)
+_X3_SPLIT = [os.environ.get("B2P_X3_SPLIT", "1") != "0"]
+
+
+def _split3_operand(o, mn, K, pattern, dev):
+    """The split-bf16 image of the logical (mn x K) fp32 operand o: three K-blocks (hi / lo per pattern
+    bit), along the rows of a k-contiguous operand, stacked for an m/n-contiguous one; (buffer, Operand)."""
+    rows, cols = (mn, K) if o.inner_is_k else (K, mn)
+    along = bool(o.inner_is_k)
+    ld16 = -(-(3 * cols if along else cols) // 8) * 8
+    buf = torch.empty(rows if along else 3 * rows, ld16, device=dev, dtype=BF16)
+    _lib.call("b2p_split3_bf16", o.ptr, rows, cols, o.ld, buf.data_ptr(), ld16, pattern, int(along), _st())
+    n = Operand()
+    n.ptr = buf.data_ptr()
+    n.ld = ld16
+    n.bs1 = n.bs2 = 0
+    n.gather1 = None
+    n.inner_is_k = o.inner_is_k
+    n.conv = 0
+    n.dtype = 1
+    return buf, n
 
 
 # split-K fix-up inside the 16-bit GEMM (counters behind the slabs); False: the separate reduce launch
