@@ -271,3 +271,135 @@ def test_dp_replayed_syncbn_full_ft_steps_equal_global_batch_steps(tmp_path):
         for r in res:
             d = float((r["bufs"][n] - b).norm())
             assert d <= 1e-4 * float(b.norm()) + 1e-6, (n, d)
+
+
+def _nccl_world1_worker(port, out_dir, graphs, in_graph):
+    """One rank, backend nccl (RCCL), B2P_DP_FORCE=1: every data-parallel code path runs over RCCL."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), B2P_DP_FORCE="1",
+                      B2P_GRAPH_COLLECTIVES="1" if in_graph else "0")
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        cfg = _cfg("tiny_conf")
+        model = build_model(cfg)
+        model.train()
+        model.sync_metrics = False
+        b = _batch(cfg, (0, cfg["B"]))
+        from wav2vec2forbrain_amd.train import ddp
+        with_trainer = {}
+        losses, counts, info = _trainer_steps(model, [b] * 3, graphs=graphs, unfreeze="brain_encoder+w2v")
+        with_trainer.update(losses=losses, counts=counts, info=info, in_graph=ddp.collectives_in_graph(),
+                            params={n: p.detach().cpu() for n, p in _optimised(model, "brain_encoder+w2v")})
+        torch.save(with_trainer, os.path.join(out_dir, f"nccl_{int(graphs)}{int(in_graph)}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_world1_captured_collectives(tmp_path):
+    """BASELINE configs[3]/[4] run over RCCL on 8 GPUs, which this box cannot: a one-rank RCCL process
+    group with the data-parallel machinery forced on (B2P_DP_FORCE=1) runs the Conformer's SyncBN
+    statistics all-reduces, the gradient-bucket all-reduces and the used-flag MAX all-reduce through
+    RCCL. Three full-fine-tune Trainer steps, eager, replayed with the collectives captured INSIDE one
+    graph (the RCCL default, train.ddp.collectives_in_graph) and replayed with the segmented capture,
+    leave the same parameters as the single-process steps (one rank: the all-reduces are identities)."""
+    import torch.multiprocessing as mp
+    name, unfreeze = "tiny_conf", "brain_encoder+w2v"
+    cfg = _cfg(name)
+    ref = build_model(cfg)
+    ref.train()
+    ref_losses, _, _ = _trainer_steps(ref, [_batch(cfg, (0, cfg["B"]))] * 3, graphs=False, unfreeze=unfreeze)
+    params = {n: p.detach().cpu() for n, p in _optimised(ref, unfreeze)}
+    ctx = mp.get_context("spawn")
+    res = {}
+    for graphs, in_graph in ((False, True), (True, True), (True, False)):
+        p = ctx.Process(target=_nccl_world1_worker, args=(_free_port(), str(tmp_path), graphs, in_graph))
+        p.start()
+        p.join(timeout=240)
+        assert p.exitcode == 0, (graphs, in_graph, p.exitcode)
+        res[(graphs, in_graph)] = torch.load(tmp_path / f"nccl_{int(graphs)}{int(in_graph)}.pt", weights_only=True)
+    for key, r in res.items():
+        graphs, in_graph = key
+        assert tuple(r["counts"]) == ((1, 2) if graphs else (3, 0)), (key, r["counts"])
+        if graphs:
+            # one graph per step with the collectives inside; one segment per collective otherwise
+            assert (r["info"]["segments"][0] == 1) == in_graph, (key, r["info"]["segments"])
+            assert r["in_graph"] == in_graph
+        for k in range(3):
+            assert abs(r["losses"][k] - ref_losses[k]) <= 1e-5 * abs(ref_losses[k]), (key, k, r["losses"], ref_losses)
+        worst = max(float((r["params"][n] - q).norm()) / (float(q.norm()) + 1e-30) for n, q in params.items()
+                    if not n.endswith("linear_k.bias"))
+        print(key, "worst relative parameter difference vs single-process steps", worst)
+        assert worst <= 1e-5, (key, worst)
+
+
+def _ld_worker(rank, port, out_dir):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        from wav2vec2forbrain_amd import functional as Fn
+        from wav2vec2forbrain_amd.train.train_loop import Trainer
+        from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+        torch.manual_seed(1234)                        # the host LayerDrop draws of eager steps: equal on every rank
+        Fn.SEEDS.reseed(99 + rank)                     # dropout masks differ per rank
+        Fn.LD_SEEDS.reseed(4242)                       # device LayerDrop draws of replays: equal on every rank
+        cfg = _cfg("tiny_a")
+        model = build_model(cfg)
+        model.train()
+        model.sync_metrics = False
+        enc = model.w2v_encoder.wav2vec2.encoder
+        enc.config.layerdrop = 0.5
+        ran = []
+        for i, layer in enumerate(enc.layers):
+            layer.register_forward_hook(lambda m, a, o, i=i: ran.append(i))
+        per = cfg["B"] // WORLD
+        b = _batch(cfg, (rank * per, (rank + 1) * per))
+        record = []
+        with Fn.precision("fp32"):
+            trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+            trainer.capture_after = 2
+            for _ in range(6):
+                ran.clear()
+                g0 = trainer.graph_steps
+                trainer.train_step(b)
+                torch.cuda.synchronize()
+                if trainer.graph_steps > g0:   # a replay: this replay's device draw per layer
+                    record.append(("replay", [int(f.item()) for f in Fn._GATE_FLAGS[-len(enc.layers):]]))
+                else:
+                    record.append(("eager", sorted(ran)))
+        counts = (trainer.eager_steps, trainer.graph_steps)
+        trainer.release_graphs()
+        Fn.set_deferred_wgrad([])
+        torch.save({"record": record, "counts": counts,
+                    "params": {n: p.detach().cpu() for n, p in _trainable(model)}},
+                   os.path.join(out_dir, f"ld_rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_layerdrop_same_layers_on_every_rank(tmp_path):
+    """Data-parallel steps at LayerDrop 0.5 (two gloo ranks on the one GPU): the eager steps (the host
+    draw of the reference, torch.rand per layer from the rank-equal torch seed) and the replays (the
+    device draw from LD_SEEDS, rank-equal, functional.layerdrop_layer) skip the same layers on both
+    ranks, while the dropout masks differ per rank; the parameters stay identical across ranks."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_ld_worker, args=(r, port, str(tmp_path))) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [torch.load(tmp_path / f"ld_rank{r}.pt", weights_only=True) for r in range(WORLD)]
+    assert tuple(res[0]["counts"]) == (2, 4), res[0]["counts"]
+    assert res[0]["record"] == res[1]["record"], (res[0]["record"], res[1]["record"])
+    kinds = [k for k, _ in res[0]["record"]]
+    assert kinds == ["eager"] * 2 + ["replay"] * 4, kinds
+    nl = _cfg("tiny_a")["layers"]
+    skipped = sum(nl - len(v) for k, v in res[0]["record"] if k == "eager") + \
+        sum(v.count(0) for k, v in res[0]["record"] if k == "replay")
+    assert skipped > 0, res[0]["record"]   # the draws did skip layers (the test is not vacuous)
+    for n in res[0]["params"]:
+        assert torch.equal(res[0]["params"][n], res[1]["params"][n]), n

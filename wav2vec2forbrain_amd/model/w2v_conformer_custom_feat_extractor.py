@@ -189,8 +189,8 @@ class W2VConformerBrainEncoderModel(B2TModel):
         assert targets is not None
         targets = targets.masked_fill(targets < 1, -100)
         import torch.distributed as dist
-        sync = (self.training and self.sync_batchnorm and dist.is_available() and dist.is_initialized()
-                and dist.get_world_size(self.process_group) > 1)
+        from ..train.ddp import dp_active
+        sync = self.training and self.sync_batchnorm and dp_active(self.process_group)
         with Fn.forward_f16(self.forward_f16), Fn.sync_batchnorm(
                 (self.process_group or dist.group.WORLD) if sync else None):
             w2v_output = self.w2v_encoder.forward(encoded_brain.logits)

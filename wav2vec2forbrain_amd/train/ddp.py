@@ -29,6 +29,7 @@ from __future__ import annotations
 
 from typing import Iterable
 
+import os
 from collections import deque
 
 import torch
@@ -37,12 +38,29 @@ import torch.distributed as dist
 from .. import functional as Fn
 
 
+def dp_active(process_group=None) -> bool:
+    """The data-parallel machinery is on: torch.distributed initialised with more than one rank, or with
+    one rank under B2P_DP_FORCE=1 (tests: the RCCL path of every collective on a one-GPU box)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False
+    return dist.get_world_size(process_group) > 1 or os.environ.get("B2P_DP_FORCE") == "1"
+
+
+def collectives_in_graph(process_group=None) -> bool:
+    """Captured data-parallel steps keep their collectives INSIDE the graph (RCCL all-reduces captured
+    as graph nodes: one graph per step instead of one segment per collective). RCCL only (gloo
+    collectives are host code); B2P_GRAPH_COLLECTIVES=0 keeps the segmented capture for RCCL too."""
+    return (dp_active(process_group) and dist.get_backend(process_group) == "nccl"
+            and os.environ.get("B2P_GRAPH_COLLECTIVES", "1") != "0")
+
+
 class GradBucketReducer:
     def __init__(self, params: Iterable[torch.nn.Parameter], bucket_mb: float = 64.0, process_group=None,
                  average: bool = True, overlap: bool = True, grad_views: bool = True, track_used: bool = True):
         self.params = [p for p in params if p.requires_grad]
         self.pg = process_group
         self.world = dist.get_world_size(process_group) if dist.is_initialized() else 1
+        self.active = dp_active(process_group)
         self.average = average
         # RCCL averages inside the collective; gloo has no AVG: sum, then one scale
         self.avg_op = (average and dist.is_initialized()
@@ -97,7 +115,7 @@ class GradBucketReducer:
         self._layer_gates = None   # graph-replayed steps: the device LayerDrop flags (make_layer_gates)
         self._seen: set = set()
         self._reset()
-        if self.world > 1:
+        if self.active:
             for p in self.params:
                 p.register_post_accumulate_grad_hook(self._hook)
         if grad_views:
@@ -158,7 +176,7 @@ class GradBucketReducer:
         else:
             loc = torch.tensor([1 if id(p) in self._seen else 0 for p in self.params], dtype=torch.int32)
             self.used.copy_(loc)
-        if self.world > 1:
+        if self.active:
             dist.all_reduce(self.used, op=dist.ReduceOp.MAX, group=self.pg)
 
     def zero_grad(self) -> None:
@@ -210,7 +228,7 @@ class GradBucketReducer:
     def finish(self):
         """Call after loss.backward(): launches the remaining buckets (in order), waits, and leaves
         the averaged gradient in every p.grad (its bucket slice)."""
-        if self.world <= 1:
+        if not self.active:
             return
         while self.next_launch < len(self.buckets):
             self._launch(self.next_launch)

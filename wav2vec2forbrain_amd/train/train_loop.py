@@ -16,7 +16,7 @@ from .. import functional as Fn
 import torch.distributed as dist
 
 from ..datasets.batch_types import SampleBatch
-from .ddp import GradBucketReducer, unused_param_names
+from .ddp import GradBucketReducer, collectives_in_graph, dp_active, unused_param_names
 from .history import EpochLosses, SingleEpochHistory, TrainHistory
 
 
@@ -44,7 +44,7 @@ class Trainer:
         self.frozen_reducer = None
         opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
         frozen = [p for p in self.model.parameters() if p.requires_grad and id(p) not in opt_ids]
-        if dist.is_initialized() and dist.get_world_size() > 1:
+        if dp_active():
             skip = unused_param_names(self.model)
             params = [p for n, p in self.model.named_parameters() if id(p) in opt_ids and n not in skip]
             self.reducer = GradBucketReducer(params, bucket_mb=float(os.environ.get("B2P_DP_BUCKET_MB", "64")))
@@ -107,7 +107,7 @@ class Trainer:
     def _graphable(self, batch) -> bool:
         return (self.use_graphs and self.model.training and batch.input.is_cuda and batch.target is not None
                 and getattr(batch, "target_lens", None) is not None and not Fn.capturing()
-                and (self.segmented or not self._sync_bn()))
+                and (self.segmented or not self._sync_bn() or collectives_in_graph()))
 
     def _capture(self, batch):
         """Captures one whole step for this batch shape (train/step_graph.py) on static copies of the
@@ -133,7 +133,12 @@ class Trainer:
 
         if self._epoch_counter is None:
             self._epoch_counter = torch.zeros(1, dtype=torch.int64, device=batch.input.device)
-        seg = dp and self.segmented
+        # RCCL: the step's collectives (SyncBN statistics) are captured inside ONE graph; the gradient
+        # buckets are exchanged after each replay (finish()). gloo: segmented capture (a gloo
+        # collective is host code): the graph splits at every collective, which a replay issues
+        # between the segments
+        in_graph = dp and collectives_in_graph()
+        seg = dp and self.segmented and not in_graph
         if dp:
             # bucket all-reduces between the segments of the backward only when no frozen-weight
             # gradient work runs on the side streams (full fine-tuning): a split joins those streams,
