@@ -194,6 +194,11 @@ _PP_SPLIT = os.environ.get("B2P_PP_SPLIT", "0") == "1"   # every eligible split-
 # frozen weight gradients (4096 x 1024, 3072 x 1024; K = 7968 tokens) -8.6 ms per step; the base
 # model's (768 x 3072 and smaller) measured 0.2 ms slower on it, so they stay on the 128 x 128 split
 _PP_MIN_MN = int(os.environ.get("B2P_PP_MIN_MN", str(3 * 1024 * 1024)))
+# ... and only while the unsplit 128 x 128 grid has fewer tiles than this (a grid that fills the chip by
+# itself needs no fp32 slabs and no reduce pass): the Conformer's 7968 x 1024 backward-data GEMMs (504
+# tiles) 69.73 -> 68.54 ms per step unsplit; the base model's 7968 x 768 (378 tiles, 1.5 rounds of the
+# CUs) stay split (14.99 vs 15.13 ms unsplit), profiles/r05o_pp_split_rule_ab.txt
+_PP_SPLIT_MAX_BLOCKS = int(os.environ.get("B2P_PP_SPLIT_MAX_BLOCKS", "448"))
 
 
 class _Deferred:
@@ -824,7 +829,8 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
         ks = 1
         tpp = -(-M // 256) * -(-N // 256) * nz1 * nz2
         kpp = min(-(-160 // tpp), K // 1024)
-        if b16 and (_PP_SPLIT or M * N * nz1 * nz2 >= _PP_MIN_MN) and tpp * kpp >= 160 and kpp >= 2:
+        if (b16 and (_PP_SPLIT or M * N * nz1 * nz2 >= _PP_MIN_MN) and tpp * kpp >= 160 and kpp >= 2
+                and blocks < _PP_SPLIT_MAX_BLOCKS):
             # 256x256 ping-pong tiles (gemm16.hip) over >= 1024-deep K slices, ~160-200 workgroups
             # (the frozen weight gradients, K = tokens): fewer, larger tiles than the 128 x 128 split
             ks = kpp
