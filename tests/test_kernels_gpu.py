@@ -212,7 +212,8 @@ def _keep_mask_ref(seed, p, B, nh, T):
 
 
 @pytest.mark.parametrize("B,T,nh,p", [(2, 249, 12, 0.0), (2, 249, 12, 0.1), (3, 100, 4, 0.1), (1, 17, 2, 0.0),
-                                       (2, 256, 3, 0.1), (2, 313, 4, 0.1), (1, 257, 2, 0.0), (1, 512, 2, 0.1)])
+                                       (2, 256, 3, 0.1), (2, 313, 4, 0.1), (1, 257, 2, 0.0), (1, 512, 2, 0.1),
+                                       (1, 241, 2, 0.1), (1, 240, 2, 0.1)])
 @pytest.mark.parametrize("variant", ["hash", "mask", "epoch", "f16"])
 def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
     """csrc/attn16.hip (bf16 MFMA, scores on-chip) vs the unfused fp32 attention core (GEMM ->

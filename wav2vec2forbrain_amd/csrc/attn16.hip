@@ -19,6 +19,7 @@
 // (b2p_softmax_fwd), so both paths agree element for element.
 #include "common.h"
 #include <type_traits>
+#include <stdlib.h>
 #include "../../include/b2p_hip.h"
 
 namespace {
@@ -177,11 +178,17 @@ __device__ __forceinline__ uint32_t keep4_bits(uint32_t key_lo, uint32_t k32, ui
   const uint32_t h0 = b2p_mix32(b2p_mix32((key_lo >> 1) ^ k32) + k32);
   const uint32_t h1 = b2p_mix32(b2p_mix32(((key_lo >> 1) + 1) ^ k32) + k32);
 #endif
-  return ((h0 & 0xFFFFu) >= thr16 ? 1u : 0u) | ((h0 >> 16) >= thr16 ? 2u : 0u) |
-         ((h1 & 0xFFFFu) >= thr16 ? 4u : 0u) | ((h1 >> 16) >= thr16 ? 8u : 0u);
+  // (v - thr16) >> 31 = 1 exactly when v < thr16 (v, thr16 <= 2^16): the drop bits by arithmetic (compares
+  // would each tie up an SGPR pair across the unrolled loop)
+  const uint32_t d = (((h0 & 0xFFFFu) - thr16) >> 31) | ((((h0 >> 16) - thr16) >> 31) << 1) |
+                     ((((h1 & 0xFFFFu) - thr16) >> 31) << 2) | ((((h1 >> 16) - thr16) >> 31) << 3);
+  return d ^ 0xFu;
 }
 
-template <int DM, bool H, int TM>   // DM 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward
+// T1: T > TM - 16, so keys >= T lie in the last key tile only: its score accumulator starts from a bias
+// (0 for keys < T, -inf beyond) computed once, and no per-element masking runs in the loop (the masked
+// form's uniform per-tile branches made the unrolled loop spill ~230 SGPRs into VGPR lanes)
+template <int DM, bool H, int TM, bool T1 = false>   // DM 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward
 __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
                                                        uint16_t* __restrict__ Ob16, float* __restrict__ lse2, int T,
                                                        int nh, float scale, DropCfg dc, uint32_t* __restrict__ maskw) {
@@ -213,6 +220,11 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
   const float c2 = scale * LOG2E;
   const uint32_t k32 = (uint32_t)dc.seed ^ b2p_mix32((uint32_t)(dc.seed >> 32) + 0x9E3779B9u);   // b2p_hash key
   const uint32_t thr16 = b2p_thr16(dc.thr);
+  f32x4 tail0 = f32x4{0.f, 0.f, 0.f, 0.f};   // T1: the last key tile's initial scores (0 / -inf)
+  if constexpr (T1) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) tail0[i] = (NKT - 1) * 16 + 4 * g + i < T ? 0.f : -INFINITY;
+  }
   for (int qt = qt0; qt < qt0 + FWD_QB / 16 && qt * 16 < T; qt += 4) {
     // opaque per-iteration image bases: keeps the compiler from hoisting the ~100 per-lane LDS
     // fragment addresses of the unrolled body out of the loop (they would not fit beside s[16])
@@ -230,16 +242,17 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     f32x4 s[NKT];
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
-      s[kt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      s[kt] = (T1 && kt == NKT - 1) ? tail0 : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) s[kt] = mfma_t<H>(row_frag(Kimg, kt * 16 + lr, 32 * ks + 8 * g), qf[ks], s[kt]);
     }
     // row max of the raw scores (scale > 0 commutes with max); keys >= T are masked only in the tiles
-    // that hold them (wave-uniform test), the scale is folded into the exponent's FMA
+    // that hold them (wave-uniform test; T1: already -inf from the accumulator's start), the scale is
+    // folded into the exponent's FMA
     float m = -INFINITY;
 #pragma unroll
     for (int kt = 0; kt < NKT; ++kt) {
-      if (kt * 16 + 16 <= T) {
+      if (T1 || kt * 16 + 16 <= T) {
 #pragma unroll
         for (int i = 0; i < 4; ++i) m = fmaxf(m, s[kt][i]);
       } else {
@@ -284,7 +297,12 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
           const float pv = s[2 * c + half][i] * inv_s;
-          s[2 * c + half][i] = (DROP && !((kb >> i) & 1u)) ? 0.f : pv;
+          if constexpr (DROP) {   // keep bit i as an all-ones / zero mask: bit arithmetic, no compare masks
+            const uint32_t km = (uint32_t)((int32_t)(kb << (31 - i)) >> 31);
+            s[2 * c + half][i] = __uint_as_float(__float_as_uint(pv) & km);
+          } else {
+            s[2 * c + half][i] = pv;
+          }
         }
       }
       const bf16x8 bp = pack_acc_t<H>(s[2 * c], s[2 * c + 1]);
@@ -538,6 +556,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
       }
       continue;
     }
+    const uint32_t qm = 0u - (uint32_t)qok;
     uint2 mw = make_uint2(0u, 0u);   // this lane's keep bytes of the query row (keys kt*16 + 4g + i)
     if (DM == 2 && qok) mw = *reinterpret_cast<const uint2*>(maskw + (int64_t)rowc * 8 + 2 * g);
     f32x4 P[16], PD[16];
@@ -552,13 +571,20 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
       }
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        // validity and keep as all-ones / zero bit masks formed arithmetically: compare-and-select per
+        // element left 64 lane masks live in SGPR pairs across the unrolled tiles (238 SGPR spills)
         const int key = kt * 16 + 4 * g + i;
-        const bool ok = qok && key < T;
-        const float p = ok ? exp2_fast(fmaf(sv[i], c2, -ls)) : 0.f;
-        const float kp = (DM == 2) ? ((((kt < 8 ? mw.x : mw.y) >> (8 * ((kt >> 1) & 3) + 4 * (kt & 1) + i)) & 1u)
-                                          ? dc.scale : 0.f)
-                                         : keep_scale<DROP>(dc, rowidx + key);
-        const float pd = ok ? dp[i] * kp : 0.f;
+        const uint32_t km = qm & (uint32_t)((key - T) >> 31);
+        const float p = __uint_as_float(__float_as_uint(exp2_fast(fmaf(sv[i], c2, -ls))) & km);
+        float kp;
+        if constexpr (DM == 2) {
+          const uint32_t wd = kt < 8 ? mw.x : mw.y;
+          const int bit = 8 * ((kt >> 1) & 3) + 4 * (kt & 1) + i;
+          kp = __uint_as_float(__float_as_uint(dc.scale) & (uint32_t)((int32_t)(wd << (31 - bit)) >> 31));
+        } else {
+          kp = keep_scale<DROP>(dc, rowidx + key);
+        }
+        const float pd = __uint_as_float(__float_as_uint(dp[i] * kp) & km);
         P[kt][i] = p;
         PD[kt][i] = pd;
         dl += p * pd;
@@ -619,6 +645,9 @@ int init_attrs_t() {
   rc |= set_lds(attn16_bwd_dq_k<0, H, TM>, fwd_lds<TM>());
   rc |= set_lds(attn16_bwd_dq_k<1, H, TM>, fwd_lds<TM>());
   if constexpr (TM == TMAX) {
+    rc |= set_lds(attn16_fwd_k<0, H, TM, true>, fwd_lds<TM>());
+    rc |= set_lds(attn16_fwd_k<1, H, TM, true>, fwd_lds<TM>());
+    rc |= set_lds(attn16_fwd_k<2, H, TM, true>, fwd_lds<TM>());
     rc |= set_lds(attn16_fwd_k<2, H, TM>, fwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dkv_k<2, H, TM>, bwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dq_k<2, H, TM>, fwd_lds<TM>());
@@ -634,6 +663,10 @@ int init_attrs() {
 }  // namespace
 
 namespace {
+bool attn_t1() {   // B2P_ATTN_T1=0: the masked form for every T (A/B)
+  static const bool on = !(getenv("B2P_ATTN_T1") && getenv("B2P_ATTN_T1")[0] == '0');
+  return on;
+}
 int attn16_fwd_launch(bool half, const void* qkv16, void* O16, void* Ob16, float* lse2, int64_t B, int64_t T,
                       int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
                       b2p_stream_t stream) {
@@ -650,7 +683,11 @@ int attn16_fwd_launch(bool half, const void* qkv16, void* O16, void* Ob16, float
   auto run = [&](auto dmc, auto hc) {
     constexpr int DM = decltype(dmc)::value;
     constexpr bool HH = decltype(hc)::value;
-    if (T <= TMAX)
+    if (T <= TMAX && T > TMAX - 16 && attn_t1())
+      hipLaunchKernelGGL((attn16_fwd_k<DM, HH, TMAX, true>), grid, dim3(FWD_NT), fwd_lds<TMAX>(), (hipStream_t)stream,
+                         (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T, (int)nh, scale, dc,
+                         dm == 2 ? mask : (uint32_t*)nullptr);
+    else if (T <= TMAX)
       hipLaunchKernelGGL((attn16_fwd_k<DM, HH, TMAX>), grid, dim3(FWD_NT), fwd_lds<TMAX>(), (hipStream_t)stream,
                          (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T, (int)nh, scale, dc,
                          dm == 2 ? mask : (uint32_t*)nullptr);
