@@ -447,6 +447,11 @@ int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float
 int b2p_attn16_bwd_f16(const void* qkv16h, const void* dO16, const float* lse2, float* delta_ws,
                        float* dqkv, void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh,
                        float scale, float drop_p, uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream);
+/* Selects the dK/dV kernel of b2p_attn16_bwd[_f16]: 1 (default) = each wave runs its two key tiles in
+ * one pass over the queries (shared LDS reads and conversions), 0 = one pass per key tile. Both
+ * accumulate in the same order, so the outputs are bitwise equal. Process-wide; the initial value
+ * comes from B2P_ATTN_DKV2 (0 selects the per-tile kernel). */
+int b2p_attn16_dkv_variant(int v);
 
 /* ------------------------------------------------------------------ CTC
  * log_softmax + nn.CTCLoss(blank=0, reduction="mean", zero_infinity=True)

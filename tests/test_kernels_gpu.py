@@ -279,6 +279,42 @@ def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
     assert float((lse2 - ref_lse2).abs().max()) < 2e-2
 
 
+@pytest.mark.parametrize("B,T,nh,p", [(2, 249, 12, 0.1), (3, 100, 4, 0.0), (1, 17, 2, 0.1), (2, 256, 3, 0.1),
+                                       (1, 241, 2, 0.1), (2, 313, 4, 0.1), (1, 512, 2, 0.0)])
+@pytest.mark.parametrize("form", ["f16_mask", "bf16_hash"])
+def test_attention_dkv_paired_tiles_bitwise(B, T, nh, p, form):
+    """The paired-key-tile dK/dV kernel (attn16_bwd_dkv2_k, the default) against the per-tile kernel
+    (b2p_attn16_dkv_variant(0)): same accumulation order per key tile, so dQ/dK/dV are bitwise equal
+    (fp32 and bf16 outputs), at T' with partial tiles, a wave whose second tile lies beyond T', and the
+    512-key kernels."""
+    Fn = _fn()
+    lib = Fn._lib.load()
+    torch.manual_seed(11)
+    dh = 64
+    D = nh * dh
+    qkv = (torch.randn(B * T, 3 * D) * 0.7).cuda()
+    dO = torch.randn(B * T, D).to(torch.bfloat16).cuda()
+    seed = 99
+    if form == "f16_mask":
+        q16 = qkv.to(torch.float16)
+        _, _, lse2, mask = Fn._attn16_fwd_f16(q16, B, T, nh, dh, p, seed)
+    else:
+        q16 = qkv.to(torch.bfloat16)
+        _, lse2 = Fn._attn16_fwd(q16, B, T, nh, dh, p, seed)
+        mask = None
+    outs = []
+    try:
+        for v in (1, 0):
+            Fn._lib.check(lib.b2p_attn16_dkv_variant(v), "dkv_variant")
+            outs.append(Fn._attn16_bwd(q16, dO, lse2, B, T, nh, dh, p, seed, mask=mask))
+        torch.cuda.synchronize()
+    finally:
+        Fn._lib.check(lib.b2p_attn16_dkv_variant(1), "dkv_variant")
+    (a32, a16), (b32, b16) = outs
+    assert torch.equal(a32, b32) and torch.equal(a16, b16)
+    assert float(a32[:, D:].abs().sum()) > 0
+
+
 def test_front_end():
     Fn = _fn()
     from oracle.b2p2t_oracle import gaussian_taps, gaussian_smooth, day_linear_softsign

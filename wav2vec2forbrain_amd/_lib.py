@@ -70,6 +70,7 @@ _SIGS = {
     "b2p_colsum_batched": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p, c_i32, c_p, c_p]),
     "b2p_colsum_parts": (c_i32, [c_p, c_i64, c_i64, c_p, c_i32, c_p]),
     "b2p_gemm16_variant": (c_i32, [c_i32]),
+    "b2p_attn16_dkv_variant": (c_i32, [c_i32]),
     "b2p_set_gate_batch": (c_i32, [c_p]),
     "b2p_split3_bf16": (c_i32, [c_p, c_i64, c_i64, c_i64, c_p, c_i64, c_i32, c_i32, c_p]),
     "b2p_i64_fill": (c_i32, [c_p, ctypes.POINTER(c_i64), c_i32, c_p]),

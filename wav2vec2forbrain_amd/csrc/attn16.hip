@@ -450,6 +450,163 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv_k(const uint16_t* __restri
   }
 }
 
+// Paired form: each wave runs its two key tiles (w and w + 4 of the block) in ONE pass over the queries,
+// so every Q / dO fragment read from LDS, every fp16 -> bf16 conversion of the Q^T operand, every lse2 /
+// delta / keep-word read serves both tiles (the per-tile form repeats them per tile: the conversions
+// alone were ~50 VALU per 32-query chunk and tile). Keep words are staged [word][query] (rows padded by
+// 8 words: the 4 words a 32-lane half reads land on distinct banks) so a lane's 4 consecutive queries
+// are one 16-byte read; validity and keep are all-ones / zero bit masks. Accumulation order per tile
+// is the per-tile kernel's, so both forms write bitwise-equal dK / dV.
+constexpr int MSK_LD = TMAX + 8;
+template <int DM, bool H, int TM>
+__global__ void __launch_bounds__(256) attn16_bwd_dkv2_k(const uint16_t* __restrict__ qkv, const float* __restrict__ delta,
+                                                         const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
+                                                         float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
+                                                         int nh, float scale, DropCfg dc,
+                                                         const uint32_t* __restrict__ maskw) {
+  static_assert(TM == TMAX || DM != 2, "the stored keep mask covers T <= 256");
+  constexpr bool DROP = DM != 0;
+  dc.seed = b2p_seed_eff(dc.seed, dc.epoch);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  float* lse_s = reinterpret_cast<float*>(smem + 2 * TM * 128);
+  float* del_s = lse_s + TM;
+  uint32_t* msk_s = reinterpret_cast<uint32_t*>(del_s + TM);   // [word j][query], row stride MSK_LD (TM 256)
+  const int nkb = (T + BWD_KB - 1) / BWD_KB;
+  const int bhi = blockIdx.x / nkb, kb = blockIdx.x - bhi * nkb;
+  const int b = bhi / nh, h = bhi - b * nh;
+  const int D = nh * DH;
+  const int64_t ld = 3 * (int64_t)D;
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63, lr = l & 15, g = l >> 4;
+  const int64_t row0 = (int64_t)b * T;
+  if (b2p_gated_off(dc.gate)) {   // LayerDrop: zero dK, dV (the bias reduction reads them)
+    for (int half = 0; half < 2; ++half) {
+      zero_block(dqkv, dqkv16, row0, kb * BWD_KB + 64 * half, T, ld, D + h * DH, tid);
+      zero_block(dqkv, dqkv16, row0, kb * BWD_KB + 64 * half, T, ld, 2 * D + h * DH, tid);
+    }
+    return;
+  }
+  load_image<TM>(smem, qkv, row0, T, ld, h * DH, tid);
+  load_image<TM>(smem + TM * 128, dO16, row0, T, D, h * DH, tid);
+  for (int qq = tid; qq < TM; qq += 256) {   // one thread per query row: lse2 and delta (from the dQ pass)
+    const int64_t o = ((int64_t)b * nh + h) * T + qq;
+    del_s[qq] = qq < T ? delta[o] : 0.f;
+    lse_s[qq] = qq < T ? lse2[o] : 0.f;
+    if (DM == 2) {   // the keep bits of keys 128kb .. 128kb+127 for every query row: word 2j + kb, j = 0..3
+#pragma unroll
+      for (int j = 0; j < 4; ++j) msk_s[j * MSK_LD + qq] = qq < T ? maskw[o * 8 + 2 * j + kb] : 0u;
+    }
+  }
+  __syncthreads();
+  const int kt0 = kb * (BWD_KB / 16) + w;
+  if (kt0 * 16 >= T) return;   // both of this wave's key tiles lie beyond T (no barrier follows)
+  const float c2 = scale * LOG2E;
+  const uint64_t bh = (uint64_t)b * nh + h;
+  const int TP = T + (T & 1);
+  uint32_t obase = 0;   // opaque image bases: no hoisting of the unrolled body's LDS addresses
+  asm volatile("" : "+v"(obase));
+  const char* Qimg = smem + obase;
+  const char* dOimg = smem + TM * 128 + obase;
+  // tile t = key tile kt0 + 4t: keys key[t] = (kt0 + 4t) * 16 + lr on the lane
+  int key[2];
+  uint32_t kokm[2];
+  bf16x8 kf[2][2], vf[2][2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    key[t] = (kt0 + 4 * t) * 16 + lr;
+    const bool kok = key[t] < T;
+    kokm[t] = 0u - (uint32_t)kok;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      kf[t][ks] = vf[t][ks] = bf16x8{};
+      if (kok) {
+        kf[t][ks] = gload8(qkv + (row0 + key[t]) * ld + D + h * DH + 32 * ks + 8 * g);
+        vf[t][ks] = to_b16<H>(gload8(qkv + (row0 + key[t]) * ld + 2 * D + h * DH + 32 * ks + 8 * g));
+      }
+    }
+  }
+  // keep bit of key[t] in its query's word (lr >> 2): mask_shift(key[0]) < 16, key[1] = key[0] + 64 -> +16
+  const int kw = lr >> 2;
+  const int ksh = mask_shift(key[0]);
+  f32x4 dv[2][4], dk[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) dv[t][dt] = dk[t][dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nchunk = (T + 31) >> 5;
+  for (int c = 0; c < nchunk; ++c) {
+    f32x4 pd[2][2], ds[2][2];   // [tile][half]
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      const int qt = 2 * c + half;
+      const int qb = qt * 16 + 4 * g;   // rows qb + i of this lane's registers
+      const float4 ls4 = *reinterpret_cast<const float4*>(lse_s + qb);
+      const float4 dl4 = *reinterpret_cast<const float4*>(del_s + qb);
+      uint4 mw4 = make_uint4(0u, 0u, 0u, 0u);
+      if (DM == 2) mw4 = *reinterpret_cast<const uint4*>(msk_s + kw * MSK_LD + qb);
+      const float lsv[4] = {ls4.x, ls4.y, ls4.z, ls4.w}, dlv[4] = {dl4.x, dl4.y, dl4.z, dl4.w};
+      const uint32_t mwv[4] = {mw4.x, mw4.y, mw4.z, mw4.w};
+      f32x4 sv[2], dp[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t) sv[t] = dp[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 qa = row_frag(Qimg, qt * 16 + lr, 32 * ks + 8 * g);
+        const bf16x8 oa = row_frag(dOimg, qt * 16 + lr, 32 * ks + 8 * g);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          sv[t] = mfma_t<H>(qa, kf[t][ks], sv[t]);
+          dp[t] = mfma(oa, vf[t][ks], dp[t]);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const uint32_t qm = (uint32_t)((qb + i - T) >> 31);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          const uint32_t km = qm & kokm[t];
+          const float p = __uint_as_float(__float_as_uint(exp2_fast(fmaf(sv[t][i], c2, -lsv[i]))) & km);
+          float ksc;
+          if constexpr (DM == 2) {
+            ksc = __uint_as_float(__float_as_uint(dc.scale) &
+                                  (uint32_t)((int32_t)(mwv[i] << (31 - (ksh + 16 * t))) >> 31));
+          } else {
+            ksc = keep_scale<DROP>(dc, (bh * T + (qb + i)) * (uint64_t)TP + key[t]);
+          }
+          pd[t][half][i] = p * ksc;
+          ds[t][half][i] = p * (dp[t][i] * ksc - dlv[i]);
+        }
+      }
+    }
+    bf16x8 bp[2], bs[2];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      bp[t] = pack_acc(pd[t][0], pd[t][1]);
+      bs[t] = pack_acc(ds[t][0], ds[t][1]);
+    }
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const bf16x8 ot = tr_frag(dOimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr);
+      const bf16x8 qtr = to_b16<H>(tr_frag(Qimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr));
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        dv[t][dt] = mfma(ot, bp[t], dv[t][dt]);
+        dk[t][dt] = mfma(qtr, bs[t], dk[t][dt]);
+      }
+    }
+  }
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    if (key[t] < T) {
+      const int64_t r = (row0 + key[t]) * ld + h * DH;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        store_out(dqkv, dqkv16, r + D + dt * 16 + 4 * g, dk[t][dt], scale);
+        store_out(dqkv, dqkv16, r + 2 * D + dt * 16 + 4 * g, dv[t][dt], 1.f);
+      }
+    }
+  }
+}
+
 // --------------------------------------------------------------------------------------- backward dQ
 // Runs BEFORE the dK/dV kernel: delta[q] = sum_key P_d dP_d is formed here from the very P and dP
 // the kernel recomputes (not as dO . O from the rounded bf16 O), so sum_key dS = 0 holds to fp32
@@ -628,7 +785,7 @@ DropCfg drop_cfg(float p, uint64_t seed) {
 template <int TM>
 constexpr size_t fwd_lds() { return 2 * TM * 128; }
 template <int TM>
-constexpr size_t bwd_lds() { return 2 * TM * 128 + 2 * TM * 4 + (TM == TMAX ? 4 * TM * 4 : 0); }
+constexpr size_t bwd_lds() { return 2 * TM * 128 + 2 * TM * 4 + (TM == TMAX ? 4 * MSK_LD * 4 : 0); }
 
 template <typename K>
 int set_lds(K kern, size_t bytes) {
@@ -642,6 +799,8 @@ int init_attrs_t() {
   rc |= set_lds(attn16_fwd_k<1, H, TM>, fwd_lds<TM>());
   rc |= set_lds(attn16_bwd_dkv_k<0, H, TM>, bwd_lds<TM>());
   rc |= set_lds(attn16_bwd_dkv_k<1, H, TM>, bwd_lds<TM>());
+  rc |= set_lds(attn16_bwd_dkv2_k<0, H, TM>, bwd_lds<TM>());
+  rc |= set_lds(attn16_bwd_dkv2_k<1, H, TM>, bwd_lds<TM>());
   rc |= set_lds(attn16_bwd_dq_k<0, H, TM>, fwd_lds<TM>());
   rc |= set_lds(attn16_bwd_dq_k<1, H, TM>, fwd_lds<TM>());
   if constexpr (TM == TMAX) {
@@ -650,6 +809,7 @@ int init_attrs_t() {
     rc |= set_lds(attn16_fwd_k<2, H, TM, true>, fwd_lds<TM>());
     rc |= set_lds(attn16_fwd_k<2, H, TM>, fwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dkv_k<2, H, TM>, bwd_lds<TM>());
+    rc |= set_lds(attn16_bwd_dkv2_k<2, H, TM>, bwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dq_k<2, H, TM>, fwd_lds<TM>());
   }
   return rc;
@@ -663,6 +823,13 @@ int init_attrs() {
 }  // namespace
 
 namespace {
+// dK/dV kernel form: 1 = paired key tiles (default), 0 = per tile (B2P_ATTN_DKV2=0 or b2p_attn16_dkv_variant;
+// A/B and the bitwise-equality test)
+int g_dkv_variant = -1;
+bool attn_dkv2() {
+  if (g_dkv_variant < 0) g_dkv_variant = (getenv("B2P_ATTN_DKV2") && getenv("B2P_ATTN_DKV2")[0] == '0') ? 0 : 1;
+  return g_dkv_variant != 0;
+}
 bool attn_t1() {   // B2P_ATTN_T1=0: the masked form for every T (A/B)
   static const bool on = !(getenv("B2P_ATTN_T1") && getenv("B2P_ATTN_T1")[0] == '0');
   return on;
@@ -745,13 +912,21 @@ int attn16_bwd_launch(bool half, const void* qkv16, const void* dO16, const floa
     if (T <= TMAX) {
       hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH, TMAX>), grid_q, dim3(256), fwd_lds<TMAX>(), st, q, delta_ws, d, lse2,
                          dqkv, d16, (int)T, (int)nh, scale, dc, mask);
-      hipLaunchKernelGGL((attn16_bwd_dkv_k<DM, HH, TMAX>), grid_k, dim3(256), bwd_lds<TMAX>(), st, q, delta_ws, d, lse2,
-                         dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+      if (attn_dkv2())
+        hipLaunchKernelGGL((attn16_bwd_dkv2_k<DM, HH, TMAX>), grid_k, dim3(256), bwd_lds<TMAX>(), st, q, delta_ws, d,
+                           lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+      else
+        hipLaunchKernelGGL((attn16_bwd_dkv_k<DM, HH, TMAX>), grid_k, dim3(256), bwd_lds<TMAX>(), st, q, delta_ws, d,
+                           lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
     } else if constexpr (DM != 2) {
       hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH, 2 * TMAX>), grid_q, dim3(256), fwd_lds<2 * TMAX>(), st, q, delta_ws,
                          d, lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
-      hipLaunchKernelGGL((attn16_bwd_dkv_k<DM, HH, 2 * TMAX>), grid_k, dim3(256), bwd_lds<2 * TMAX>(), st, q, delta_ws,
-                         d, lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+      if (attn_dkv2())
+        hipLaunchKernelGGL((attn16_bwd_dkv2_k<DM, HH, 2 * TMAX>), grid_k, dim3(256), bwd_lds<2 * TMAX>(), st, q,
+                           delta_ws, d, lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+      else
+        hipLaunchKernelGGL((attn16_bwd_dkv_k<DM, HH, 2 * TMAX>), grid_k, dim3(256), bwd_lds<2 * TMAX>(), st, q,
+                           delta_ws, d, lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
     }
   };
   auto by_dm = [&](auto hc) {
@@ -765,6 +940,11 @@ int attn16_bwd_launch(bool half, const void* qkv16, const void* dO16, const floa
   return 0;
 }
 }  // namespace
+
+extern "C" int b2p_attn16_dkv_variant(int v) {
+  g_dkv_variant = v ? 1 : 0;
+  return 0;
+}
 
 extern "C" int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws, float* dqkv,
                               void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh, float scale, float drop_p,
