@@ -613,7 +613,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dkv2_k(const uint16_t* __restr
 // rounding — otherwise the residual feeds a systematic, Q-correlated error into dK. Pass 1 keeps
 // P and dP*keep in registers, pass 2 forms dS and dQ^T += K^T dS^T. One workgroup per (batch, head,
 // 128 queries): K and V staged once, 4 waves x query tiles w and w + 4.
-template <int DM, bool H, int TM>   // DM 0: no dropout, 1: hash the keep mask, 2: keep bits in memory; H: fp16 qkv
+template <int DM, bool H, int TM, bool T1 = false>   // DM 0: no dropout, 1: hash, 2: keep bits in memory; H: fp16 qkv; T1: T > TM - 16
 __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restrict__ qkv, float* __restrict__ delta,
                                                        const uint16_t* __restrict__ dO16, const float* __restrict__ lse2,
                                                        float* __restrict__ dqkv, uint16_t* __restrict__ dqkv16, int T,
@@ -640,6 +640,9 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
   const float c2 = scale * LOG2E;
   const int TP = T + (T & 1);
   const int qt0 = qh * (FWD_QB / 16) + w;
+  uint32_t tailm[4];   // T1: validity masks of this lane's keys in the last key tile
+#pragma unroll
+  for (int i = 0; i < 4; ++i) tailm[i] = (uint32_t)((TM - 16 + 4 * g + i - T) >> 31);
   for (int qt = qt0; qt < qt0 + FWD_QB / 16 && qt * 16 < T; qt += 4) {
     uint32_t obase = 0;   // opaque image bases: no hoisting of the unrolled body's LDS addresses
     asm volatile("" : "+v"(obase));
@@ -713,7 +716,7 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
       }
       continue;
     }
-    const uint32_t qm = 0u - (uint32_t)qok;
+    // keys >= T are masked; rows q >= T need no mask (a lane's dS only reaches its own, unstored dQ row)
     uint2 mw = make_uint2(0u, 0u);   // this lane's keep bytes of the query row (keys kt*16 + 4g + i)
     if (DM == 2 && qok) mw = *reinterpret_cast<const uint2*>(maskw + (int64_t)rowc * 8 + 2 * g);
     f32x4 P[16], PD[16];
@@ -731,13 +734,14 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
         // validity and keep as all-ones / zero bit masks formed arithmetically: compare-and-select per
         // element left 64 lane masks live in SGPR pairs across the unrolled tiles (238 SGPR spills)
         const int key = kt * 16 + 4 * g + i;
-        const uint32_t km = qm & (uint32_t)((key - T) >> 31);
+        // T1: only the last key tile holds keys >= T (its 4 masks computed once per kernel)
+        const uint32_t km = T1 ? (kt == 15 ? tailm[i] : ~0u) : (uint32_t)((key - T) >> 31);
         const float p = __uint_as_float(__float_as_uint(exp2_fast(fmaf(sv[i], c2, -ls))) & km);
         float kp;
         if constexpr (DM == 2) {
           const uint32_t wd = kt < 8 ? mw.x : mw.y;
           const int bit = 8 * ((kt >> 1) & 3) + 4 * (kt & 1) + i;
-          kp = __uint_as_float(__float_as_uint(dc.scale) & (uint32_t)((int32_t)(wd << (31 - bit)) >> 31));
+          kp = __uint_as_float(__float_as_uint(dc.scale) & (uint32_t)__builtin_amdgcn_sbfe((int)wd, bit, 1));
         } else {
           kp = keep_scale<DROP>(dc, rowidx + key);
         }
@@ -753,22 +757,56 @@ __global__ void __launch_bounds__(256) attn16_bwd_dq_k(const uint16_t* __restric
     f32x4 dq[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) dq[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float dqs = scale;
+    if constexpr (H) {
+      // fp16 K (as staged) x fp16 dS: the whole row's dS is in registers, so it is scaled by a power of
+      // two that puts the row's largest |dS| in [1, 2) (fp16 then holds it with 11 significant bits,
+      // bf16 would keep 8) and the product is unscaled at the store; no per-chunk fp16 -> bf16
+      // conversion of the K^T operand
+      float mx = 0.f;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
-      f32x4 ds[2];
+      for (int kt = 0; kt < 16; ++kt)
 #pragma unroll
-      for (int half = 0; half < 2; ++half)
+        for (int i = 0; i < 4; ++i) {
+          const float d = P[kt][i] * (PD[kt][i] - dl);
+          P[kt][i] = d;
+          mx = fmaxf(mx, fabsf(d));
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const int em = min(max((int)(__float_as_uint(mx) >> 23), 1), 253);   // mx = 2^(em-127) * 1.f
+      const float rs = __uint_as_float((uint32_t)(254 - em) << 23);          // 2^-(em-127)
+      dqs = scale * __uint_as_float((uint32_t)em << 23);                     // scale * 2^(em-127)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) ds[half][i] = P[2 * c + half][i] * (PD[2 * c + half][i] - dl);
-      const bf16x8 bs = pack_acc(ds[0], ds[1]);
+      for (int c = 0; c < 8; ++c) {
+        f32x4 ds[2];
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-        dq[dt] = mfma(to_b16<H>(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr)), bs, dq[dt]);
+        for (int half = 0; half < 2; ++half)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ds[half][i] = P[2 * c + half][i] * rs;
+        const bf16x8 bs = pack_acc_t<true>(ds[0], ds[1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          dq[dt] = mfma_t<true>(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dq[dt]);
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        f32x4 ds[2];
+#pragma unroll
+        for (int half = 0; half < 2; ++half)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) ds[half][i] = P[2 * c + half][i] * (PD[2 * c + half][i] - dl);
+        const bf16x8 bs = pack_acc(ds[0], ds[1]);
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+          dq[dt] = mfma(tr_frag(Kimg, 32 * c + 4 * g, 32 * c + 16 + 4 * g, dt * 16, lr), bs, dq[dt]);
+      }
     }
     if (qok) {
       const int64_t r = (row0 + q) * ld + h * DH;
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) store_out(dqkv, dqkv16, r + dt * 16 + 4 * g, dq[dt], scale);
+      for (int dt = 0; dt < 4; ++dt) store_out(dqkv, dqkv16, r + dt * 16 + 4 * g, dq[dt], dqs);
     }
   }
 }
@@ -811,6 +849,9 @@ int init_attrs_t() {
     rc |= set_lds(attn16_bwd_dkv_k<2, H, TM>, bwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dkv2_k<2, H, TM>, bwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dq_k<2, H, TM>, fwd_lds<TM>());
+    rc |= set_lds(attn16_bwd_dq_k<0, H, TM, true>, fwd_lds<TM>());
+    rc |= set_lds(attn16_bwd_dq_k<1, H, TM, true>, fwd_lds<TM>());
+    rc |= set_lds(attn16_bwd_dq_k<2, H, TM, true>, fwd_lds<TM>());
   }
   return rc;
 }
@@ -910,8 +951,12 @@ int attn16_bwd_launch(bool half, const void* qkv16, const void* dO16, const floa
     constexpr int DM = decltype(dm)::value;
     constexpr bool HH = decltype(hc)::value;
     if (T <= TMAX) {
-      hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH, TMAX>), grid_q, dim3(256), fwd_lds<TMAX>(), st, q, delta_ws, d, lse2,
-                         dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+      if (T > TMAX - 16 && attn_t1())
+        hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH, TMAX, true>), grid_q, dim3(256), fwd_lds<TMAX>(), st, q, delta_ws,
+                           d, lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
+      else
+        hipLaunchKernelGGL((attn16_bwd_dq_k<DM, HH, TMAX>), grid_q, dim3(256), fwd_lds<TMAX>(), st, q, delta_ws, d,
+                           lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
       if (attn_dkv2())
         hipLaunchKernelGGL((attn16_bwd_dkv2_k<DM, HH, TMAX>), grid_k, dim3(256), bwd_lds<TMAX>(), st, q, delta_ws, d,
                            lse2, dqkv, d16, (int)T, (int)nh, scale, dc, mask);
