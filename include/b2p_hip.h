@@ -211,6 +211,17 @@ int b2p_layernorm_bwd16(const float* dy, const float* x, const float* gamma, con
                         int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
                         float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
                         uint16_t* d16, float* workspace, b2p_stream_t stream);
+/* b2p_layernorm_bwd16 with a second accumulator added to dx alone, after dx_accum and after the
+ * dx_dropped / dbias_in outputs are formed (NULL = none; d16 of dx includes it): the skip-path
+ * gradient of a LayerDrop-selected encoder layer (functional.layerdrop_layer), folded into the layer's
+ * input-gradient LayerNorm instead of a separate add. With dgamma = dbeta = dbias_in = NULL the
+ * parameter gradients are left as per-block partials in workspace: [3][nblk][cols] floats at offset
+ * 0, nblk = ceil(rows / 16) (dgamma | dbeta | dbias_in rows, summed later by the caller). */
+int b2p_layernorm_bwd_acc2(const float* dy, const float* x, const float* gamma, const float* mean,
+                           const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                           int64_t cols, const float* dx_accum, const float* dx_accum2, float drop_p,
+                           uint64_t drop_seed, float* dx_dropped, float in_drop_p, uint64_t in_drop_seed,
+                           float* dbias_in, uint16_t* d16, float* workspace, b2p_stream_t stream);
 
 /* fp32 -> bf16 (round to nearest even), the GEMM operand copy of a weight or activation
  * (master copies stay fp32; replaces the implicit .to(bfloat16) of autocast) */

@@ -192,3 +192,56 @@ def test_captured_layerdrop_adam_leaves_dropped_layers(name):
         if ".layers." in n:   # an encoder layer's tensors stepped once per replay that kept the layer
             k = int(n.split(".layers.")[1].split(".")[0])
             assert e_step == used_layers[k], (n, e_step, used_layers[k])
+
+
+@pytest.mark.parametrize("name", ["tiny_a", "tiny_conf", "tiny_stable"])
+def test_layerdrop_skip_gradient_fold_bitwise(name):
+    """The skip-path gradient of a LayerDrop-selected layer is added inside the layer's input-gradient
+    LayerNorm backward (functional._SkipSlot, b2p_layernorm_bwd_acc2) instead of by autograd in a
+    separate add: replayed steps with and without the fold give bitwise-equal losses and gradients
+    (exactly one of the two summands is nonzero in every replay), and the fold really removes the
+    skip gradient from autograd (every layer's select hands it to a claiming Function)."""
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.train.step_graph import StepGraph
+    cfg = CFG[name]
+    out = {}
+    for fold in (True, False):
+        Fn._LD_SKIP_FOLD = fold
+        Fn.SEEDS.reseed(99)
+        Fn.LD_SEEDS.reseed(99)
+        torch.manual_seed(3)
+        model = _model(name)
+        batch = _batch(cfg)
+        slots = []
+        orig = Fn._LayerDropSelect.apply
+
+        def spy(x, y, p, seed, slot=None):
+            slots.append(slot)
+            return orig(x, y, p, seed, slot)
+
+        def step():
+            for p in model.parameters():
+                p.grad = None
+            o = model(batch)
+            o.loss.backward()
+            return o.metrics["ctc_loss"]
+
+        Fn._LayerDropSelect.apply = spy
+        try:
+            with Fn.precision("bf16"):
+                sg = StepGraph(step, None, warmup=0, warm_replays=0)
+                sg.capture()
+                losses = [float(sg.replay()) for _ in range(REPLAYS)]
+                grads = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
+                sg.release()
+        finally:
+            Fn._LayerDropSelect.apply = orig
+            Fn._LD_SKIP_FOLD = True
+        torch.cuda.synchronize()
+        assert len(slots) == cfg["layers"]
+        assert all((s is not None) == fold for s in slots), slots
+        out[fold] = (losses, grads)
+    assert out[True][0] == out[False][0]
+    assert out[True][1].keys() == out[False][1].keys()
+    for n, g in out[True][1].items():
+        assert torch.equal(g, out[False][1][n]), n

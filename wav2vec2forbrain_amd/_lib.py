@@ -86,6 +86,8 @@ _SIGS = {
     "b2p_layernorm_fwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_u64, c_p]),
     "b2p_layernorm_bwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_f32, c_u64,
                                     c_p, c_f32, c_u64, c_p, c_p, c_p, c_p]),
+    "b2p_layernorm_bwd_acc2": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_p, c_p, c_f32, c_u64,
+                                       c_p, c_f32, c_u64, c_p, c_p, c_p, c_p]),
     "b2p_cast_bf16": (c_i32, [c_p, c_p, c_i64, c_p]),
     "b2p_softmax_fwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_u64, c_p]),
     "b2p_softmax_bwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_f32, c_u64, c_p]),

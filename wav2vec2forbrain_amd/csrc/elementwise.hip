@@ -481,14 +481,19 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
 }
 
 constexpr int LN_BWD_ROWS = 16;   // rows per block (4 per wave): ~500 blocks at 8k rows
-template <bool PF>   // PF: prefetch the next row (B2P_LN_PREFETCH, default 1)
+// PF: prefetch the next row (B2P_LN_PREFETCH, default 1). MODE bits: 1 = dx_accum, 2 = dx_accum2, 4 = dxd
+// (compile-time, so a form holds registers only for the streams it reads: all three at once would not
+// fit two waves per SIMD)
+constexpr int LNB_A1 = 1, LNB_A2 = 2, LNB_DXD = 4;
+template <bool PF, int MODE>
 __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, const float* __restrict__ x,
                                                 const float* __restrict__ gamma, const float* __restrict__ mean,
                                                 const float* __restrict__ rstd, float* __restrict__ dx,
                                                 const float* __restrict__ dx_accum, float* __restrict__ part,
                                                 int64_t rows, int cols, uint32_t thr, float dscale, uint64_t seed,
                                                 float drop_p, float* __restrict__ dxd, uint32_t thr2, float dscale2,
-                                                uint64_t seed2, uint16_t* __restrict__ d16, const uint64_t* __restrict__ epoch) {
+                                                uint64_t seed2, uint16_t* __restrict__ d16, const uint64_t* __restrict__ epoch,
+                                                const float* __restrict__ dx_accum2) {
   seed = b2p_seed_eff(seed, epoch);
   seed2 = b2p_seed_eff(seed2, epoch);
   __shared__ float red[4][3][LN_MAXV * 256];   // cols <= 1024
@@ -505,7 +510,7 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
   const int64_t row_base = (int64_t)blockIdx.x * LN_BWD_ROWS + wave * (LN_BWD_ROWS / 4);
   // the residual gradient dx_accum is fetched with dy / x (read at the store, it cost a full load
   // latency per row)
-  float4 nd[LN_MAXV], nx[LN_MAXV], na[LN_MAXV];
+  float4 nd[LN_MAXV], nx[LN_MAXV], na[LN_MAXV], nb[LN_MAXV];
   auto fetch = [&](int64_t r) {
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
@@ -513,7 +518,8 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
       if (c < nv && r < rows) {
         nd[i] = reinterpret_cast<const float4*>(dy + r * cols)[c];
         nx[i] = reinterpret_cast<const float4*>(x + r * cols)[c];
-        if (dx_accum) na[i] = reinterpret_cast<const float4*>(dx_accum + r * cols)[c];
+        if (MODE & LNB_A1) na[i] = reinterpret_cast<const float4*>(dx_accum + r * cols)[c];
+        if (MODE & LNB_A2) nb[i] = reinterpret_cast<const float4*>(dx_accum2 + r * cols)[c];
       }
     }
   };
@@ -529,12 +535,13 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
     if (row >= rows) break;
     const float mu = mean[row], rs = rstd[row];
     if (!PF && rr > 0) fetch(row);
-    float4 cd[LN_MAXV], cx[LN_MAXV], ca[LN_MAXV];
+    float4 cd[LN_MAXV], cx[LN_MAXV], ca[LN_MAXV], cb[LN_MAXV];
 #pragma unroll
     for (int i = 0; i < LN_MAXV; ++i) {
       cd[i] = nd[i];
       cx[i] = nx[i];
       ca[i] = na[i];
+      cb[i] = nb[i];
     }
     if (PF && rr + 1 < LN_BWD_ROWS / 4) fetch(row + 1);
     float4 xh[LN_MAXV], gg[LN_MAXV];
@@ -574,16 +581,22 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
         o.y = rs * (gg[i].y - s1 - xh[i].y * s2);
         o.z = rs * (gg[i].z - s1 - xh[i].z * s2);
         o.w = rs * (gg[i].w - s1 - xh[i].w * s2);
-        if (dx_accum) {
+        if (MODE & LNB_A1) {
           // the residual add stays a separate rounding (no fused multiply-add with the rs product):
           // the same bits as when the add sat behind its own load
           asm volatile("" : "+v"(o.x), "+v"(o.y), "+v"(o.z), "+v"(o.w));
           const float4 a = ca[i];
           o.x += a.x; o.y += a.y; o.z += a.z; o.w += a.w;
         }
-        dxr[c] = o;
-        if (d16 && !dxd) reinterpret_cast<uint2*>(d16 + row * cols)[c] = b2p_pack_bf16x4(o);
-        if (dxd) {   // gradient of the dropout that produced this LN's input (residual branch)
+        float4 ox = o;
+        if (MODE & LNB_A2) {   // a separate rounding after the first accumulator, as autograd's add was
+          asm volatile("" : "+v"(ox.x), "+v"(ox.y), "+v"(ox.z), "+v"(ox.w));
+          const float4 b = cb[i];
+          ox.x += b.x; ox.y += b.y; ox.z += b.z; ox.w += b.w;
+        }
+        dxr[c] = ox;
+        if (d16 && !(MODE & LNB_DXD)) reinterpret_cast<uint2*>(d16 + row * cols)[c] = b2p_pack_bf16x4(ox);
+        if (MODE & LNB_DXD) {   // gradient of the dropout that produced this LN's input (residual branch)
           const uint64_t base = (uint64_t)row * cols + 4 * c;
           float4 q;
           bool kk[4];
@@ -612,8 +625,8 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
   __syncthreads();
   for (int c = threadIdx.x; c < cols; c += 256) {
 #pragma unroll
-    for (int q = 0; q < 3; ++q)
-      part[((int64_t)blockIdx.x * 3 + q) * cols + c] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
+    for (int q = 0; q < 3; ++q)   // [3][nblk][cols]: each output's partial rows contiguous
+      part[((int64_t)q * gridDim.x + blockIdx.x) * cols + c] = red[0][q][c] + red[1][q][c] + red[2][q][c] + red[3][q][c];
   }
 }
 
@@ -621,20 +634,28 @@ __global__ void __launch_bounds__(256) ln_bwd_k(const float* __restrict__ dy, co
 // (dgamma | dbeta | dropout-input bias) summed over the blocks straight into their destinations (was
 // the two-phase column sum + a scatter: three launches per LayerNorm backward). 128 columns (float4 per
 // thread) x 8 row lanes per block, 8 independent partial sums per thread.
-__global__ void __launch_bounds__(256) ln_param_reduce_k(const float* __restrict__ part, int nblk, int cols,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 2))) ln_param_reduce_k(const float* __restrict__ part, int nblk, int cols,
                                                          float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                          float* __restrict__ dbias_in) {
   __shared__ float4 red[8][32];
   const int c4 = threadIdx.x & 31, rl = threadIdx.x >> 5;
   const int n = blockIdx.x * 128 + 4 * c4;   // column of the [3][cols] row
   const int N = 3 * cols;
+  const int q0 = n / cols;                   // output (dgamma | dbeta | dbias_in): partials [q0][nblk][cols]
   float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
   if (n < N) {
-    const float* p = part + n;
-#pragma unroll 8
-    for (int r = rl; r < nblk; r += 8) {
-      const float4 x = *reinterpret_cast<const float4*>(p + (int64_t)r * N);
-      s.x += x.x; s.y += x.y; s.z += x.z; s.w += x.w;
+    const float* p = part + (int64_t)q0 * nblk * cols + (n - q0 * cols);
+    // rows rl, rl + 8, ... summed in order; 32 of them in flight per batch (8 per batch left each thread
+    // ~8 dependent memory round trips at 500 partial rows: 7.1 us per launch on the Conformer)
+    // (rows past the end load as +0: adding them leaves every sum unchanged)
+    for (int r = rl; r < nblk; r += 8 * 32) {
+      float4 x[32];
+#pragma unroll
+      for (int k = 0; k < 32; ++k)
+        x[k] = r + 8 * k < nblk ? *reinterpret_cast<const float4*>(p + (int64_t)(r + 8 * k) * cols)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < 32; ++k) { s.x += x[k].x; s.y += x[k].y; s.z += x[k].z; s.w += x[k].w; }
     }
   }
   red[rl][c4] = s;
@@ -948,6 +969,26 @@ extern "C" int b2p_layernorm_fwd(const float* x, const float* gamma, const float
   return b2p_layernorm_fwd16(x, gamma, beta, y, nullptr, mean, rstd, rows, cols, eps, drop_p, drop_seed, stream);
 }
 
+namespace {
+typedef void (*LnBwdKernel)(const float*, const float*, const float*, const float*, const float*, float*, const float*,
+                            float*, int64_t, int, uint32_t, float, uint64_t, float, float*, uint32_t, float, uint64_t,
+                            uint16_t*, const uint64_t*, const float*);
+template <bool PF>
+LnBwdKernel ln_bwd_pick(int mode) {
+  switch (mode) {
+    case 0: return ln_bwd_k<PF, 0>;
+    case 1: return ln_bwd_k<PF, 1>;
+    case 2: return ln_bwd_k<PF, 2>;
+    case 3: return ln_bwd_k<PF, 3>;
+    case 4: return ln_bwd_k<PF, 4>;
+    case 5: return ln_bwd_k<PF, 5>;
+    case 6: return ln_bwd_k<PF, 6>;
+    default: return ln_bwd_k<PF, 7>;
+  }
+}
+LnBwdKernel ln_bwd_kernel(bool pf, int mode) { return pf ? ln_bwd_pick<true>(mode) : ln_bwd_pick<false>(mode); }
+}  // namespace
+
 extern "C" int64_t b2p_layernorm_bwd_workspace(int64_t rows, int64_t cols) {
   const int64_t nblk = (rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS;
   return nblk * 3 * cols + 3 * cols + ((nblk + kColsumRows - 1) / kColsumRows) * 3 * cols;
@@ -958,6 +999,15 @@ extern "C" int b2p_layernorm_bwd16(const float* dy, const float* x, const float*
                                    int64_t cols, const float* dx_accum, float drop_p, uint64_t drop_seed,
                                    float* dx_dropped, float in_drop_p, uint64_t in_drop_seed, float* dbias_in,
                                    uint16_t* d16, float* workspace, b2p_stream_t stream) {
+  return b2p_layernorm_bwd_acc2(dy, x, gamma, mean, rstd, dx, dgamma, dbeta, rows, cols, dx_accum, nullptr, drop_p,
+                                drop_seed, dx_dropped, in_drop_p, in_drop_seed, dbias_in, d16, workspace, stream);
+}
+
+extern "C" int b2p_layernorm_bwd_acc2(const float* dy, const float* x, const float* gamma, const float* mean,
+                                      const float* rstd, float* dx, float* dgamma, float* dbeta, int64_t rows,
+                                      int64_t cols, const float* dx_accum, const float* dx_accum2, float drop_p,
+                                      uint64_t drop_seed, float* dx_dropped, float in_drop_p, uint64_t in_drop_seed,
+                                      float* dbias_in, uint16_t* d16, float* workspace, b2p_stream_t stream) {
   B2P_CHECK_ARG(dy && x && gamma && mean && rstd && dx && workspace, "layernorm_bwd: NULL pointer");
   B2P_CHECK_ARG(cols % 4 == 0 && cols <= 64 * 4 * LN_MAXV, "layernorm_bwd: cols must be %%4 and <= 1024");
   B2P_CHECK_ARG(((uintptr_t)d16 & 7u) == 0, "layernorm_bwd: d16 must be 8-byte aligned");
@@ -965,15 +1015,17 @@ extern "C" int b2p_layernorm_bwd16(const float* dy, const float* x, const float*
   const int nblk = (int)((rows + LN_BWD_ROWS - 1) / LN_BWD_ROWS);
   hipStream_t st = (hipStream_t)stream;
   static const bool pf = getenv("B2P_LN_PREFETCH") ? atoi(getenv("B2P_LN_PREFETCH")) != 0 : true;
-  hipLaunchKernelGGL(pf ? ln_bwd_k<true> : ln_bwd_k<false>, dim3(nblk), dim3(256), 0, st, dy, x, gamma, mean, rstd, dx, dx_accum, workspace,
+  const int mode = (dx_accum ? LNB_A1 : 0) | (dx_accum2 ? LNB_A2 : 0) | (dx_dropped ? LNB_DXD : 0);
+  hipLaunchKernelGGL(ln_bwd_kernel(pf, mode), dim3(nblk), dim3(256), 0, st, dy, x, gamma, mean, rstd, dx, dx_accum, workspace,
                      rows, (int)cols, b2p_dropout_threshold(drop_p), drop_p > 0.f ? 1.f / (1.f - drop_p) : 1.f,
                      drop_seed, drop_p, dx_dropped, b2p_dropout_threshold(in_drop_p),
-                     in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed, d16, b2p_seed_epoch());
+                     in_drop_p > 0.f ? 1.f / (1.f - in_drop_p) : 1.f, in_drop_seed, d16, b2p_seed_epoch(), dx_accum2);
   // partials [nblk][3][cols] -> dgamma | dbeta | dbias_in in one launch
   B2P_CHECK_ARG(((uintptr_t)dgamma & 15u) == 0 && ((uintptr_t)dbeta & 15u) == 0 && ((uintptr_t)dbias_in & 15u) == 0,
                 "layernorm_bwd: dgamma / dbeta / dbias_in must be 16-byte aligned");
-  hipLaunchKernelGGL(ln_param_reduce_k, dim3((unsigned)((3 * cols + 127) / 128)), dim3(256), 0, st, workspace, nblk,
-                     (int)cols, dgamma, dbeta, dx_dropped ? dbias_in : nullptr);
+  if (dgamma || dbeta || (dx_dropped && dbias_in))   // else the caller sums the partials later
+    hipLaunchKernelGGL(ln_param_reduce_k, dim3((unsigned)((3 * cols + 127) / 128)), dim3(256), 0, st, workspace,
+                       nblk, (int)cols, dgamma, dbeta, dx_dropped ? dbias_in : nullptr);
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -1068,8 +1120,10 @@ __global__ void __launch_bounds__(256) split3_bf16_k(const float* __restrict__ x
   if (nv == 4 && ((uintptr_t)xs & 15u) == 0) {
     const float4 q = *reinterpret_cast<const float4*>(xs);
     v[0] = q.x; v[1] = q.y; v[2] = q.z; v[3] = q.w;
-  } else {
-    for (int j = 0; j < nv; ++j) v[j] = xs[j];
+  } else {   // unrolled with guards: a runtime-bounded loop indexed the arrays in scratch memory
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j < nv) v[j] = xs[j];
   }
   uint16_t hb[4], lb[4];
 #pragma unroll
@@ -1088,7 +1142,9 @@ __global__ void __launch_bounds__(256) split3_bf16_k(const float* __restrict__ x
     if (nv == 4 && ((uintptr_t)ys & 7u) == 0) {
       *reinterpret_cast<uint2*>(ys) = lo ? lv : hv;
     } else {
-      for (int j = 0; j < nv; ++j) ys[j] = lo ? lb[j] : hb[j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (j < nv) ys[j] = lo ? lb[j] : hb[j];
     }
   }
 }

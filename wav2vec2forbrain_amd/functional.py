@@ -1043,16 +1043,17 @@ def _ln_fwd(x2d, g, b, eps, drop_p=0.0, seed=0):
 
 
 def _ln_bwd(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, seed=0, in_drop_p=-1.0,
-            in_seed=0, dbias_in=None):
+            in_seed=0, dbias_in=None, dx_accum2=None):
+    """dx_accum2: a second accumulator added to dx alone (LayerDrop's skip gradient, _skip_take)."""
     rows, cols = x.shape
     dx = torch.empty_like(x)
     dg = torch.empty(cols, device=x.device) if need_params else None
     db = torch.empty(cols, device=x.device) if need_params else None
     ws = torch.empty(int(_lib.load().b2p_layernorm_bwd_workspace(rows, cols)), device=x.device)
     dxd = torch.empty_like(x) if in_drop_p >= 0.0 else None
-    _lib.call("b2p_layernorm_bwd", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows, cols,
-              _p(dx_accum), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed, _p(dbias_in),
-              _p(ws), _st())
+    _lib.call("b2p_layernorm_bwd_acc2", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows,
+              cols, _p(dx_accum), _p(dx_accum2), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed,
+              _p(dbias_in), None, _p(ws), _st())
     return dx, dg, db, dxd
 
 
@@ -1223,7 +1224,7 @@ def _ln_fwd16(x2d, g, b, eps, drop_p=0.0, seed=0):
 
 
 def _ln_bwd16(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, seed=0, in_drop_p=-1.0,
-              in_seed=0, dbias_in=None):
+              in_seed=0, dbias_in=None, dx_accum2=None):
     """as _ln_bwd, plus d16 = bf16(dx_dropped if in_drop_p >= 0 else dx)"""
     rows, cols = x.shape
     dx = torch.empty_like(x)
@@ -1232,8 +1233,8 @@ def _ln_bwd16(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0,
     ws = torch.empty(int(_lib.load().b2p_layernorm_bwd_workspace(rows, cols)), device=x.device)
     dxd = torch.empty_like(x) if in_drop_p >= 0.0 else None
     d16 = torch.empty(rows, cols, device=x.device, dtype=BF16)
-    _lib.call("b2p_layernorm_bwd16", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows,
-              cols, _p(dx_accum), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed,
+    _lib.call("b2p_layernorm_bwd_acc2", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows,
+              cols, _p(dx_accum), _p(dx_accum2), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed,
               _p(dbias_in), _p(d16), _p(ws), _st())
     return dx, dg, db, dxd, d16
 
@@ -1743,12 +1744,50 @@ def _b16_of(x):
     return t[1] if t is not None and t[0] == x._version else None
 
 
+class _SkipSlot:
+    """The skip-path gradient of one LayerDrop-selected layer, handed from the select's backward to the
+    layer Function that consumes the layer input (it adds it to its input gradient inside its last
+    LayerNorm backward, b2p_layernorm_bwd_acc2, instead of autograd adding the two gradients in a
+    separate pass). Exactly one of the two is nonzero (the route kernel writes dout to one side and
+    zeros to the other; a skipped layer's gated backward yields exact zeros), so the sum is bitwise the
+    one autograd formed."""
+    __slots__ = ("claimed", "grad")
+
+    def __init__(self):
+        self.claimed = False
+        self.grad = None
+
+
+_SKIP_CLAIM: dict = {}   # data_ptr of a layer input -> its _SkipSlot, while that layer's forward runs
+# B2P_LD_SKIP_FOLD=0: the skip gradient goes back through autograd (its own add kernel), as before
+_LD_SKIP_FOLD = os.environ.get("B2P_LD_SKIP_FOLD", "1") != "0"
+
+
+def _skip_claim(x):
+    """Called by a layer Function's forward with its input: the slot whose skip gradient its backward
+    must add to dx (None when x is not a LayerDrop-selected layer's input or was claimed already)."""
+    slot = _SKIP_CLAIM.get(x.data_ptr()) if _SKIP_CLAIM else None
+    if slot is None or slot.claimed:
+        return None
+    slot.claimed = True
+    return slot
+
+
+def _skip_take(slot):
+    """The skip gradient for a claiming Function's backward (None: nothing to add)."""
+    if slot is None:
+        return None
+    g, slot.grad = slot.grad, None
+    return g
+
+
 class _LayerDropSelect(torch.autograd.Function):
     """out = keep ? y : x with keep drawn on the device (csrc/layerdrop.hip); the backward routes
-    dout to the layer (keep) or around it (skip)."""
+    dout to the layer (keep) or around it (skip). With a claimed _SkipSlot the skip gradient goes to
+    the layer's input Function instead of back through autograd."""
 
     @staticmethod
-    def forward(ctx, x, y, p, seed):
+    def forward(ctx, x, y, p, seed, slot=None):
         x = x.contiguous()
         y = y.contiguous()
         _chk(x, "layerdrop.x")
@@ -1758,7 +1797,7 @@ class _LayerDropSelect(torch.autograd.Function):
         x16, y16 = (_b16_of(x), _b16_of(y)) if out16 is not None else (None, None)
         _lib.call("b2p_layerdrop_select", _p(x), _p(y), _p(out), _p(x16), _p(y16), _p(out16), y.numel(), float(p),
                   seed, _st())
-        ctx.p, ctx.seed = p, seed
+        ctx.p, ctx.seed, ctx.slot = p, seed, slot
         if out16 is not None:
             attach16(out, out16)
         return out
@@ -1769,7 +1808,10 @@ class _LayerDropSelect(torch.autograd.Function):
         d_keep = torch.empty_like(dout)
         d_skip = torch.empty_like(dout)
         _lib.call("b2p_layerdrop_route", _p(dout), _p(d_keep), _p(d_skip), dout.numel(), float(ctx.p), ctx.seed, _st())
-        return d_skip, d_keep, None, None
+        if ctx.slot is not None:   # folded into the layer's input gradient (_SkipSlot)
+            ctx.slot.grad = d_skip
+            return None, d_keep, None, None, None
+        return d_skip, d_keep, None, None, None
 
 
 LAYERDROP_LOG = None   # tests: when a list, layerdrop_layer appends each layer's draw seed
@@ -1818,16 +1860,24 @@ def layerdrop_layer(layer, x, p):
     _lib.call("b2p_layerdrop_flag", _p(flag), float(p), seed, _st())
     for prm in layer.parameters():
         _LD_PARAM_GATE[id(prm)] = (weakref.ref(prm), flag)
-    if LAYERDROP_GATE:
-        # the layer's GEMMs and fused attention (forward, backward, deferred weight gradients) read
-        # this replay's draw and do no work when it skips the layer; the select below still routes
-        with _gated(flag):
+    slot = None
+    if _LD_SKIP_FOLD and LAYERDROP_GATE and x.requires_grad and x.is_contiguous():
+        slot = _SkipSlot()
+        _SKIP_CLAIM[x.data_ptr()] = slot
+    try:
+        if LAYERDROP_GATE:
+            # the layer's GEMMs and fused attention (forward, backward, deferred weight gradients) read
+            # this replay's draw and do no work when it skips the layer; the select below still routes
+            with _gated(flag):
+                y = layer(x)
+        else:
             y = layer(x)
-    else:
-        y = layer(x)
+    finally:
+        if slot is not None:
+            _SKIP_CLAIM.pop(x.data_ptr(), None)
     for b, o in zip(bufs, olds):
         _lib.call("b2p_layerdrop_select", _p(o), _p(b), _p(b), None, None, None, b.numel(), float(p), seed, _st())
-    return _LayerDropSelect.apply(x, y, float(p), seed)
+    return _LayerDropSelect.apply(x, y, float(p), seed, slot if slot is not None and slot.claimed else None)
 
 
 def layerdrop_keep(p, seed, epoch=None) -> bool:
@@ -2078,6 +2128,7 @@ def _attn16_bwd(qkv16, dO16, lse2, B, T, nh, dh, p_attn, seed, want32=True, mask
 class _EncoderLayer(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, cfg, wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
+        ctx.skip = _skip_claim(x)   # LayerDrop skip gradient folded into dx (_SkipSlot)
         nh, eps, p_attn, p_hid, p_act, seeds = cfg
         _chk(x, "encoder_layer.x")
         B, T, D = x.shape
@@ -2146,7 +2197,8 @@ class _EncoderLayer(torch.autograd.Function):
         del dpre
         # LN1 backward -> dy1 ; dz1 = dropout-mask(dy1) (attention output dropout)
         dbo = torch.empty(D, device=dev) if ng[9] else None
-        dy1, dg1, dbe1, dz1 = _ln_bwd(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1], dbias_in=dbo)
+        dy1, dg1, dbe1, dz1 = _ln_bwd(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1], dbias_in=dbo,
+                                       dx_accum2=_skip_take(ctx.skip))
         dwo = torch.empty_like(wo) if ng[8] else None
         if dwo is not None:
             mm_tn(dz1, O, dwo)
@@ -2182,6 +2234,7 @@ class _EncoderLayer16(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, cfg, wq, bq, wk, bk, wv, bv, wo, bo, g1, be1, w1, b1, w2, b2, g2, be2):
+        ctx.skip = _skip_claim(x)   # LayerDrop skip gradient folded into dx (_SkipSlot)
         nh, eps, p_attn, p_hid, p_act, seeds = cfg
         _chk(x, "encoder_layer.x")
         B, T, D = x.shape
@@ -2336,7 +2389,7 @@ class _EncoderLayer16(torch.autograd.Function):
         # LN1 backward -> dy1 ; dz1 = dropout-mask(dy1) (attention output dropout)
         dbo = torch.empty(D, device=dev) if ng[9] else None
         dy1, dg1, dbe1, _dz1, dz1_16 = _ln_bwd16(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1],
-                                                 dbias_in=dbo)
+                                                 dbias_in=dbo, dx_accum2=_skip_take(ctx.skip))
         del _dz1
         dwo = None
         if ng[8]:
@@ -2617,6 +2670,7 @@ class _FFNBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, g, b, w1, b1, w2, b2, cfg):
+        ctx.skip = _skip_claim(x)   # LayerDrop skip gradient folded into dx (_SkipSlot)
         act, eps, p_act, p_hid, s_act, s_hid, scale = cfg
         _chk(x, "ffn.x")
         B, T, D = x.shape
@@ -2697,7 +2751,7 @@ class _FFNBlock(torch.autograd.Function):
             colsum(dpre, NT, F, db1)
         dh = torch.empty(NT, D, device=dev)
         mm_nn(dpre, w1, dh)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip))
         return (dx.view(ctx.shape), *_defer_small(ctx.prm, (dg, db, dw1, db1, dw2, db2)), None)
 
     @staticmethod
@@ -2726,7 +2780,7 @@ class _FFNBlock(torch.autograd.Function):
         dw1 = _wgrad16(w1, ng[3], dpre16, F, h if h.dtype == BF16 else cast16(h), D, NT)
         dh = torch.empty(NT, D, device=dev)
         gemm(NT, D, F, op(dpre16, 0, F, True), op(weight16t(w1), 0, F, True), dh, D)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip))
         return (dx.view(ctx.shape), *_defer_small(ctx.prm, (dg, db, dw1, db1, dw2, db2)), None)
 
 
@@ -2771,6 +2825,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, g, b, wq, bq, wk, bk, wv, bv, wo, bo, cos_t, sin_t, cfg):
+        ctx.skip = _skip_claim(x)   # LayerDrop skip gradient folded into dx (_SkipSlot)
         nh, eps, p_attn, p_out, seeds = cfg
         _chk(x, "conformer_attn.x")
         B, T, D = x.shape
@@ -2885,7 +2940,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
         else:
             for i, w in enumerate((wq, wk, wv)):
                 gemm(NT, D, D, op(dqkv, i * D, 3 * D, True), op(w, 0, D, False), dh, D, beta=0.0 if i == 0 else 1.0)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip))
         return (dx.view(B, T, D), *_defer_small(ctx.prm, (dg, db, *grads, dwo, dbo)), None, None, None)
 
     @staticmethod
@@ -2943,7 +2998,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
             gemm(NT, D, D, op(dqkv16, 2 * D, 3 * D, True), op(weight16t(wv), 0, D, True), dh, D, beta=1.0)
         else:
             gemm(NT, D, 3 * D, op(dqkv16, 0, 3 * D, True), op(weight16t(wq, wk, wv), 0, 3 * D, True), dh, D)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip))
         return (dx.view(B, T, D), *_defer_small(ctx.prm, (dg, db, *grads, dwo, dbo)), None, None, None)
 
 
