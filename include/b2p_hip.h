@@ -543,6 +543,16 @@ int b2p_layernorm_fwd_x16(const float* x, const float* gamma, const float* beta,
 /* Forward rotary embedding (as b2p_rotary, inverse 0) written as a 16-bit operand (fp16 when fp16). */
 int b2p_rotary16(const float* x, const float* cos_t, const float* sin_t, uint16_t* out, int fp16, int64_t B, int64_t T,
                  int64_t H, int64_t D, int64_t ld, b2p_stream_t stream);
+/* LayerNorm + rotary embedding in one pass for the Conformer attention block (TF conf
+ * Wav2Vec2ConformerSelfAttention with position_embeddings_type="rotary": query and key read the rotated
+ * LN output, value the plain one). 16-bit outputs only, each optional (NULL skips it): h16 / hr16 the
+ * forward operands (fp16 when half16, else bf16), h16b / hr16b bf16 copies for the weight gradients.
+ * Equal bit for bit to b2p_layernorm_fwd_x16 followed by b2p_rotary16 of the fp32 output.
+ * cols % 256 == 0, cols <= 1024, head_dim in {32, 64, 128, 256}, rows = B * T. */
+int b2p_layernorm_rotary16(const float* x, const float* gamma, const float* beta, float* mean, float* rstd,
+                           int64_t rows, int64_t cols, float eps, int64_t T, int64_t head_dim, const float* cos_t,
+                           const float* sin_t, int half16, uint16_t* h16, uint16_t* h16b, uint16_t* hr16,
+                           uint16_t* hr16b, b2p_stream_t stream);
 /* out = bf16(dropout(act(pre))) with the mask of a GEMM epilogue over the same flat index (n % 4 == 0):
  * recomputes a Conformer FFN intermediate (TF conf Wav2Vec2ConformerFeedForward) for its weight
  * gradient. */

@@ -916,6 +916,32 @@ def test_conformer_16bit_producers():
     assert torch.equal(c16, c32.half())
 
 
+@pytest.mark.parametrize("B,T,D,dh", [(3, 100, 256, 64), (2, 249, 1024, 64), (1, 37, 512, 32), (2, 50, 256, 128),
+                                      (1, 5, 256, 256)])
+def test_layernorm_rotary_one_pass_bitwise(B, T, D, dh):
+    """b2p_layernorm_rotary16 (LayerNorm + rotary, 16-bit outputs only) equals the two-launch form it
+    replaces in the Conformer attention block -- LayerNorm with an fp32 output, then b2p_rotary16 of that
+    output -- bit for bit, for the plain and rotated operands in fp16 and bf16, and its mean / rstd equal
+    the LayerNorm kernel's."""
+    Fn = _fn()
+    torch.manual_seed(5)
+    nh = D // dh
+    x = 2 * torch.randn(B * T, D, device="cuda") + 0.3
+    g, b = 1 + 0.1 * torch.randn(D, device="cuda"), 0.1 * torch.randn(D, device="cuda")
+    cos_t, sin_t = Fn.rotary_tables(T, dh, 10000, "cuda")
+    assert Fn.ln_rotary16_ok(D, dh)
+    for half in (True, False):
+        y, y16, mean, rstd, y16b = Fn._ln_fwd_x16(x, g, b, 1e-5, half, want_b16=True)
+        r16 = Fn._rotary16(y, cos_t, sin_t, B, T, nh, dh, half)
+        r16b = Fn._rotary16(y, cos_t, sin_t, B, T, nh, dh, False)
+        h16, h16b, hr16, hr16b, m2, s2 = Fn._ln_rotary16(x, g, b, 1e-5, T, dh, cos_t, sin_t, half)
+        torch.cuda.synchronize()
+        assert h16.dtype == (torch.float16 if half else torch.bfloat16) and hr16b.dtype == torch.bfloat16
+        assert torch.equal(m2, mean) and torch.equal(s2, rstd)
+        assert torch.equal(h16, y16) and torch.equal(hr16, r16)
+        assert torch.equal(h16b, y16b) and torch.equal(hr16b, r16b)
+
+
 @pytest.mark.parametrize("act", [3, 1])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("NT,D,F", [(300, 128, 512), (7968, 1024, 4096)])

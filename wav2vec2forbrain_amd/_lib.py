@@ -150,6 +150,8 @@ _SIGS = {
     "b2p_layernorm_fwd_x16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_p]),
     "b2p_glu_bwd16": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_p]),
     "b2p_rotary16": (c_i32, [c_p, c_p, c_p, c_p, c_i32, c_i64, c_i64, c_i64, c_i64, c_i64, c_p]),
+    "b2p_layernorm_rotary16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_i64, c_i64, c_p, c_p, c_i32,
+                                       c_p, c_p, c_p, c_p, c_p]),
     "b2p_act_dropout_cast16": (c_i32, [c_p, c_p, c_i64, c_i32, c_f32, c_u64, c_p]),
     "b2p_rotary": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_glu_fwd": (c_i32, [c_p, c_p, c_i64, c_i64, c_p]),

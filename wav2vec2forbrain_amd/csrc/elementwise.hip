@@ -480,6 +480,85 @@ __global__ void __launch_bounds__(256) ln_fwd_k(const float* __restrict__ x, con
   }
 }
 
+// LayerNorm + rotary embedding in one pass (the Conformer attention block's input: Q/K read the rotated
+// LN output, V the plain one), 16-bit outputs only: h16 / hr16 (the forward GEMM operands, fp16 when
+// half) and h16b / hr16b (bf16 copies, the backward's weight-gradient operands; a null pointer skips a
+// copy). Lane l holds float4 c = l + 64 i; within a head of HD columns the rotate-half partner of
+// columns 4c .. 4c+3 is float4 c ^ (HD / 8), i.e. lane l ^ (HD / 8) of the same i (HD / 4 divides 64).
+// The LayerNorm and rotation arithmetic is that of ln_fwd_k and rotary16_k (conformer.hip), so the
+// outputs equal LN -> fp32 -> rotary16 bit for bit. TF conf Wav2Vec2ConformerRotaryPositionalEmbedding
+// / Wav2Vec2ConformerSelfAttention (rotary on the LN output for query and key only).
+template <int HD>
+__global__ void __launch_bounds__(256) ln_rot16_k(const float* __restrict__ x, const float* __restrict__ gamma,
+                                                  const float* __restrict__ beta, float* __restrict__ mean,
+                                                  float* __restrict__ rstd, int64_t rows, int cols, float eps, int T,
+                                                  const float* __restrict__ ct, const float* __restrict__ st,
+                                                  int half16, uint16_t* __restrict__ h16, uint16_t* __restrict__ h16b,
+                                                  uint16_t* __restrict__ hr16, uint16_t* __restrict__ hr16b) {
+  static_assert(HD % 8 == 0 && 64 % (HD / 4) == 0, "head dim: the partner float4 must sit in the same wave row");
+  const int lane = threadIdx.x & 63;
+  const int64_t row = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;   // wave-uniform: the shuffles below see whole waves only
+  const int nv = cols >> 2;
+  const float4* xr = reinterpret_cast<const float4*>(x + row * cols);
+  float4 v[LN_MAXV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) { v[i] = xr[c]; s += v[i].x + v[i].y + v[i].z + v[i].w; }
+  }
+  const float mu = warp_sum(s) / cols;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nv) {
+      const float a = v[i].x - mu, b = v[i].y - mu, cc = v[i].z - mu, d = v[i].w - mu;
+      q += a * a + b * b + cc * cc + d * d;
+    }
+  }
+  const float var = warp_sum(q) / cols;
+  const float rs = rsqrtf(var + eps);
+  if (lane == 0) { mean[row] = mu; rstd[row] = rs; }
+  const float4* g4 = reinterpret_cast<const float4*>(gamma);
+  const float4* b4 = reinterpret_cast<const float4*>(beta);
+  const int t = (int)(row % T);
+  const int d = (4 * lane) % HD;           // head-local column of this lane's float4 (same for every i)
+  const float sg = d < HD / 2 ? -1.f : 1.f;
+  const float4 cs = *reinterpret_cast<const float4*>(ct + (int64_t)t * HD + d);
+  const float4 sn = *reinterpret_cast<const float4*>(st + (int64_t)t * HD + d);
+#pragma unroll
+  for (int i = 0; i < LN_MAXV; ++i) {
+    const int c = lane + 64 * i;
+    if (64 * i < nv) {   // uniform over the wave (nv % 64 == 0 is checked on the host): shuffles stay whole
+      float4 o = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c < nv) {
+        const float4 g = g4[c], bb = b4[c];
+        o.x = (v[i].x - mu) * rs * g.x + bb.x;
+        o.y = (v[i].y - mu) * rs * g.y + bb.y;
+        o.z = (v[i].z - mu) * rs * g.z + bb.z;
+        o.w = (v[i].w - mu) * rs * g.w + bb.w;
+      }
+      float4 ov;
+      ov.x = __shfl_xor(o.x, HD / 8);
+      ov.y = __shfl_xor(o.y, HD / 8);
+      ov.z = __shfl_xor(o.z, HD / 8);
+      ov.w = __shfl_xor(o.w, HD / 8);
+      float4 r;
+      r.x = o.x * cs.x + sg * ov.x * sn.x;
+      r.y = o.y * cs.y + sg * ov.y * sn.y;
+      r.z = o.z * cs.z + sg * ov.z * sn.z;
+      r.w = o.w * cs.w + sg * ov.w * sn.w;
+      const int64_t off = row * cols;
+      if (h16) reinterpret_cast<uint2*>(h16 + off)[c] = b2p_pack16x4(o, half16);
+      if (h16b) reinterpret_cast<uint2*>(h16b + off)[c] = b2p_pack_bf16x4(o);
+      if (hr16) reinterpret_cast<uint2*>(hr16 + off)[c] = b2p_pack16x4(r, half16);
+      if (hr16b) reinterpret_cast<uint2*>(hr16b + off)[c] = b2p_pack_bf16x4(r);
+    }
+  }
+}
+
 constexpr int LN_BWD_ROWS = 16;   // rows per block (4 per wave): ~500 blocks at 8k rows
 // PF: prefetch the next row (B2P_LN_PREFETCH, default 1). MODE bits: 1 = dx_accum, 2 = dx_accum2, 4 = dxd
 // (compile-time, so a form holds registers only for the streams it reads: all three at once would not
@@ -959,6 +1038,37 @@ extern "C" int b2p_layernorm_fwd_x16(const float* x, const float* gamma, const f
   hipLaunchKernelGGL(ln_fwd_k, dim3(nblocks(rows, 4)), dim3(256), 0, (hipStream_t)stream, x, gamma, beta, y,
                      mean, rstd, rows, (int)cols, eps, 0u, 1.f, (uint64_t)0, 0.f, y16, b2p_seed_epoch(),
                      y16_fp16 ? 1 : 0, y16b);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_layernorm_rotary16(const float* x, const float* gamma, const float* beta, float* mean, float* rstd,
+                                      int64_t rows, int64_t cols, float eps, int64_t T, int64_t head_dim,
+                                      const float* cos_t, const float* sin_t, int half16, uint16_t* h16,
+                                      uint16_t* h16b, uint16_t* hr16, uint16_t* hr16b, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && gamma && beta && mean && rstd && cos_t && sin_t, "layernorm_rotary16: NULL pointer");
+  B2P_CHECK_ARG(cols % 256 == 0 && cols <= 64 * 4 * LN_MAXV && cols % head_dim == 0,
+                "layernorm_rotary16: cols must be a multiple of 256 (<= 1024) and of the head dim");
+  B2P_CHECK_ARG(head_dim == 32 || head_dim == 64 || head_dim == 128 || head_dim == 256,
+                "layernorm_rotary16: head dim must be 32, 64, 128 or 256");
+  B2P_CHECK_ARG(T > 0 && rows % T == 0, "layernorm_rotary16: rows must be whole sequences of T");
+  B2P_CHECK_ARG(((uintptr_t)x & 15u) == 0 && ((uintptr_t)cos_t & 15u) == 0 && ((uintptr_t)sin_t & 15u) == 0 &&
+                    ((uintptr_t)h16 & 7u) == 0 && ((uintptr_t)h16b & 7u) == 0 && ((uintptr_t)hr16 & 7u) == 0 &&
+                    ((uintptr_t)hr16b & 7u) == 0,
+                "layernorm_rotary16: x / cos / sin 16-B and outputs 8-B aligned");
+  if (rows <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const dim3 grid(nblocks(rows, 4));
+#define B2P_LNROT(HD)                                                                                            \
+  hipLaunchKernelGGL(ln_rot16_k<HD>, grid, dim3(256), 0, st, x, gamma, beta, mean, rstd, rows, (int)cols, eps, \
+                     (int)T, cos_t, sin_t, half16 ? 1 : 0, h16, h16b, hr16, hr16b)
+  switch (head_dim) {
+    case 32: B2P_LNROT(32); break;
+    case 64: B2P_LNROT(64); break;
+    case 128: B2P_LNROT(128); break;
+    default: B2P_LNROT(256); break;
+  }
+#undef B2P_LNROT
   B2P_CHECK_LAUNCH();
   return 0;
 }

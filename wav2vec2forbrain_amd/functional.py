@@ -2635,6 +2635,33 @@ def _ln_fwd_x16(x2d, g, b, eps, half, want32=True, want_b16=False):
     return y, y16, mean, rstd
 
 
+# Conformer attention block: LayerNorm + rotary in one launch (B2P_LN_ROT=0: LayerNorm with an fp32
+# output, then b2p_rotary16 in the forward and again in the backward)
+_LN_ROT = [os.environ.get("B2P_LN_ROT", "1") != "0"]
+
+
+def ln_rotary16_ok(D, hd) -> bool:
+    return D % 256 == 0 and D <= 1024 and hd in (32, 64, 128, 256) and D % hd == 0
+
+
+def _ln_rotary16(x2d, g, b, eps, T, hd, cos_t, sin_t, half):
+    """(h16, h16b, hr16, hr16b, mean, rstd): LayerNorm of x2d and its rotary rotation as 16-bit operands
+    (fp16 h16 / hr16 under half, with bf16 copies h16b / hr16b; in bf16 the copies are h16 / hr16)."""
+    rows, cols = x2d.shape
+    dt = torch.float16 if half else BF16
+    dev = x2d.device
+    h16 = torch.empty(rows, cols, device=dev, dtype=dt)
+    hr16 = torch.empty(rows, cols, device=dev, dtype=dt)
+    h16b = torch.empty(rows, cols, device=dev, dtype=BF16) if half else h16
+    hr16b = torch.empty(rows, cols, device=dev, dtype=BF16) if half else hr16
+    mean = torch.empty(rows, device=dev)
+    rstd = torch.empty(rows, device=dev)
+    _lib.call("b2p_layernorm_rotary16", _p(x2d), _p(g), _p(b), _p(mean), _p(rstd), rows, cols, float(eps), T, hd,
+              _p(cos_t), _p(sin_t), int(half), _p(h16), _p(h16b) if half else None, _p(hr16),
+              _p(hr16b) if half else None, _st())
+    return h16, h16b, hr16, hr16b, mean, rstd
+
+
 def _rotary16(h, cos_t, sin_t, B, T, nh, hd, half):
     out = torch.empty(h.shape, device=h.device, dtype=torch.float16 if half else BF16)
     _lib.call("b2p_rotary16", _p(h), _p(cos_t), _p(sin_t), _p(out), int(half), B, T, nh, hd, h.shape[-1], _st())
@@ -2844,12 +2871,19 @@ class _ConformerAttnBlock(torch.autograd.Function):
             # the Q/K/V operands come straight from their producers as 16-bit copies (LayerNorm, rotary):
             # fp16 under forward_f16, else bf16; the fp32 rotated copy is never stored
             half = _state.fwd16
-            if half:   # fp16 operand for the forward GEMMs, bf16 copy for the V weight gradient
+            hr16b = None
+            if cos_t is not None and _LN_ROT[0] and _bwd16_path() and ln_rotary16_ok(D, hd):
+                # LayerNorm + rotary in one pass, 16-bit outputs only (no fp32 LN output, no rotary
+                # launches): the backward keeps the bf16 rotated copy for the Q/K weight gradients
+                h16, h16b, hr16, hr16b, mean, rstd = _ln_rotary16(x2, g, b, eps, T, hd, cos_t, sin_t, half)
+                h = None
+            elif half:   # fp16 operand for the forward GEMMs, bf16 copy for the V weight gradient
                 h, h16, mean, rstd, h16b = _ln_fwd_x16(x2, g, b, eps, half, want_b16=True)
             else:
                 h, h16, mean, rstd = _ln_fwd_x16(x2, g, b, eps, half)
                 h16b = h16
-            hr16 = _rotary16(h, cos_t, sin_t, B, T, nh, hd, half) if cos_t is not None else h16
+            if h is not None:
+                hr16 = _rotary16(h, cos_t, sin_t, B, T, nh, hd, half) if cos_t is not None else h16
             hr = None
             for i, (w, bb, src) in enumerate(((wq, bq, hr16), (wk, bk, hr16), (wv, bv, h16))):
                 wbuf, wop = _w_op16(w, half)
@@ -2863,7 +2897,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
                 del wbuf
             del h16, hr16
         else:
-            h16b = None
+            h16b = hr16b = None
             h, mean, rstd = _ln_fwd(x2, g, b, eps)
             if cos_t is not None:
                 hr = torch.empty_like(h)
@@ -2887,7 +2921,7 @@ class _ConformerAttnBlock(torch.autograd.Function):
             gemm(NT, D, D, op(O, 0, D, True), op(wo, 0, D, True), y, D, bias=bo, drop_p=p_out, seed=seeds[1],
                  residual=x2)
         ctx.save_for_backward(x2, h, hr if (cos_t is not None and hr is not None) else None, mean, rstd, qkv, P, Pd,
-                              O, g, wq, wk, wv, wo, cos_t, sin_t, h16b)
+                              O, g, wq, wk, wv, wo, cos_t, sin_t, h16b, hr16b)
         ctx.cfg = cfg
         ctx.shape = (B, T, D)
         ctx.has_b = [t is not None for t in (bq, bk, bv, bo)]
@@ -2896,8 +2930,9 @@ class _ConformerAttnBlock(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo, cos_t, sin_t, h16b = ctx.saved_tensors
+        x2, h, hr, mean, rstd, qkv, P, Pd, O, g, wq, wk, wv, wo, cos_t, sin_t, h16b, hr16b = ctx.saved_tensors
         ctx.h16b = h16b
+        ctx.hr16b = hr16b
         nh, eps, p_attn, p_out, seeds = ctx.cfg
         B, T, D = ctx.shape
         NT, hd = B * T, D // nh
@@ -2970,6 +3005,8 @@ class _ConformerAttnBlock(torch.autograd.Function):
         h16 = ctx.h16b if ctx.h16b is not None else cast16(h)
         if cos_t is None:
             hr16 = h16
+        elif ctx.hr16b is not None:   # LayerNorm + rotary forward: its bf16 rotated copy
+            hr16 = ctx.hr16b
         elif hr is None:   # the forward kept no fp32 rotated copy: rotate h again, into bf16
             hr16 = _rotary16(h, cos_t, sin_t, B, T, nh, hd, False)
         else:
