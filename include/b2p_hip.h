@@ -523,6 +523,9 @@ int b2p_accum_recs(const int64_t* recs, int ntensors, b2p_stream_t stream);
 int b2p_accum_rows_recs(const int64_t* recs, int ntensors, b2p_stream_t stream);
 
 /* dropout with an extra output scale: y = x * keep(seed, i) * scale / (1-p) (macaron half-step) */
+/* y = x * (*s) with the scalar s read on the device (16-B aligned x, y): the CTC loss backward's
+ * grad * grad_output (torch.autograd seeds a reduced loss with a device scalar). */
+int b2p_scale_by_device_scalar(const float* x, const float* s, float* y, int64_t n, b2p_stream_t stream);
 int b2p_dropout_scaled(const float* x, float* y, int64_t n, float p, uint64_t seed, float scale,
                        b2p_stream_t stream);
 /* Output-dropout backward of a Conformer block in one pass (replaces b2p_dropout_scaled + a bf16
@@ -584,6 +587,11 @@ int b2p_dwconv_bwd(const float* x, const float* w, const float* dy, float* dx, f
  * biased variance), updates running stats (momentum, unbiased variance), applies gamma/beta and the
  * fused activation act (B2P_ACT_SILU = swish). pre (optional) keeps the pre-activation. */
 int64_t b2p_batchnorm_workspace(int64_t M, int64_t C);
+/* num_batches_tracked (int64, device) of the next training-mode statistics launch on this host thread
+ * (b2p_batchnorm_fwd, or b2p_batchnorm_finalize phase 1): that launch adds 1 to it on the device,
+ * unless the LayerDrop gate (b2p_set_gate) is closed -- torch _BatchNorm.forward's
+ * num_batches_tracked.add_(1) without a separate launch. NULL clears it. */
+int b2p_batchnorm_count_next(int64_t* num_batches_tracked);
 int b2p_batchnorm_fwd(const float* x, const float* gamma, const float* beta, float* running_mean,
                       float* running_var, float* y, float* pre, float* mean, float* rstd, int64_t M,
                       int64_t C, float eps, float momentum, int act, float* workspace,

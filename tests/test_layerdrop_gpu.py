@@ -84,6 +84,7 @@ def test_captured_layerdrop_redraws_per_replay(name):
             patterns.append(tuple(Fn.layerdrop_keep(P_LD, s, ep) for s in seeds))
         grads_g = {n: p.grad.detach().clone() for n, p in model.named_parameters() if p.grad is not None}
         bufs_g = {n: b.detach().clone() for n, b in model.named_buffers() if b.is_floating_point()}
+        counts_g = {n: int(b) for n, b in model.named_buffers() if n.endswith("num_batches_tracked")}
         sg.release()
     torch.cuda.synchronize()
     # the draw changes between replays (with p = 0.5 over REPLAYS replays)
@@ -119,6 +120,10 @@ def test_captured_layerdrop_redraws_per_replay(name):
     for n, b in bufs_g.items():   # BatchNorm running statistics: updated only by kept layers
         e = dict(ref.named_buffers())[n]
         assert float((b - e).norm()) <= 1e-5 * float(e.norm()) + 1e-7, n
+    # num_batches_tracked counts the replays that kept the layer (torch _BatchNorm.forward runs only then)
+    counts_e = {n: int(b) for n, b in ref.named_buffers() if n.endswith("num_batches_tracked")}
+    assert counts_g == counts_e and (not counts_g or len(set(counts_g.values())) > 1 or
+                                     0 < min(counts_g.values()) < REPLAYS), (counts_g, counts_e)
 
 
 @pytest.mark.parametrize("name", ["tiny_a", "tiny_conf"])

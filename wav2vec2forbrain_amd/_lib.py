@@ -144,6 +144,7 @@ _SIGS = {
     "b2p_posconv16_bwd_data": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_posconv16_wgrad": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_seed_epoch_step": (c_i32, [c_p, c_p]),
+    "b2p_scale_by_device_scalar": (c_i32, [c_p, c_p, c_p, c_i64, c_p]),
     "b2p_dropout_scaled": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_f32, c_p]),
     "b2p_drop_cast_colsum_parts": (c_i64, [c_i64]),
     "b2p_drop_cast_colsum": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_f32, c_u64, c_f32, c_p]),
@@ -165,6 +166,7 @@ _SIGS = {
     "b2p_batchnorm_eval": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_i32, c_p, c_p]),
     "b2p_batchnorm_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p]),
     "b2p_batchnorm_stats": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_p, c_p]),
+    "b2p_batchnorm_count_next": (c_i32, [c_p]),
     "b2p_batchnorm_finalize": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_i32, c_p]),
     "b2p_batchnorm_apply": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p]),
     "b2p_batchnorm_bwd_sums": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p]),

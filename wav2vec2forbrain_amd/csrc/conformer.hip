@@ -313,7 +313,8 @@ __global__ void dw_transpose_k(const float* __restrict__ kc, float* __restrict__
 // ---- BatchNorm1d (training statistics over M rows, per channel)
 __global__ void bn_finalize_k(const float* __restrict__ sum, const float* __restrict__ sqdev, const float* __restrict__ mean,
                               float* __restrict__ rstd, float* __restrict__ run_mean, float* __restrict__ run_var,
-                              int64_t C, int64_t count, float eps, float momentum, const int32_t* __restrict__ gate) {
+                              int64_t C, int64_t count, float eps, float momentum, const int32_t* __restrict__ gate,
+                              int64_t* __restrict__ nbt = nullptr) {
   const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
   const float mu = mean[c];
@@ -322,6 +323,7 @@ __global__ void bn_finalize_k(const float* __restrict__ sum, const float* __rest
   // LayerDrop: a replay that skips this layer leaves the running statistics untouched (the reference
   // never runs the layer), so the captured step needs no snapshot / restore of them
   if (b2p_gated_off(gate)) return;
+  if (nbt && c == 0) *nbt += 1;   // BatchNorm's num_batches_tracked (torch _BatchNorm.forward, training)
   if (run_mean) run_mean[c] = (1.f - momentum) * run_mean[c] + momentum * mu;
   if (run_var) {
     const float unb = count > 1 ? sqdev[c] / (float)(count - 1) : var;
@@ -648,10 +650,27 @@ static void bn_bwd_dx_launch(const float* g, const float* x, const float* mean, 
                        C, count);
 }
 
+namespace {
+// num_batches_tracked of the next training BatchNorm's statistics launch (b2p_batchnorm_count_next),
+// incremented by bn_finalize_k under the LayerDrop gate; consumed by that launch
+thread_local int64_t* g_bn_counter = nullptr;
+int64_t* take_bn_counter() {
+  int64_t* p = g_bn_counter;
+  g_bn_counter = nullptr;
+  return p;
+}
+}  // namespace
+
+extern "C" int b2p_batchnorm_count_next(int64_t* num_batches_tracked) {
+  g_bn_counter = num_batches_tracked;
+  return 0;
+}
+
 extern "C" int b2p_batchnorm_fwd(const float* x, const float* gamma, const float* beta, float* running_mean,
                                  float* running_var, float* y, float* pre, float* mean, float* rstd, int64_t M,
                                  int64_t C, float eps, float momentum, int act, float* workspace,
                                  b2p_stream_t stream) {
+  int64_t* nbt = take_bn_counter();
   B2P_CHECK_ARG(x && gamma && beta && y && mean && rstd && workspace, "batchnorm_fwd: NULL");
   hipStream_t st = (hipStream_t)stream;
   if (M <= 0) return 0;
@@ -662,7 +681,7 @@ extern "C" int b2p_batchnorm_fwd(const float* x, const float* gamma, const float
   hipLaunchKernelGGL(scale_k, dim3(nblk(C)), dim3(256), 0, st, mean, C, 1.f / (float)M);
   if (colsum_impl(x, mean, 1, M, C, C, 0, 3, sqdev, 0, part, st)) return 1;
   hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sqdev, mean, rstd,
-                     running_mean, running_var, C, M, eps, momentum, b2p_gate());
+                     running_mean, running_var, C, M, eps, momentum, b2p_gate(), nbt);
   bn_apply_launch(x, mean, rstd, gamma, beta, y, pre, M, C, act, st);
   B2P_CHECK_LAUNCH();
   return 0;
@@ -714,6 +733,7 @@ extern "C" int b2p_batchnorm_stats(const float* x, const float* center, float* o
 extern "C" int b2p_batchnorm_finalize(float* sum_or_mean, const float* sqdev, float* rstd, float* running_mean,
                                       float* running_var, int64_t C, int64_t count, float eps, float momentum,
                                       int phase, b2p_stream_t stream) {
+  int64_t* nbt = phase == 1 ? take_bn_counter() : nullptr;
   B2P_CHECK_ARG(sum_or_mean && count > 0, "batchnorm_finalize: bad arguments");
   hipStream_t st = (hipStream_t)stream;
   if (C <= 0) return 0;
@@ -723,7 +743,7 @@ extern "C" int b2p_batchnorm_finalize(float* sum_or_mean, const float* sqdev, fl
     B2P_CHECK_ARG(sqdev && rstd, "batchnorm_finalize: phase 1 needs sqdev and rstd");
     hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sqdev,
                        (const float*)sum_or_mean, rstd, running_mean, running_var, C, count, eps, momentum,
-                       b2p_gate());
+                       b2p_gate(), nbt);
   }
   B2P_CHECK_LAUNCH();
   return 0;

@@ -406,6 +406,22 @@ extern "C" int b2p_colsum_parts(const float* part, int64_t ntiles, int64_t N, fl
 
 namespace {
 
+// y = x * (*s): a gradient scaled by the incoming scalar gradient of a reduced loss, read on the device
+// (the CTC loss backward: d loss_total / d logits = grad * d loss_total / d loss)
+__global__ void scale_dev_k(const float4* __restrict__ x, const float* __restrict__ s, float4* __restrict__ y,
+                            int64_t n4) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const float c = *s;
+  const float4 v = x[i];
+  y[i] = make_float4(v.x * c, v.y * c, v.z * c, v.w * c);
+}
+__global__ void scale_dev_tail_k(const float* __restrict__ x, const float* __restrict__ s, float* __restrict__ y,
+                                 int64_t n0, int64_t n) {
+  const int64_t i = n0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = x[i] * *s;
+}
+
 // ------------------------------------------------------------------ dropout
 __global__ void dropout_k(const float* __restrict__ x, float* __restrict__ y, int64_t n, uint32_t thr,
                           float scale, uint64_t seed, const uint64_t* __restrict__ epoch) {
@@ -1001,6 +1017,19 @@ extern "C" int b2p_colsum_batched(const float* X, const float* Y, int64_t batch,
   B2P_CHECK_ARG(X && out && partial, "colsum_batched: NULL pointer");
   B2P_CHECK_ARG(mode != 2 || Y, "colsum_batched: mode 2 needs Y");
   return colsum_impl(X, Y, batch, M, N, ld, bstride, mode, out, accumulate, partial, (hipStream_t)stream);
+}
+
+extern "C" int b2p_scale_by_device_scalar(const float* x, const float* s, float* y, int64_t n, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && s && y, "scale_by_device_scalar: NULL pointer");
+  B2P_CHECK_ARG(((uintptr_t)x & 15u) == 0 && ((uintptr_t)y & 15u) == 0, "scale_by_device_scalar: x / y 16-B aligned");
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const int64_t n4 = n / 4;
+  if (n4) hipLaunchKernelGGL(scale_dev_k, dim3(nblocks(n4)), dim3(256), 0, st, reinterpret_cast<const float4*>(x), s,
+                             reinterpret_cast<float4*>(y), n4);
+  if (n > 4 * n4) hipLaunchKernelGGL(scale_dev_tail_k, dim3(1), dim3(256), 0, st, x, s, y, 4 * n4, n);
+  B2P_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int b2p_dropout(const float* x, float* y, int64_t n, float p, uint64_t seed, b2p_stream_t stream) {

@@ -1142,6 +1142,26 @@ def weight16(*ws, half=False):
     return out
 
 
+_BS: dict = {}
+
+
+def _scaled_bias(b, scale):
+    """b * scale (the macaron FFN's half-step output bias, TF conf EncoderLayer: x + 0.5 * ffn(x)), cached
+    like the 16-bit weight copies: a frozen bias costs no launch per step."""
+    if b is None:
+        return None
+    key = (id(b), float(scale))
+    st = _stamp((b,))
+    cache = _cache_ok((b,))
+    hit = _BS.get(key) if cache else None
+    if hit is not None and hit[0] == st:
+        return hit[1]
+    out = b * scale
+    if cache:
+        _BS[key] = (st, out)
+    return out
+
+
 def weight16t(*ws):
     """Transposed bf16 copy [C][sum R] of fp32 weights (R x C each, stacked along R): the
     k-contiguous B operand of a backward-data GEMM dX = dY W (NT kernel instead of the slower
@@ -2003,6 +2023,8 @@ def _posconv16_bwd(ctx, e16, wg, wv, w, norms, pre, dxsum, dlg, dlb):
         dg = torch.empty_like(wg)
         dv = torch.empty_like(wv)
         _lib.call("b2p_weight_norm_bwd", _p(wg), _p(wv), _p(norms), _p(dw), _p(dg), _p(dv), O, Ig, K, _p(ws), _st())
+    # frozen parameters' gradients join the batched side-stream accumulation (no autograd adds)
+    dg, dv, dcb, dlg, dlb = _defer_small(ctx.prm, (dg, dv, dcb, dlg, dlb))
     return (de if ng[0] else None), dg, dv, dcb, dlg, dlb, None, None, None, None
 
 
@@ -2477,7 +2499,11 @@ class _CTC(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         (grad,) = ctx.saved_tensors
-        return grad * gout, None, None, None, None
+        if gout.numel() != 1 or gout.dtype != torch.float32 or gout.device != grad.device:
+            return grad * gout, None, None, None, None
+        g = torch.empty_like(grad)
+        _lib.call("b2p_scale_by_device_scalar", _p(grad), _p(gout.contiguous()), _p(g), grad.numel(), _st())
+        return g, None, None, None, None
 
 
 def ctc_loss(logits, targets, in_lens, tgt_lens, blank=0):
@@ -2704,7 +2730,7 @@ class _FFNBlock(torch.autograd.Function):
         NT, F = B * T, w1.shape[0]
         dev = x.device
         x2 = x.view(NT, D)
-        bs = b2 * scale if b2 is not None else None
+        bs = _scaled_bias(b2, scale)
         y = torch.empty(NT, D, device=dev)
         if bf16_mode():
             # 16-bit operands written by their producers (LayerNorm, FFN1 epilogue): no cast passes;
@@ -3092,7 +3118,7 @@ class _ConvModule(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, g, b, w_pw1, w_dw, bn_g, bn_b, w_pw2, bn_rm, bn_rv, cfg):
-        act, eps, bn_eps, momentum, p, seed, training = cfg
+        act, eps, bn_eps, momentum, p, seed, training, nbt = cfg
         _chk(x, "conv_module.x")
         B, T, D = x.shape
         NT = B * T
@@ -3125,6 +3151,8 @@ class _ConvModule(torch.autograd.Function):
             bm = torch.empty(D, device=dev)
             br = torch.empty(D, device=dev)
             sync = _state.sync_bn
+            if nbt is not None:
+                _lib.call("b2p_batchnorm_count_next", _p(nbt))
             if sync is not None:
                 _bn_fwd_sync(c, bn_g, bn_b, bn_rm, bn_rv, s, pre, bm, br, NT, D, bn_eps, momentum, act, ws, sync)
             else:
@@ -3146,7 +3174,7 @@ class _ConvModule(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         x2, h, mean, rstd, a, u, c, pre, bm, br, s, g, w_pw1, w_dw, bn_g, w_pw2 = ctx.saved_tensors
-        act, eps, bn_eps, momentum, p, seed, training = ctx.cfg
+        act, eps, bn_eps, momentum, p, seed, training, _ = ctx.cfg
         if not training:
             raise RuntimeError("conv module backward in eval mode (running BN statistics) is not supported")
         B, T, D, K = ctx.shape
@@ -3226,10 +3254,11 @@ def conformer_conv_module(x, cm, act, p, training):
     bn = cm.batch_norm
     if not training:
         p = 0.0
+    # num_batches_tracked += 1 (torch _BatchNorm.forward in training) happens on the device, inside the
+    # statistics launch and under the LayerDrop gate (b2p_batchnorm_count_next)
+    nbt = bn.num_batches_tracked if training and bn.track_running_stats else None
     cfg = (act, float(cm.layer_norm.eps), float(bn.eps), float(bn.momentum if bn.momentum is not None else 0.1),
-           float(p), SEEDS.next() if p > 0 else 0, bool(training))
-    if training and bn.num_batches_tracked is not None:
-        bn.num_batches_tracked.add_(1)
+           float(p), SEEDS.next() if p > 0 else 0, bool(training), nbt)
     with _fp32_if("conv"):
         return _ConvModule.apply(x.contiguous(), cm.layer_norm.weight, cm.layer_norm.bias, cm.pointwise_conv1.weight,
                                  cm.depthwise_conv.weight, bn.weight, bn.bias, cm.pointwise_conv2.weight,
