@@ -98,7 +98,8 @@ def _build_locked(verbose: bool, jobs: int | None) -> str:
     if os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
         return LIB
     tmp = LIB + ".tmp"
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-L/opt/rocm/lib", "-lhipblaslt",
+           "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), file=sys.stderr, flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
