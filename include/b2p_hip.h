@@ -626,6 +626,17 @@ int b2p_batchnorm_finalize(float* sum_or_mean, const float* sqdev, float* rstd, 
 int b2p_batchnorm_apply(const float* x, const float* mean, const float* rstd, const float* gamma,
                         const float* beta, float* y, float* pre, int64_t M, int64_t C, int act,
                         b2p_stream_t stream);
+/* b2p_batchnorm_fwd / b2p_batchnorm_apply writing the activation output as 16-bit GEMM operands: y (fp32),
+ * y16 (fp16 when y16_fp16, else bf16) and y16b (bf16) are each optional, at least one is given (TF conf
+ * Wav2Vec2ConformerConvolutionModule: BN -> activation -> pointwise_conv2; the conv module keeps the
+ * fp16 forward operand and the bf16 weight-gradient operand only). C % 4 == 0, aligned pointers. */
+int b2p_batchnorm_fwd16(const float* x, const float* gamma, const float* beta, float* running_mean, float* running_var,
+                        float* y, uint16_t* y16, int y16_fp16, uint16_t* y16b, float* pre, float* mean, float* rstd,
+                        int64_t M, int64_t C, float eps, float momentum, int act, float* workspace,
+                        b2p_stream_t stream);
+int b2p_batchnorm_apply16(const float* x, const float* mean, const float* rstd, const float* gamma, const float* beta,
+                          float* y, uint16_t* y16, int y16_fp16, uint16_t* y16b, float* pre, int64_t M, int64_t C,
+                          int act, b2p_stream_t stream);
 int b2p_batchnorm_bwd_sums(const float* dy, const float* pre, const float* x, const float* mean,
                            const float* rstd, float* g, float* sum_g, float* sum_gx, int64_t M,
                            int64_t C, int act, float* workspace, b2p_stream_t stream);

@@ -1176,3 +1176,76 @@ def test_colsum_pinned_counters_survive_pool_wrap():
     lib.b2p_colsum_pool_state(-1, ctypes.byref(res))
     assert res.value == reserved0, (res.value, reserved0)
     del keep
+
+
+def test_batchnorm_16bit_outputs_bitwise():
+    """b2p_batchnorm_fwd16 / b2p_batchnorm_apply16 (the Conformer conv module's BatchNorm + activation
+    writing only the pointwise-conv-2 operands) against b2p_batchnorm_fwd / apply and a rounding of their
+    fp32 output: equal bits for the fp16 and bf16 copies, the same statistics and pre-activation."""
+    Fn = _fn()
+    from wav2vec2forbrain_amd import _lib
+    lib = _lib.load()
+    P, st = Fn._p, Fn._st()
+    torch.manual_seed(7)
+    M, C = 1000, 512
+    x = torch.randn(M, C, device="cuda") * 1.7 + 0.2
+    gamma, beta = torch.rand(C, device="cuda") + 0.5, torch.randn(C, device="cuda") * 0.1
+    ws = torch.empty(int(lib.b2p_batchnorm_workspace(M, C)), device="cuda")
+    outs = {}
+    for form in ("fp32", "16"):
+        rm, rv = torch.zeros(C, device="cuda"), torch.ones(C, device="cuda")
+        y = torch.empty(M, C, device="cuda")
+        y16 = torch.empty(M, C, device="cuda", dtype=torch.float16)
+        y16b = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+        pre, mean, rstd = torch.empty(M, C, device="cuda"), torch.empty(C, device="cuda"), torch.empty(C, device="cuda")
+        if form == "fp32":
+            _lib.call("b2p_batchnorm_fwd", P(x), P(gamma), P(beta), P(rm), P(rv), P(y), P(pre), P(mean), P(rstd), M, C,
+                      1e-5, 0.1, 3, P(ws), st)
+        else:
+            _lib.call("b2p_batchnorm_fwd16", P(x), P(gamma), P(beta), P(rm), P(rv), None, P(y16), 1, P(y16b), P(pre),
+                      P(mean), P(rstd), M, C, 1e-5, 0.1, 3, P(ws), st)
+        torch.cuda.synchronize()
+        outs[form] = (y, y16, y16b, pre, mean, rstd, rm, rv)
+    y, _, _, pre, mean, rstd, rm, rv = outs["fp32"]
+    _, y16, y16b, pre2, mean2, rstd2, rm2, rv2 = outs["16"]
+    assert torch.equal(y16, y.half()) and torch.equal(y16b, y.bfloat16())
+    for a, b in ((pre, pre2), (mean, mean2), (rstd, rstd2), (rm, rm2), (rv, rv2)):
+        assert torch.equal(a, b)
+    # the SyncBN stage form: bf16 operand only
+    yb = torch.empty(M, C, device="cuda", dtype=torch.bfloat16)
+    _lib.call("b2p_batchnorm_apply16", P(x), P(mean), P(rstd), P(gamma), P(beta), None, P(yb), 0, None, None, M, C, 3,
+              st)
+    torch.cuda.synchronize()
+    assert torch.equal(yb, y.bfloat16())
+
+
+def test_conformer_conv_module_bn16_bitwise():
+    """The conv module's 16-bit BatchNorm outputs (no fp32 activation, no cast passes) leave the tiny
+    Conformer's bf16 training step bitwise unchanged: loss and every gradient."""
+    Fn = _fn()
+    from tests.helpers import CFG, batch_dict, build_model
+    from wav2vec2forbrain_amd.datasets.batch_types import make_b2t_batch
+    cfg = CFG["tiny_conf"]
+    b = batch_dict(cfg)
+    batch = make_b2t_batch(b["x"], b["target"], b["day_idxs"], b["input_lens"], b["target_lens"]).cuda()
+    res = []
+    for on in (False, True):
+        Fn._BN16[0] = on
+        try:
+            torch.manual_seed(0)
+            Fn.SEEDS.reseed(1234)
+            Fn.LD_SEEDS.reseed(1234)
+            model = build_model(cfg)
+            model.train()
+            with Fn.precision("bf16"):
+                out = model(batch)
+                out.loss.backward()
+                Fn.join_wgrad()
+            torch.cuda.synchronize()
+            res.append((float(out.loss), {n: p.grad.clone() for n, p in model.named_parameters() if p.grad is not None}))
+        finally:
+            Fn._BN16[0] = True
+    assert res[0][0] == res[1][0]
+    assert res[0][1].keys() == res[1][1].keys()
+    for n in res[0][1]:
+        assert torch.equal(res[0][1][n], res[1][1][n]), n

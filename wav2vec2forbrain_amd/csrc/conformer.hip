@@ -393,9 +393,12 @@ __global__ void bn_gxhat_k(const float* __restrict__ g, const float* __restrict_
 // float4 forms of the four BatchNorm elementwise passes above (C % 4 == 0, 16-B aligned tensors):
 // the same per-element expressions, 4 consecutive channels per thread, one index division per 4
 // elements (the scalar kernels' 64-bit modulo per element held them at ~60 % of HBM speed)
+// y (fp32), y16 (fp16 when half, else bf16) and y16b (bf16) are each optional: the Conformer conv module
+// keeps only the 16-bit operands of the pointwise conv 2 (its forward GEMM and its weight gradient)
 __global__ void bn_apply4_k(const float4* __restrict__ x, const float* __restrict__ mean, const float* __restrict__ rstd,
                             const float* __restrict__ gamma, const float* __restrict__ beta, float4* __restrict__ y,
-                            float4* __restrict__ pre, int64_t n4, int64_t C4, int act) {
+                            float4* __restrict__ pre, int64_t n4, int64_t C4, int act, uint2* __restrict__ y16 = nullptr,
+                            int half = 0, uint2* __restrict__ y16b = nullptr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
   const int64_t c = 4 * (i % C4);
@@ -408,7 +411,10 @@ __global__ void bn_apply4_k(const float4* __restrict__ x, const float* __restric
     o[q] = act_f(v[q], act);
   }
   if (pre) pre[i] = make_float4(v[0], v[1], v[2], v[3]);
-  y[i] = make_float4(o[0], o[1], o[2], o[3]);
+  const float4 ov = make_float4(o[0], o[1], o[2], o[3]);
+  if (y) y[i] = ov;
+  if (y16) y16[i] = b2p_pack16x4(ov, half != 0);
+  if (y16b) y16b[i] = b2p_pack_bf16x4(ov);
 }
 
 __global__ void bn_grad_pre4_k(const float4* __restrict__ dy, const float4* __restrict__ pre, float4* __restrict__ g,
@@ -615,9 +621,21 @@ static void bn_apply_launch(const float* x, const float* mean, const float* rstd
   if (bn_vec(C, {x, y, pre}))
     hipLaunchKernelGGL(bn_apply4_k, dim3(nblk(M * C / 4)), dim3(256), 0, st, reinterpret_cast<const float4*>(x), mean,
                        rstd, gamma, beta, reinterpret_cast<float4*>(y), reinterpret_cast<float4*>(pre), M * C / 4, C / 4,
-                       act);
+                       act, (uint2*)nullptr, 0, (uint2*)nullptr);
   else
-    bn_apply_launch(x, mean, rstd, gamma, beta, y, pre, M, C, act, st);
+    hipLaunchKernelGGL(bn_apply_k, dim3(nblk(M * C)), dim3(256), 0, st, x, mean, rstd, gamma, beta, y, pre, M, C, act);
+}
+// the 16-bit-output form (vector path only: C % 4 == 0, 16-B aligned fp32 and 8-B aligned 16-bit pointers,
+// checked by the callers)
+static void bn_apply16_launch(const float* x, const float* mean, const float* rstd, const float* gamma,
+                              const float* beta, float* y, uint16_t* y16, int half, uint16_t* y16b, float* pre, int64_t M,
+                              int64_t C, int act, hipStream_t st) {
+  hipLaunchKernelGGL(bn_apply4_k, dim3(nblk(M * C / 4)), dim3(256), 0, st, reinterpret_cast<const float4*>(x), mean,
+                     rstd, gamma, beta, reinterpret_cast<float4*>(y), reinterpret_cast<float4*>(pre), M * C / 4, C / 4,
+                     act, reinterpret_cast<uint2*>(y16), half, reinterpret_cast<uint2*>(y16b));
+}
+bool bn16_ok(int64_t C, const void* x, const void* y, const void* pre, const void* y16, const void* y16b) {
+  return bn_vec(C, {x, y, pre}) && ((uintptr_t)y16 & 7u) == 0 && ((uintptr_t)y16b & 7u) == 0;
 }
 static void bn_grad_pre_launch(const float* dy, const float* pre, float* g, int64_t M, int64_t C, int act,
                                hipStream_t st) {
@@ -683,6 +701,38 @@ extern "C" int b2p_batchnorm_fwd(const float* x, const float* gamma, const float
   hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sqdev, mean, rstd,
                      running_mean, running_var, C, M, eps, momentum, b2p_gate(), nbt);
   bn_apply_launch(x, mean, rstd, gamma, beta, y, pre, M, C, act, st);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_batchnorm_fwd16(const float* x, const float* gamma, const float* beta, float* running_mean,
+                                   float* running_var, float* y, uint16_t* y16, int y16_fp16, uint16_t* y16b, float* pre,
+                                   float* mean, float* rstd, int64_t M, int64_t C, float eps, float momentum, int act,
+                                   float* workspace, b2p_stream_t stream) {
+  int64_t* nbt = take_bn_counter();
+  B2P_CHECK_ARG(x && gamma && beta && (y || y16 || y16b) && mean && rstd && workspace, "batchnorm_fwd16: NULL");
+  B2P_CHECK_ARG(bn16_ok(C, x, y, pre, y16, y16b), "batchnorm_fwd16: needs C %% 4 == 0 and aligned pointers");
+  hipStream_t st = (hipStream_t)stream;
+  if (M <= 0) return 0;
+  float* sqdev = workspace;
+  float* part = workspace + 4 * C;
+  if (colsum_impl(x, nullptr, 1, M, C, C, 0, 0, mean, 0, part, st)) return 1;
+  hipLaunchKernelGGL(scale_k, dim3(nblk(C)), dim3(256), 0, st, mean, C, 1.f / (float)M);
+  if (colsum_impl(x, mean, 1, M, C, C, 0, 3, sqdev, 0, part, st)) return 1;
+  hipLaunchKernelGGL(bn_finalize_k, dim3(nblk(C)), dim3(256), 0, st, (const float*)nullptr, sqdev, mean, rstd,
+                     running_mean, running_var, C, M, eps, momentum, b2p_gate(), nbt);
+  bn_apply16_launch(x, mean, rstd, gamma, beta, y, y16, y16_fp16, y16b, pre, M, C, act, st);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_batchnorm_apply16(const float* x, const float* mean, const float* rstd, const float* gamma,
+                                     const float* beta, float* y, uint16_t* y16, int y16_fp16, uint16_t* y16b, float* pre,
+                                     int64_t M, int64_t C, int act, b2p_stream_t stream) {
+  B2P_CHECK_ARG(x && mean && rstd && gamma && beta && (y || y16 || y16b), "batchnorm_apply16: NULL");
+  B2P_CHECK_ARG(bn16_ok(C, x, y, pre, y16, y16b), "batchnorm_apply16: needs C %% 4 == 0 and aligned pointers");
+  if (M * C <= 0) return 0;
+  bn_apply16_launch(x, mean, rstd, gamma, beta, y, y16, y16_fp16, y16b, pre, M, C, act, (hipStream_t)stream);
   B2P_CHECK_LAUNCH();
   return 0;
 }

@@ -2728,6 +2728,7 @@ def _act_dropout_cast16(pre, act, p, seed):
 
 
 _FFN_F16B = [os.environ.get("B2P_FFN_F16B", "1") != "0"]
+_BN16 = [os.environ.get("B2P_BN16", "1") != "0"]
 _FFN_PRE16 = [os.environ.get("B2P_FFN_PRE16", "1") != "0"]
 
 
@@ -3081,7 +3082,8 @@ class _ConformerAttnBlock(torch.autograd.Function):
 
 
 # ------------------------------------------------------------------ synchronised BatchNorm
-def _bn_fwd_sync(c, gamma, beta, run_mean, run_var, y, pre, mean, rstd, M, C, eps, momentum, act, ws, group):
+def _bn_fwd_sync(c, gamma, beta, run_mean, run_var, y, pre, mean, rstd, M, C, eps, momentum, act, ws, group, y16=None,
+                 half=False, y16b=None):
     """Training BatchNorm over the rows of every data-parallel rank: the
     per-channel sum and the sum of squared deviations from the global mean are all-reduced
     (2 x C floats per conv module); running statistics use the global count, like torch SyncBN."""
@@ -3096,8 +3098,12 @@ def _bn_fwd_sync(c, gamma, beta, run_mean, run_var, y, pre, mean, rstd, M, C, ep
     collective(lambda: dist.all_reduce(sq, group=group))
     _lib.call("b2p_batchnorm_finalize", _p(mean), _p(sq), _p(rstd), _p(run_mean), _p(run_var), C, count, float(eps),
               float(momentum), 1, _st())
-    _lib.call("b2p_batchnorm_apply", _p(c), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(y), _p(pre), M, C, act,
-              _st())
+    if y16 is not None:   # 16-bit operand outputs (y may be None)
+        _lib.call("b2p_batchnorm_apply16", _p(c), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(y), _p(y16), int(half),
+                  _p(y16b), _p(pre), M, C, act, _st())
+    else:
+        _lib.call("b2p_batchnorm_apply", _p(c), _p(mean), _p(rstd), _p(gamma), _p(beta), _p(y), _p(pre), M, C, act,
+                  _st())
 
 
 def _bn_bwd_sync(dy, pre, c, mean, rstd, gamma, dx, dgamma, dbeta, M, C, act, ws, group):
@@ -3158,9 +3164,16 @@ class _ConvModule(torch.autograd.Function):
         _lib.call("b2p_glu_fwd", _p(a), _p(u), NT, D, _st())
         c = torch.empty(NT, D, device=dev)
         _lib.call("b2p_dwconv_fwd", _p(u), _p(w_dw), _p(c), B, T, D, K, _st())
-        s = torch.empty(NT, D, device=dev)
         ws = torch.empty(int(_lib.load().b2p_batchnorm_workspace(NT, D)), device=dev)
         sync = None
+        # bf16 training step: the BatchNorm + activation writes only the 16-bit operands of pointwise conv 2
+        # (its forward GEMM: fp16 under forward_f16; its weight gradient: bf16), no fp32 output and no cast
+        # passes (B2P_BN16=0: fp32 output, operands cast from it)
+        o16 = training and _BN16[0] and bf16_mode() and _bwd16_path() and D % 4 == 0
+        half = o16 and _state.fwd16
+        s = None if o16 else torch.empty(NT, D, device=dev)
+        s16 = torch.empty(NT, D, device=dev, dtype=torch.float16 if half else BF16) if o16 else None
+        s16b = torch.empty(NT, D, device=dev, dtype=BF16) if half else None
         if training:
             pre = torch.empty(NT, D, device=dev)
             bm = torch.empty(D, device=dev)
@@ -3169,7 +3182,12 @@ class _ConvModule(torch.autograd.Function):
             if nbt is not None:
                 _lib.call("b2p_batchnorm_count_next", _p(nbt))
             if sync is not None:
-                _bn_fwd_sync(c, bn_g, bn_b, bn_rm, bn_rv, s, pre, bm, br, NT, D, bn_eps, momentum, act, ws, sync)
+                _bn_fwd_sync(c, bn_g, bn_b, bn_rm, bn_rv, s, pre, bm, br, NT, D, bn_eps, momentum, act, ws, sync,
+                             y16=s16, half=half, y16b=s16b)
+            elif o16:
+                _lib.call("b2p_batchnorm_fwd16", _p(c), _p(bn_g), _p(bn_b), _p(bn_rm), _p(bn_rv), None, _p(s16),
+                          int(half), _p(s16b), _p(pre), _p(bm), _p(br), NT, D, float(bn_eps), float(momentum), act,
+                          _p(ws), _st())
             else:
                 _lib.call("b2p_batchnorm_fwd", _p(c), _p(bn_g), _p(bn_b), _p(bn_rm), _p(bn_rv), _p(s), _p(pre),
                           _p(bm), _p(br), NT, D, float(bn_eps), float(momentum), act, _p(ws), _st())
@@ -3178,7 +3196,13 @@ class _ConvModule(torch.autograd.Function):
             _lib.call("b2p_batchnorm_eval", _p(c), _p(bn_g), _p(bn_b), _p(bn_rm), _p(bn_rv), _p(s), NT, D,
                       float(bn_eps), act, _p(ws), _st())
         y = torch.empty(NT, D, device=dev)
-        gemm(NT, D, D, op(s, 0, D, True), op(w_pw2, 0, D, True), y, D, drop_p=p, seed=seed, residual=x2)
+        if o16:
+            wbuf, wop = _w_op16(w_pw2, half)
+            gemm(NT, D, D, op(s16, 0, D, True), wop, y, D, drop_p=p, seed=seed, residual=x2)
+            del wbuf
+            s = s16b if half else s16   # the bf16 weight-gradient operand is what the backward keeps
+        else:
+            gemm(NT, D, D, op(s, 0, D, True), op(w_pw2, 0, D, True), y, D, drop_p=p, seed=seed, residual=x2)
         ctx.save_for_backward(x2, h, mean, rstd, a, u, c, pre, bm, br, s, g, w_pw1, w_dw, bn_g, w_pw2)
         ctx.cfg = cfg
         ctx.shape = (B, T, D, K)
@@ -3201,7 +3225,7 @@ class _ConvModule(torch.autograd.Function):
         ds = torch.empty(NT, D, device=dev)
         if b16:
             do16, _ = _drop_cast_colsum(dy, p, seed, 1.0, False)
-            dpw2 = _wgrad16(w_pw2, ng[7], do16, D, cast16(s), D, NT)
+            dpw2 = _wgrad16(w_pw2, ng[7], do16, D, s if s.dtype == BF16 else cast16(s), D, NT)
             gemm(NT, D, D, op(do16, 0, D, True), op(weight16t(w_pw2), 0, D, True), ds, D)
             del do16
         else:
