@@ -199,6 +199,9 @@ _PP_MIN_MN = int(os.environ.get("B2P_PP_MIN_MN", str(3 * 1024 * 1024)))
 # tiles) 69.73 -> 68.54 ms per step unsplit; the base model's 7968 x 768 (378 tiles, 1.5 rounds of the
 # CUs) stay split (14.99 vs 15.13 ms unsplit), profiles/r05o_pp_split_rule_ab.txt
 _PP_SPLIT_MAX_BLOCKS = int(os.environ.get("B2P_PP_SPLIT_MAX_BLOCKS", "448"))
+# ... unless K is long enough that one 128 x 128 tile's K loop dominates (the front end's implicit-unfold
+# backward-data GEMM, 8192 x 1024 x 24576 in the Conformer step: 1.39 ms unsplit on 128 x 128 tiles)
+_PP_SPLIT_LONG_K = int(os.environ.get("B2P_PP_SPLIT_LONG_K", "8192"))
 
 
 class _Deferred:
@@ -834,7 +837,7 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
         tpp = -(-M // 256) * -(-N // 256) * nz1 * nz2
         kpp = min(-(-160 // tpp), K // 1024)
         if (b16 and (_PP_SPLIT or M * N * nz1 * nz2 >= _PP_MIN_MN) and tpp * kpp >= 160 and kpp >= 2
-                and blocks < _PP_SPLIT_MAX_BLOCKS):
+                and (blocks < _PP_SPLIT_MAX_BLOCKS or K >= _PP_SPLIT_LONG_K)):
             # 256x256 ping-pong tiles (gemm16.hip) over >= 1024-deep K slices, ~160-200 workgroups
             # (the frozen weight gradients, K = tokens): fewer, larger tiles than the 128 x 128 split
             ks = kpp
