@@ -40,6 +40,19 @@ from .. import functional as Fn
 # one per model) share it instead of each opening another.
 _CAPTURE_STREAMS: dict = {}
 
+# The step counter the library's dropout kernels currently read (b2p_set_seed_epoch keeps a raw device
+# pointer): held here so the tensor outlives every StepGraph that shares it. Without this reference a
+# Trainer collected without release() left the library pointing at freed memory, and the next eager
+# kernels read whatever tensor the allocator put there (two dropout launches with one seed drew
+# different masks).
+_INSTALLED_EPOCH = [None]
+
+
+def _install_epoch(t) -> None:
+    _lib.check(_lib.load().b2p_set_seed_epoch(None if t is None else ctypes.c_void_p(t.data_ptr())),
+               "b2p_set_seed_epoch")
+    _INSTALLED_EPOCH[0] = t
+
 
 def live_graph_nodes(module_prefix: str = "wav2vec2forbrain_amd") -> int:
     """Number of live autograd nodes of custom Functions defined under module_prefix (the backward
@@ -143,7 +156,7 @@ class StepGraph:
         lib = _lib.load()
         if self.epoch is None:
             self.epoch = torch.zeros(1, dtype=torch.int64, device=dev)
-        _lib.check(lib.b2p_set_seed_epoch(ctypes.c_void_p(self.epoch.data_ptr())), "b2p_set_seed_epoch")
+        _install_epoch(self.epoch)
         if self.opt is not None:
             self.opt.make_capturable(dev)
         Fn.set_gemm_timing(False)
@@ -225,7 +238,7 @@ class StepGraph:
     def release(self) -> None:
         """Back to eager semantics (the seed counter is no longer mixed in); the executable graph and
         its resources are destroyed now rather than whenever the Python object is collected."""
-        _lib.check(_lib.load().b2p_set_seed_epoch(None), "b2p_set_seed_epoch")
+        _install_epoch(None)
         if self.graph is not None:
             torch.cuda.synchronize()
             self.graph.reset()
