@@ -448,6 +448,21 @@ int b2p_attn16_fwd(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t
 int b2p_attn16_fwd_f16(const void* qkv16h, void* O16h, void* Ob16, float* lse2, int64_t B, int64_t T,
                        int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
                        b2p_stream_t stream);
+/* Dropout keep bits of n_layers attention launches drawn ahead in one launch: mask (n_layers, B, nh, T, 8)
+ * int32, layer l's block equal word for word to the mask b2p_attn16_fwd[_f16] stores with seed seeds[l]
+ * (a host array; the graph-replay step counter is mixed in as there). T <= 256, 0 < drop_p < 1. Replaces
+ * the per-layer draw inside the reference's attention dropout (TF w2v Wav2Vec2Attention.forward
+ * nn.functional.dropout(attn_weights), TF conf :458-470); the encoder issues it beside the GRU. */
+int b2p_attn16_keep_masks(uint32_t* mask, const uint64_t* seeds, int64_t n_layers, int64_t B, int64_t T,
+                          int64_t nh, float drop_p, b2p_stream_t stream);
+/* b2p_attn16_fwd / b2p_attn16_fwd_f16 with the keep bits READ from mask (one layer's block of
+ * b2p_attn16_keep_masks, or a mask an earlier forward stored): same outputs as the storing forward with
+ * that mask's seed; the backward takes the same mask. */
+int b2p_attn16_fwd_keep(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
+                        int64_t dh, float scale, float drop_p, const uint32_t* mask, b2p_stream_t stream);
+int b2p_attn16_fwd_f16_keep(const void* qkv16h, void* O16h, void* Ob16, float* lse2, int64_t B, int64_t T,
+                            int64_t nh, int64_t dh, float scale, float drop_p, const uint32_t* mask,
+                            b2p_stream_t stream);
 int b2p_attn16_bwd(const void* qkv16, const void* dO16, const float* lse2, float* delta_ws,
                    float* dqkv, void* dqkv16, int64_t B, int64_t T, int64_t nh, int64_t dh,
                    float scale, float drop_p, uint64_t drop_seed, const uint32_t* mask, b2p_stream_t stream);

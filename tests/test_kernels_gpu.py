@@ -279,6 +279,50 @@ def test_fused_attention_bf16_vs_fp32_core(B, T, nh, p, variant):
     assert float((lse2 - ref_lse2).abs().max()) < 2e-2
 
 
+@pytest.mark.parametrize("B,T,nh", [(2, 249, 12), (1, 17, 2), (2, 256, 3), (1, 241, 2), (3, 240, 2), (1, 1, 1)])
+@pytest.mark.parametrize("half", [True, False])
+@pytest.mark.parametrize("epoch", [False, True])
+def test_attention_keep_masks_drawn_ahead(B, T, nh, half, epoch):
+    """b2p_attn16_keep_masks (the encoder's masks drawn ahead beside the GRU, functional.attn_keep_plan)
+    against the masks the storing forwards draw: layer l's block equals, word for word, the mask
+    b2p_attn16_fwd[_f16] stores with seed l (with and without the graph-replay step counter), and the
+    forward that reads it (b2p_attn16_fwd[_f16]_keep) writes O, its bf16 copy and lse2 bitwise equal to
+    the storing forward's."""
+    import ctypes
+    Fn = _fn()
+    lib = Fn._lib.load()
+    torch.manual_seed(5)
+    dh, p = 64, 0.1
+    D = nh * dh
+    qkv = (torch.randn(B * T, 3 * D) * 0.7).cuda().to(torch.float16 if half else torch.bfloat16)
+    seeds = [11, 2 ** 61 + 3, 977]
+    ctr = torch.full((1,), 5, dtype=torch.int64, device="cuda")
+    masks = torch.empty(len(seeds), B, nh, T, 8, device="cuda", dtype=torch.int32)
+    arr = (ctypes.c_uint64 * len(seeds))(*seeds)
+    if epoch:
+        Fn._lib.check(lib.b2p_set_seed_epoch(ctypes.c_void_p(ctr.data_ptr())), "set_seed_epoch")
+    try:
+        Fn._lib.call("b2p_attn16_keep_masks", masks.data_ptr(), ctypes.addressof(arr), len(seeds), B, T, nh, p,
+                     Fn._st())
+        for l, seed in enumerate(seeds):
+            if half:
+                Oh, Ob, lse2, mask = Fn._attn16_fwd_f16(qkv, B, T, nh, dh, p, seed)
+                Oh2, Ob2, lse22 = torch.empty_like(Oh), torch.empty_like(Ob), torch.empty_like(lse2)
+                Fn._lib.call("b2p_attn16_fwd_f16_keep", qkv.data_ptr(), Oh2.data_ptr(), Ob2.data_ptr(),
+                             lse22.data_ptr(), B, T, nh, dh, float(dh ** -0.5), p, masks[l].data_ptr(), Fn._st())
+                assert torch.equal(Oh, Oh2) and torch.equal(Ob, Ob2) and torch.equal(lse2, lse22)
+            else:
+                O16, lse2, mask = Fn._attn16_fwd(qkv, B, T, nh, dh, p, seed, want_mask=True)
+                O2, lse22 = torch.empty_like(O16), torch.empty_like(lse2)
+                Fn._lib.call("b2p_attn16_fwd_keep", qkv.data_ptr(), O2.data_ptr(), lse22.data_ptr(), B, T, nh, dh,
+                             float(dh ** -0.5), p, masks[l].data_ptr(), Fn._st())
+                assert torch.equal(O16, O2) and torch.equal(lse2, lse22)
+            assert torch.equal(mask, masks[l]), l
+        torch.cuda.synchronize()
+    finally:
+        Fn._lib.check(lib.b2p_set_seed_epoch(None), "set_seed_epoch")
+
+
 @pytest.mark.parametrize("B,T,nh,p", [(2, 249, 12, 0.1), (3, 100, 4, 0.0), (1, 17, 2, 0.1), (2, 256, 3, 0.1),
                                        (1, 241, 2, 0.1), (2, 313, 4, 0.1), (1, 512, 2, 0.0)])
 @pytest.mark.parametrize("form", ["f16_mask", "bf16_hash"])

@@ -1,0 +1,25 @@
+set -u
+# attention keep masks drawn ahead beside the GRU: kernel equality tests, the trainer / DP tests that
+# capture the plan, step-time A/B (B2P_ATTN_KEEP_AHEAD=0/1), one replayed base step with its timeline
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05ae; mkdir -p $O
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels_gpu.py -k \
+  "keep_masks or fused_attention" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_trainer_gpu.py \
+  tests/test_dp_gpu.py tests/test_layerdrop_gpu.py tests/test_gemm_gpu.py::test_dropout_epilogue_mask_consistent \
+  > $O/pytest2.log 2>&1 || { tail -30 $O/pytest2.log; exit 1; }
+tail -1 $O/pytest2.log
+run() {  # tag config env...
+  local tag=$1 C=$2; shift 2
+  env "$@" timeout -k 10 300 python3 bench.py --config $C --steps 20 --warmup 5 --no-cpu-baseline --no-parity \
+    --no-conformer --no-extra --no-roofline > $O/b_$tag.json 2> $O/b_$tag.err || { tail -5 $O/b_$tag.err; return 1; }
+  echo "$tag $(python3 -c "import json; print(json.loads(open('$O/b_$tag.json').read().strip().splitlines()[-1])['ms_per_step'])") ms"
+}
+run base_ka0 base B2P_ATTN_KEEP_AHEAD=0 && run base_ka1 base B2P_ATTN_KEEP_AHEAD=1 && \
+run conf_ka0 conformer B2P_ATTN_KEEP_AHEAD=0 && run conf_ka1 conformer B2P_ATTN_KEEP_AHEAD=1 || exit 1
+timeout -k 10 300 rocprofv3 --kernel-trace -d $O/tb -o kt -- python3 bench.py --steps 8 --warmup 3 --no-cpu-baseline \
+  --no-parity --no-roofline --no-conformer --no-extra > $O/base.log 2>&1 || { tail -20 $O/base.log; exit 1; }
+python3 tools/step_breakdown.py $O/tb 8 40 > $O/base_replay_step.txt 2>&1; head -3 $O/base_replay_step.txt
+python3 tools/step_timeline.py $O/tb 8 15 > $O/base_timeline.txt 2>&1; tail -1 $O/base_timeline.txt
+find $O -name "*.db" -delete; find $O -name "*.csv" -delete

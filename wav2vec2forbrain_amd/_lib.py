@@ -121,6 +121,9 @@ _SIGS = {
     "b2p_gru_hprev": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i32, c_p]),
     "b2p_attn16_fwd": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p, c_p]),
     "b2p_attn16_fwd_f16": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p, c_p]),
+    "b2p_attn16_fwd_keep": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_p, c_p]),
+    "b2p_attn16_fwd_f16_keep": (c_i32, [c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_p, c_p]),
+    "b2p_attn16_keep_masks": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_p]),
     "b2p_attn16_bwd": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p,
                                c_p]),
     "b2p_attn16_bwd_f16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_f32, c_f32, c_u64, c_p,

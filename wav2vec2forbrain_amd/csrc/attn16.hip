@@ -188,11 +188,13 @@ __device__ __forceinline__ uint32_t keep4_bits(uint32_t key_lo, uint32_t k32, ui
 // T1: T > TM - 16, so keys >= T lie in the last key tile only: its score accumulator starts from a bias
 // (0 for keys < T, -inf beyond) computed once, and no per-element masking runs in the loop (the masked
 // form's uniform per-tile branches made the unrolled loop spill ~230 SGPRs into VGPR lanes)
-template <int DM, bool H, int TM, bool T1 = false>   // DM 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward
+// DM 0: no dropout, 1: hash the keep mask, 2: also store the keep bits for the backward, 3: read the keep
+// bits from maskw (drawn ahead by attn_keep_k, the layout DM 2 stores)
+template <int DM, bool H, int TM, bool T1 = false>
 __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ O16,
                                                        uint16_t* __restrict__ Ob16, float* __restrict__ lse2, int T,
                                                        int nh, float scale, DropCfg dc, uint32_t* __restrict__ maskw) {
-  static_assert(TM == TMAX || DM != 2, "the stored keep mask covers T <= 256");
+  static_assert(TM == TMAX || DM < 2, "the stored keep mask covers T <= 256");
   constexpr int NKT = TM / 16;   // key tiles
   constexpr bool DROP = DM != 0;
   if (b2p_gated_off(dc.gate)) return;   // LayerDrop: this replay skips the layer (outputs unused)
@@ -234,6 +236,14 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     const char* Vimg = smem + TM * 128 + obase;
     const int q = qt * 16 + lr;
     const bool qok = q < T;
+    uint32_t mbits[2] = {0u, 0u};   // this lane's keep bits: byte c = keys 32c + 4g + i (bit i), +16 (bit 4 + i)
+    if constexpr (DM == 3) {        // issued first: the load hides under the S MFMAs
+      if (qok) {
+        const uint2 mw = *reinterpret_cast<const uint2*>(maskw + (((int64_t)b * nh + h) * T + q) * 8 + 2 * g);
+        mbits[0] = mw.x;
+        mbits[1] = mw.y;
+      }
+    }
     if (qt != qt0) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) qf[ks] = qok ? gload8(qkv + (row0 + q) * ld + h * DH + 32 * ks + 8 * g) : bf16x8{};
@@ -286,13 +296,14 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     f32x4 o[4];
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
-    uint32_t mbits[2] = {0u, 0u};   // this lane's keep bits: byte c = keys 32c + 4g + i (bit i), +16 (bit 4 + i)
 #pragma unroll
     for (int c = 0; c < NKT / 2; ++c) {
 #pragma unroll
       for (int half = 0; half < 2; ++half) {
         const int key0 = (2 * c + half) * 16 + 4 * g;
-        const uint32_t kb = DROP ? keep4_bits(rowlo + (uint32_t)key0, k32, thr16) : 0xFu;
+        const uint32_t kb = DM == 3 ? (mbits[c >> 2] >> (8 * (c & 3) + 4 * half)) & 0xFu
+                            : DROP  ? keep4_bits(rowlo + (uint32_t)key0, k32, thr16)
+                                    : 0xFu;
         if (DM == 2) mbits[c >> 2] |= kb << (8 * (c & 3) + 4 * half);
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -329,6 +340,39 @@ __global__ void __launch_bounds__(FWD_NT) attn16_fwd_k(const uint16_t* __restric
     }
     if (qok && g == 0) lse2[((int64_t)b * nh + h) * T + q] = mc + __log2f(sum);
   }
+}
+
+// Dropout keep bits of several layers' attention in one launch (b2p_attn16_keep_masks): for each layer's
+// seed, word for word the mask a DM 2 forward stores, so that layer's forward reads its bits (DM 3)
+// instead of hashing them in its VALU-bound softmax loop, and the backward reads them as before. The
+// model forward issues it on a side stream at its start (functional.attn_keep_plan). One thread per (layer, batch x head x query row, lane group g): the 16 keep4_bits
+// of the 8 bytes forward lane (g, query) writes.
+constexpr int KEEP_LAYERS = 32;   // layers per launch (seeds by value)
+constexpr int KEEP_LDS = 24 * 1024;
+struct KeepSeeds {
+  uint64_t seed[KEEP_LAYERS];
+};
+__global__ void __launch_bounds__(256) attn_keep_k(uint32_t* __restrict__ mask, KeepSeeds ks,
+                                                   const uint64_t* __restrict__ epoch, int64_t rows, int T,
+                                                   uint32_t thr, int nl) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t per = rows * 4;
+  if (i >= per * nl) return;
+  const int layer = (int)(i / per);
+  const int64_t r = i - layer * per;
+  const int64_t row = r >> 2;   // (b * nh + h) * T + q
+  const int g = (int)(r & 3);
+  const uint64_t seed = b2p_seed_eff(ks.seed[layer], epoch);
+  const uint32_t k32 = (uint32_t)seed ^ b2p_mix32((uint32_t)(seed >> 32) + 0x9E3779B9u);
+  const uint32_t thr16 = b2p_thr16(thr);
+  const uint32_t rowlo = (uint32_t)row * (uint32_t)(T + (T & 1));
+  uint32_t mb[2] = {0u, 0u};
+#pragma unroll
+  for (int c = 0; c < TMAX / 32; ++c)
+#pragma unroll
+    for (int half = 0; half < 2; ++half)
+      mb[c >> 2] |= keep4_bits(rowlo + (uint32_t)((2 * c + half) * 16 + 4 * g), k32, thr16) << (8 * (c & 3) + 4 * half);
+  *reinterpret_cast<uint2*>(mask + (int64_t)layer * rows * 8 + row * 8 + 2 * g) = make_uint2(mb[0], mb[1]);
 }
 
 // ------------------------------------------------------------------------------------ backward dK dV
@@ -846,6 +890,8 @@ int init_attrs_t() {
     rc |= set_lds(attn16_fwd_k<1, H, TM, true>, fwd_lds<TM>());
     rc |= set_lds(attn16_fwd_k<2, H, TM, true>, fwd_lds<TM>());
     rc |= set_lds(attn16_fwd_k<2, H, TM>, fwd_lds<TM>());
+    rc |= set_lds(attn16_fwd_k<3, H, TM, true>, fwd_lds<TM>());
+    rc |= set_lds(attn16_fwd_k<3, H, TM>, fwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dkv_k<2, H, TM>, bwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dkv2_k<2, H, TM>, bwd_lds<TM>());
     rc |= set_lds(attn16_bwd_dq_k<2, H, TM>, fwd_lds<TM>());
@@ -877,7 +923,7 @@ bool attn_t1() {   // B2P_ATTN_T1=0: the masked form for every T (A/B)
 }
 int attn16_fwd_launch(bool half, const void* qkv16, void* O16, void* Ob16, float* lse2, int64_t B, int64_t T,
                       int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed, uint32_t* mask,
-                      b2p_stream_t stream) {
+                      b2p_stream_t stream, bool mask_in = false) {
   B2P_CHECK_ARG(qkv16 && O16 && lse2, "attn16_fwd: NULL pointer");
   B2P_CHECK_ARG(dh == DH && T <= 2 * TMAX && T > 0, "attn16_fwd: needs head size 64 and T <= 512");
   B2P_CHECK_ARG(!mask || T <= TMAX, "attn16_fwd: the stored keep mask covers T <= 256 (pass NULL: the backward rehashes)");
@@ -887,19 +933,20 @@ int attn16_fwd_launch(bool half, const void* qkv16, void* O16, void* Ob16, float
                 "(32-bit dropout element index)");
   dim3 grid((unsigned)(B * nh * ((T + FWD_QB - 1) / FWD_QB)));
   const DropCfg dc = drop_cfg(drop_p, drop_seed);
-  const int dm = drop_p > 0.f ? (mask ? 2 : 1) : 0;
+  B2P_CHECK_ARG(!mask_in || (mask && drop_p > 0.f), "attn16_fwd: reading the keep bits needs the mask and p > 0");
+  const int dm = drop_p > 0.f ? (mask ? (mask_in ? 3 : 2) : 1) : 0;
   auto run = [&](auto dmc, auto hc) {
     constexpr int DM = decltype(dmc)::value;
     constexpr bool HH = decltype(hc)::value;
     if (T <= TMAX && T > TMAX - 16 && attn_t1())
       hipLaunchKernelGGL((attn16_fwd_k<DM, HH, TMAX, true>), grid, dim3(FWD_NT), fwd_lds<TMAX>(), (hipStream_t)stream,
                          (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T, (int)nh, scale, dc,
-                         dm == 2 ? mask : (uint32_t*)nullptr);
+                         dm >= 2 ? mask : (uint32_t*)nullptr);
     else if (T <= TMAX)
       hipLaunchKernelGGL((attn16_fwd_k<DM, HH, TMAX>), grid, dim3(FWD_NT), fwd_lds<TMAX>(), (hipStream_t)stream,
                          (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T, (int)nh, scale, dc,
-                         dm == 2 ? mask : (uint32_t*)nullptr);
-    else if constexpr (DM != 2)
+                         dm >= 2 ? mask : (uint32_t*)nullptr);
+    else if constexpr (DM < 2)
       hipLaunchKernelGGL((attn16_fwd_k<DM, HH, 2 * TMAX>), grid, dim3(FWD_NT), fwd_lds<2 * TMAX>(), (hipStream_t)stream,
                          (const uint16_t*)qkv16, (uint16_t*)O16, (uint16_t*)Ob16, lse2, (int)T, (int)nh, scale, dc,
                          (uint32_t*)nullptr);
@@ -907,11 +954,13 @@ int attn16_fwd_launch(bool half, const void* qkv16, void* O16, void* Ob16, float
   using F = std::false_type;
   using Tr = std::true_type;
   if (half) {
-    if (dm == 2) run(std::integral_constant<int, 2>(), Tr());
+    if (dm == 3) run(std::integral_constant<int, 3>(), Tr());
+    else if (dm == 2) run(std::integral_constant<int, 2>(), Tr());
     else if (dm == 1) run(std::integral_constant<int, 1>(), Tr());
     else run(std::integral_constant<int, 0>(), Tr());
   } else {
-    if (dm == 2) run(std::integral_constant<int, 2>(), F());
+    if (dm == 3) run(std::integral_constant<int, 3>(), F());
+    else if (dm == 2) run(std::integral_constant<int, 2>(), F());
     else if (dm == 1) run(std::integral_constant<int, 1>(), F());
     else run(std::integral_constant<int, 0>(), F());
   }
@@ -930,6 +979,41 @@ extern "C" int b2p_attn16_fwd_f16(const void* qkv16h, void* O16h, void* Ob16, fl
                                   int64_t nh, int64_t dh, float scale, float drop_p, uint64_t drop_seed,
                                   uint32_t* mask, b2p_stream_t stream) {
   return attn16_fwd_launch(true, qkv16h, O16h, Ob16, lse2, B, T, nh, dh, scale, drop_p, drop_seed, mask, stream);
+}
+
+extern "C" int b2p_attn16_fwd_keep(const void* qkv16, void* O16, float* lse2, int64_t B, int64_t T, int64_t nh,
+                                   int64_t dh, float scale, float drop_p, const uint32_t* mask, b2p_stream_t stream) {
+  return attn16_fwd_launch(false, qkv16, O16, nullptr, lse2, B, T, nh, dh, scale, drop_p, 0, const_cast<uint32_t*>(mask),
+                           stream, true);
+}
+
+extern "C" int b2p_attn16_fwd_f16_keep(const void* qkv16h, void* O16h, void* Ob16, float* lse2, int64_t B, int64_t T,
+                                       int64_t nh, int64_t dh, float scale, float drop_p, const uint32_t* mask,
+                                       b2p_stream_t stream) {
+  return attn16_fwd_launch(true, qkv16h, O16h, Ob16, lse2, B, T, nh, dh, scale, drop_p, 0, const_cast<uint32_t*>(mask),
+                           stream, true);
+}
+
+extern "C" int b2p_attn16_keep_masks(uint32_t* mask, const uint64_t* seeds, int64_t n_layers, int64_t B, int64_t T,
+                                     int64_t nh, float drop_p, b2p_stream_t stream) {
+  B2P_CHECK_ARG(mask && seeds, "attn16_keep_masks: NULL pointer");
+  B2P_CHECK_ARG(T > 0 && T <= TMAX && drop_p > 0.f && drop_p < 1.f, "attn16_keep_masks: needs 0 < T <= 256, 0 < p < 1");
+  B2P_CHECK_ARG(B * nh * T * (T + (T & 1)) < (1ll << 32), "attn16_keep_masks: B * heads * T * T must stay below 2^32");
+  const int64_t rows = B * nh * T;
+  if (rows <= 0 || n_layers <= 0) return 0;
+  const uint32_t thr = b2p_dropout_threshold(drop_p);
+  for (int64_t l0 = 0; l0 < n_layers; l0 += KEEP_LAYERS) {
+    const int nl = (int)(n_layers - l0 < KEEP_LAYERS ? n_layers - l0 : KEEP_LAYERS);
+    KeepSeeds ks{};
+    for (int j = 0; j < nl; ++j) ks.seed[j] = seeds[l0 + j];
+    // 24 KB of (unused) LDS per workgroup: a workgroup cannot land on a CU that holds a GRU recurrence
+    // (gru16: ~149 KB of its 160 KB), which it would slow by sharing its issue slots (measured: +97 us
+    // on a 479 us gru16_fwd at the base workload with no LDS request)
+    hipLaunchKernelGGL(attn_keep_k, dim3((unsigned)((rows * 4 * nl + 255) / 256)), dim3(256), KEEP_LDS, (hipStream_t)stream,
+                       mask + l0 * rows * 8, ks, b2p_seed_epoch(), rows, (int)T, thr, nl);
+    B2P_CHECK_LAUNCH();
+  }
+  return 0;
 }
 
 namespace {

@@ -594,6 +594,9 @@ def flush_wgrad(after=None) -> None:
     the main stream has queued so far. Each parameter's work always goes to the same side stream
     (its accumulations stay ordered); independent weight-gradient GEMMs on different streams run
     concurrently, which fills the chip without split-K partial sums and their reduce launches."""
+    if _WGRAD_DEBUG:
+        print(f"flush_wgrad: {len(_Deferred.queue)} queued, {len(_Deferred.accs)} accs, after={after is not None}, "
+              f"capturing={capturing()}", flush=True)
     if not _Deferred.queue and not _Deferred.accs:
         return
     main = torch.cuda.current_stream()
@@ -674,6 +677,8 @@ def collective(fn) -> None:
         fn()
         return
     _join_sides()
+    if _KEEP_PLAN[0] is not None:
+        _KEEP_PLAN[0].join()
     seg.split(fn)
 
 
@@ -1585,11 +1590,9 @@ class _GRULayer(torch.autograd.Function):
             doL = torch.empty(_ln_floats(B, T, H, ndir, 1), device=dev)
             _lib.call("b2p_gru_lane_permute", _p(dout), _p(doL), B, T, H, ndir, 1, 1, 0x0, 1, _st())
             dgL = torch.empty(_ln_floats(B, T, H, ndir, 4), device=dev)
-            ev = torch.cuda.Event()
-            ev.record()
-            _lib.call("b2p_gru_bwd16", _p(doL), _p(whh_s), _p(hL), _p(saved), _p(h0), _p(dgL), _p(dh0), B, T, H,
-                      ndir, _st())
-            flush_wgrad(ev)   # frozen-parameter gradient GEMMs fill the chip beside the 4-CU recurrence
+            # frozen-parameter gradient GEMMs fill the chip beside the 4-CU recurrence
+            _gru_bwd_launch(lambda: _lib.call("b2p_gru_bwd16", _p(doL), _p(whh_s), _p(hL), _p(saved), _p(h0), _p(dgL),
+                                              _p(dh0), B, T, H, ndir, _st()))
             del doL
             # dgi = LN records (0, 1, 2), dgh = LN records (0, 1, 3)
             _lib.call("b2p_gru_lane_permute", _p(dgL), _p(dgi), B, T, H, ndir, 4, 3, 0xF210, 0, _st())
@@ -1597,19 +1600,14 @@ class _GRULayer(torch.autograd.Function):
             del dgL
         elif usemc:
             ws = _gru_mc_ws(B, H, ndir, dev)
-            ev = torch.cuda.Event()
-            ev.record()
-            _lib.call("b2p_gru_bwd_mc", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi), _p(dgh), _p(dh0),
-                      _p(ws), B, T, H, ndir, _st())
+            # frozen-parameter gradient GEMMs beside the (H/64 x 4)-CU recurrence
+            _gru_bwd_launch(lambda: _lib.call("b2p_gru_bwd_mc", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0),
+                                              _p(dgi), _p(dgh), _p(dh0), _p(ws), B, T, H, ndir, _st()))
             _gru_mc_fold(ws, 2, ctx.whh0, H, dev)
-            flush_wgrad(ev)   # frozen-parameter gradient GEMMs beside the (H/64 x 4)-CU recurrence
         else:
             dhbuf = torch.empty(ndir, B, H, device=dev)
-            ev = torch.cuda.Event()
-            ev.record()
-            _lib.call("b2p_gru_bwd", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi), _p(dgh), _p(dh0),
-                      _p(dhbuf), B, T, H, ndir, _st())
-            flush_wgrad(ev)
+            _gru_bwd_launch(lambda: _lib.call("b2p_gru_bwd", _p(dout), _p(whh_s), _p(out), _p(saved), _p(h0), _p(dgi),
+                                              _p(dgh), _p(dh0), _p(dhbuf), B, T, H, ndir, _st()))
         grads = [None] * (4 * ndir)
         # recurrent weights: dW_hh[d] = dgh[:, :, d]^T @ hprev[d]
         hp = torch.empty(ndir, B, T, H, device=dev)
@@ -2113,12 +2111,140 @@ def attn16_ok(T, dh) -> bool:
     return dh == 64 and 0 < T <= 512
 
 
+# ---------------------------------------------------------------- attention keep masks drawn ahead
+# The attention dropout keep bits of every layer of one encoder forward, drawn by one launch
+# (b2p_attn16_keep_masks) on a side stream at the start of the model's forward (beside the front end);
+# each layer's fused attention forward then reads its bits
+# (b2p_attn16_fwd[_f16]_keep) instead of hashing them inside its VALU-bound softmax loop, and the
+# backward reads the same block as before. Layers take the blocks in call order (a host-skipped
+# LayerDrop layer leaves one unused: every block is an independent draw). Measured: attention forward
+# 38.4 -> 33.2 us per base layer, the step unchanged within noise (profiles/r05ag_attn_keep_ahead_ab.txt).
+# B2P_ATTN_KEEP_AHEAD=0: each forward hashes its own (A/B).
+_KEEP_AHEAD = [os.environ.get("B2P_ATTN_KEEP_AHEAD", "1") != "0"]
+_KEEP_PLAN: list = [None]
+
+
+class _KeepPlan:
+    def __init__(self, n, B, T, nh, p):
+        self.key = (B, T, nh, float(p))
+        self.n, self.next, self.joined, self.ev = n, 0, False, None
+        self.masks = torch.empty(n, B, nh, T, 8, device=torch.cuda.current_stream().device, dtype=torch.int32)
+        self.seeds = (ctypes.c_uint64 * n)(*[SEEDS.next() for _ in range(n)])
+
+    def launch(self) -> None:
+        """Issue the draw on the side stream, ordered after the main stream's work so far. Issued at the
+        start of the model forward it runs beside the front end (profiles/r05ag_attn_keep_ahead_ab.txt:
+        issued at the GRU recurrence's launch instead, it slowed the 4-CU recurrence by 20 %)."""
+        if self.ev is not None:
+            return
+        main = torch.cuda.current_stream()
+        if not _Deferred.sides:
+            n_side = max(1, int(os.environ.get("B2P_SIDE_STREAMS", "1")))
+            _Deferred.sides = [torch.cuda.Stream(device=main.device) for _ in range(n_side)]
+        side = _Deferred.sides[0]
+        B, T, nh, p = self.key
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            _lib.call("b2p_attn16_keep_masks", _p(self.masks), ctypes.addressof(self.seeds), self.n, B, T, nh, p,
+                      _st())
+            self.ev = torch.cuda.Event()
+            self.ev.record()
+        self.masks.record_stream(side)
+
+    def join(self) -> None:
+        if not self.joined:
+            self.launch()
+            torch.cuda.current_stream().wait_event(self.ev)
+            self.joined = True
+
+    def take(self, B, T, nh, p):
+        if (B, T, nh, float(p)) != self.key or self.next >= self.n:
+            return None
+        self.join()
+        self.next += 1
+        return self.masks[self.next - 1]
+
+
+@contextlib.contextmanager
+def attn_keep_plan(n_layers, B, T, nh, dh, p_attn, training):
+    """Around a model forward: draw the encoder's attention keep masks ahead (see _KeepPlan) when the
+    fused 16-bit attention with a stored mask will run (bf16 mode, training, p > 0, T' <= 256)."""
+    on = (_KEEP_AHEAD[0] and training and p_attn > 0 and n_layers > 0 and bf16_mode()
+          and attn16_ok(T, dh) and T <= 256 and _KEEP_PLAN[0] is None)
+    if not on:
+        yield
+        return
+    _KEEP_PLAN[0] = _KeepPlan(int(n_layers), int(B), int(T), int(nh), p_attn)
+    _KEEP_PLAN[0].launch()
+    try:
+        yield
+    finally:
+        pl, _KEEP_PLAN[0] = _KEEP_PLAN[0], None
+        pl.join()   # a capture must join the side stream even when no layer took a block
+
+
+def attn_keep_plan_cfg(cfg, brain_encoder, inputs, training):
+    """attn_keep_plan for an encoder config (num_hidden_layers, num_attention_heads, hidden_size,
+    attention_dropout) and the brain encoder's input (B, L, ...): the encoder sees T' =
+    brain_encoder.output_length(L) frames (the B2P2T Unfold; the GRU keeps the length)."""
+    shp = getattr(inputs, "shape", None)
+    if shp is None or len(shp) < 2:
+        return contextlib.nullcontext()
+    T = brain_encoder.output_length(shp[1]) if hasattr(brain_encoder, "output_length") else shp[1]
+    return attn_keep_plan(cfg.num_hidden_layers, shp[0], T, cfg.num_attention_heads,
+                          cfg.hidden_size // cfg.num_attention_heads, cfg.attention_dropout, training)
+
+
+# Where the queued frozen weight gradients go out relative to the GRU recurrence backward (A/B):
+# "after" = flushed after the recurrence launch, ordered after the event before it; "first" = flushed
+# before the recurrence launch; "fork" = the recurrence itself launched on a stream of its own (forked
+# from and joined back into the current stream), the flush after it. All three measured equal step
+# times (base 14.49 / 14.49 / 14.47 ms, Conformer 66.11 / - / 65.96 ms: profiles/r05ak_gru_bwd_mode_ab.txt).
+_GRU_BWD_MODE = os.environ.get("B2P_GRU_BWD_MODE", "after")
+_GRU_STREAM: list = [None]
+
+
+def _gru_bwd_launch(launch) -> None:
+    """Launch a GRU recurrence backward (launch() on the current stream) with the frozen weight
+    gradients flushed beside it (flush_wgrad), in the order _GRU_BWD_MODE selects."""
+    ev = torch.cuda.Event()
+    ev.record()
+    if _GRU_BWD_MODE == "first":
+        flush_wgrad(ev)
+        launch()
+    elif _GRU_BWD_MODE == "fork":
+        main = torch.cuda.current_stream()
+        if _GRU_STREAM[0] is None:
+            _GRU_STREAM[0] = torch.cuda.Stream(device=main.device)
+        gs = _GRU_STREAM[0]
+        gs.wait_event(ev)
+        with torch.cuda.stream(gs):
+            launch()
+            done = torch.cuda.Event()
+            done.record()
+        flush_wgrad(ev)
+        main.wait_event(done)
+    else:
+        launch()
+        flush_wgrad(ev)
+
+
+def _keep_take(B, T, nh, p_attn):
+    pl = _KEEP_PLAN[0]
+    return None if pl is None or p_attn <= 0 else pl.take(B, T, nh, p_attn)
+
+
 def _attn16_fwd(qkv16, B, T, nh, dh, p_attn, seed, want_mask=False):
     """qkv16 (B*T, 3D) bf16 -> O16 (B*T, D) bf16, lse2 (B, nh, T) f32 (fused, scores stay on-chip)
     [, mask: the dropout keep bits (B, nh, T, 8) int32 for the backward, None without dropout]."""
     dev = qkv16.device
     O16 = torch.empty(B * T, nh * dh, device=dev, dtype=BF16)
     lse2 = torch.empty(B, nh, T, device=dev)
+    mask = _keep_take(B, T, nh, p_attn) if want_mask else None
+    if mask is not None:
+        _lib.call("b2p_attn16_fwd_keep", _p(qkv16), _p(O16), _p(lse2), B, T, nh, dh, float(dh ** -0.5),
+                  float(p_attn), mask.data_ptr(), _st())
+        return O16, lse2, mask
     # the stored keep mask covers T' <= 256 (32 bytes a row); longer windows rehash in the backward
     mask = torch.empty(B, nh, T, 8, device=dev, dtype=torch.int32) if (want_mask and p_attn > 0 and T <= 256) else None
     _lib.call("b2p_attn16_fwd", _p(qkv16), _p(O16), _p(lse2), B, T, nh, dh, float(dh ** -0.5), float(p_attn),
@@ -2141,6 +2267,11 @@ def _attn16_fwd_f16(qkvh, B, T, nh, dh, p_attn, seed):
     Oh = torch.empty(B * T, nh * dh, device=dev, dtype=torch.float16)
     Ob = torch.empty(B * T, nh * dh, device=dev, dtype=BF16)
     lse2 = torch.empty(B, nh, T, device=dev)
+    mask = _keep_take(B, T, nh, p_attn)
+    if mask is not None:
+        _lib.call("b2p_attn16_fwd_f16_keep", _p(qkvh), _p(Oh), _p(Ob), _p(lse2), B, T, nh, dh, float(dh ** -0.5),
+                  float(p_attn), mask.data_ptr(), _st())
+        return Oh, Ob, lse2, mask
     mask = torch.empty(B, nh, T, 8, device=dev, dtype=torch.int32) if (p_attn > 0 and T <= 256) else None
     _lib.call("b2p_attn16_fwd_f16", _p(qkvh), _p(Oh), _p(Ob), _p(lse2), B, T, nh, dh, float(dh ** -0.5),
               float(p_attn), seed, None if mask is None else mask.data_ptr(), _st())

@@ -90,6 +90,10 @@ class B2P2TModel(B2TModel):
             return out
         return self.neural_decoder.forward(preprocessed_batch)
 
+    def output_length(self, L: int) -> int:
+        """Frames of the Unfold((k,1), stride) of L input bins (Fn.Unfolded.T): what the encoder sees."""
+        return (L - self.config.unfolder_kernel_len) // self.config.unfolder_stride_len + 1
+
     @classmethod
     def get_in_size_after_preprocessing(cls, unfolder_kernel_len: int):
         return 256 * unfolder_kernel_len

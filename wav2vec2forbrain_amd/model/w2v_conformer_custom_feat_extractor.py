@@ -181,6 +181,11 @@ class W2VConformerBrainEncoderModel(B2TModel):
         self.process_group = None
 
     def forward(self, batch: B2tSampleBatch):
+        # the encoder's attention dropout keep masks drawn on a side stream beside the GRU (Fn.attn_keep_plan)
+        with Fn.attn_keep_plan_cfg(self.w2v_encoder.config, self.brain_encoder, batch.input, self.training):
+            return self._forward(batch)
+
+    def _forward(self, batch: B2tSampleBatch):
         # the brain encoder's forward GEMMs on fp16 operands too: its GRU features feed every later
         # step's update (bf16 operands there put 3.7e-4 relative into the step-1 loss, tools/traj_err.py)
         with Fn.forward_f16(self.forward_f16):

@@ -273,6 +273,11 @@ class W2VBrainEncoderModel(B2TModel):
         self.forward_f16 = True
 
     def forward(self, batch: B2tSampleBatch):
+        # the encoder's attention dropout keep masks drawn on a side stream beside the GRU (Fn.attn_keep_plan)
+        with Fn.attn_keep_plan_cfg(self.w2v_encoder.config, self.brain_encoder, batch.input, self.training):
+            return self._forward(batch)
+
+    def _forward(self, batch: B2tSampleBatch):
         with Fn.forward_f16(self.brain_forward_f16):
             encoded_brain = self.brain_encoder.forward(batch)
         targets = batch.target
