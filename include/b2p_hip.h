@@ -538,6 +538,13 @@ int b2p_accum_recs(const int64_t* recs, int ntensors, b2p_stream_t stream);
 int b2p_accum_rows_recs(const int64_t* recs, int ntensors, b2p_stream_t stream);
 
 /* dropout with an extra output scale: y = x * keep(seed, i) * scale / (1-p) (macaron half-step) */
+/* out_lens[i] = (int32)((float)(in_lens[i] - kernel) / (float)stride): the unfolded input lengths of
+ * src/model/b2p2t_model.py:170-173 (int64 lengths, float32 true division, truncation), one launch. */
+int b2p_unfold_lens(const int64_t* in_lens, int32_t* out_lens, int64_t n, int64_t kernel, int64_t stride,
+                    b2p_stream_t stream);
+/* out[i] = targets[i] < 1 ? -100 : targets[i] (int64): the CTC targets of
+ * src/model/w2v_custom_feat_extractor.py:70 / w2v_conformer_custom_feat_extractor.py:41, one launch. */
+int b2p_ctc_targets(const int64_t* targets, int64_t* out, int64_t n, b2p_stream_t stream);
 /* y = x * (*s) with the scalar s read on the device (16-B aligned x, y): the CTC loss backward's
  * grad * grad_output (torch.autograd seeds a reduced loss with a device scalar). */
 int b2p_scale_by_device_scalar(const float* x, const float* s, float* y, int64_t n, b2p_stream_t stream);

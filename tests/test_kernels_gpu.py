@@ -1293,3 +1293,20 @@ def test_conformer_conv_module_bn16_bitwise():
     assert res[0][1].keys() == res[1][1].keys()
     for n in res[0][1]:
         assert torch.equal(res[0][1][n], res[1][1][n]), n
+
+
+def test_unfold_lens_and_ctc_targets_match_reference_expressions():
+    """b2p_unfold_lens / b2p_ctc_targets (one launch each in the step) against the reference's own torch
+    expressions on the same device tensors (src/model/b2p2t_model.py:170-173,
+    src/model/w2v_custom_feat_extractor.py:70): bitwise, including lengths below the kernel size
+    (negative quotients truncate toward zero) and targets at and below the blank."""
+    Fn = _fn()
+    g = torch.Generator().manual_seed(3)
+    lens = torch.cat([torch.randint(-50, 5000, (997,), generator=g), torch.tensor([0, 1, 13, 14, 15, 16, 2 ** 24 + 3])])
+    lens = lens.cuda()
+    for k, s in ((14, 4), (32, 4), (1, 1), (7, 3)):
+        ref = ((lens - k) / s).to(torch.int32)
+        assert torch.equal(Fn.unfold_lens(lens, k, s), ref), (k, s)
+    t = torch.randint(-5, 41, (32, 77), generator=g).cuda()
+    assert torch.equal(Fn.ctc_targets(t), torch.where(t < 1, torch.tensor(-100, device="cuda"), t))
+    assert torch.equal(Fn.ctc_targets(t[:, :5]), t[:, :5].masked_fill(t[:, :5] < 1, -100))   # non-contiguous view

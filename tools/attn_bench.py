@@ -41,3 +41,19 @@ for kind in ("f16", "bf16"):
         tb = timeit(lambda: Fn._attn16_bwd(q16, dO, lse2, B, T, nh, dh, p, 5, mask=mask))
         print(f"attn16[{kind}] B={B} T={T} nh={nh} p={p}: fwd {tf:.1f} us ({fl / tf / 1e6:.0f} TFLOP/s), "
               f"bwd {tb:.1f} us ({2.5 * fl / tb / 1e6:.0f} TFLOP/s)", flush=True)
+# the bf16 mode's forward with the keep bits drawn ahead (functional.attn_keep_plan: b2p_attn16_keep_masks
+# + b2p_attn16_fwd_f16_keep, DM 3), and the draw itself for one layer
+import ctypes
+q16 = q.to(torch.float16)
+masks = torch.empty(1, B, nh, T, 8, device="cuda", dtype=torch.int32)
+seeds = (ctypes.c_uint64 * 1)(5)
+draw = lambda: Fn._lib.call("b2p_attn16_keep_masks", masks.data_ptr(), ctypes.addressof(seeds), 1, B, T, nh, 0.1, Fn._st())
+draw()
+Oh = torch.empty(B * T, nh * dh, device="cuda", dtype=torch.float16)
+Ob = torch.empty(B * T, nh * dh, device="cuda", dtype=torch.bfloat16)
+lse2 = torch.empty(B, nh, T, device="cuda")
+fk = lambda: Fn._lib.call("b2p_attn16_fwd_f16_keep", q16.data_ptr(), Oh.data_ptr(), Ob.data_ptr(), lse2.data_ptr(), B, T,
+                          nh, dh, float(dh ** -0.5), 0.1, masks[0].data_ptr(), Fn._st())
+tf, td = timeit(fk), timeit(draw)
+print(f"attn16[f16, keep bits read] B={B} T={T} nh={nh} p=0.1: fwd {tf:.1f} us ({fl / tf / 1e6:.0f} TFLOP/s); "
+      f"keep-mask draw {td:.1f} us per layer", flush=True)

@@ -148,6 +148,8 @@ _SIGS = {
     "b2p_posconv16_wgrad": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_i64, c_i64, c_p]),
     "b2p_seed_epoch_step": (c_i32, [c_p, c_p]),
     "b2p_scale_by_device_scalar": (c_i32, [c_p, c_p, c_p, c_i64, c_p]),
+    "b2p_unfold_lens": (c_i32, [c_p, c_p, c_i64, c_i64, c_i64, c_p]),
+    "b2p_ctc_targets": (c_i32, [c_p, c_p, c_i64, c_p]),
     "b2p_dropout_scaled": (c_i32, [c_p, c_p, c_i64, c_f32, c_u64, c_f32, c_p]),
     "b2p_drop_cast_colsum_parts": (c_i64, [c_i64]),
     "b2p_drop_cast_colsum": (c_i32, [c_p, c_p, c_p, c_i64, c_i64, c_f32, c_u64, c_f32, c_p]),

@@ -1019,6 +1019,44 @@ extern "C" int b2p_colsum_batched(const float* X, const float* Y, int64_t batch,
   return colsum_impl(X, Y, batch, M, N, ld, bstride, mode, out, accumulate, partial, (hipStream_t)stream);
 }
 
+// ------------------------------------------------------------------ batch bookkeeping on the device
+// The reference's own per-batch tensor ops on the step's path, one launch each instead of torch's 2-3
+// elementwise launches (and the masked_fill copy):
+//   out_lens = ((in_lens - k) / s).to(int32)   (src/model/b2p2t_model.py:170-173: int64 minus int, true
+//              division in float32, truncation toward zero)
+//   out_t    = where(t < 1, -100, t)            (src/model/w2v_custom_feat_extractor.py:70,
+//              w2v_conformer_custom_feat_extractor.py:41)
+__global__ void unfold_lens_k(const int64_t* __restrict__ in, int32_t* __restrict__ out, int64_t n, int64_t k, float s) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (int32_t)(__fdiv_rn((float)(in[i] - k), s));
+}
+__global__ void ctc_targets_k(const int64_t* __restrict__ t, int64_t* __restrict__ out, int64_t n) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) {
+    const int64_t v = t[i];
+    out[i] = v < 1 ? -100 : v;
+  }
+}
+
+extern "C" int b2p_unfold_lens(const int64_t* in_lens, int32_t* out_lens, int64_t n, int64_t kernel, int64_t stride,
+                               b2p_stream_t stream) {
+  B2P_CHECK_ARG(in_lens && out_lens, "unfold_lens: NULL pointer");
+  B2P_CHECK_ARG(stride > 0, "unfold_lens: stride must be positive");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(unfold_lens_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, in_lens, out_lens, n, kernel,
+                     (float)stride);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int b2p_ctc_targets(const int64_t* targets, int64_t* out, int64_t n, b2p_stream_t stream) {
+  B2P_CHECK_ARG(targets && out, "ctc_targets: NULL pointer");
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(ctc_targets_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, targets, out, n);
+  B2P_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int b2p_scale_by_device_scalar(const float* x, const float* s, float* y, int64_t n, b2p_stream_t stream) {
   B2P_CHECK_ARG(x && s && y, "scale_by_device_scalar: NULL pointer");
   B2P_CHECK_ARG(((uintptr_t)x & 15u) == 0 && ((uintptr_t)y & 15u) == 0, "scale_by_device_scalar: x / y 16-B aligned");

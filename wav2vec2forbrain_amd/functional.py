@@ -2655,6 +2655,41 @@ class _CTC(torch.autograd.Function):
         return g, None, None, None, None
 
 
+def unfold_lens(in_lens, kernel: int, stride: int):
+    """((in_lens - kernel) / stride).to(torch.int32) (reference src/model/b2p2t_model.py:170-173) in one
+    launch (b2p_unfold_lens) for device int64 lengths; any other input takes the reference's expression."""
+    if not (in_lens.is_cuda and in_lens.dtype == torch.int64):
+        return ((in_lens - kernel) / stride).to(torch.int32)
+    x = in_lens.contiguous()
+    out = torch.empty(x.shape, device=x.device, dtype=torch.int32)
+    _lib.call("b2p_unfold_lens", x.data_ptr(), out.data_ptr(), x.numel(), int(kernel), int(stride), _st())
+    return out
+
+
+def ctc_targets(targets):
+    """targets.masked_fill(targets < 1, -100) (reference src/model/w2v_custom_feat_extractor.py:70) in one
+    launch (b2p_ctc_targets) for device int64 targets; any other input takes the reference's expression."""
+    if not (targets.is_cuda and targets.dtype == torch.int64):
+        return targets.masked_fill(targets < 1, -100)
+    t = targets.contiguous()
+    out = torch.empty_like(t)
+    _lib.call("b2p_ctc_targets", t.data_ptr(), out.data_ptr(), t.numel(), _st())
+    return out
+
+
+def loss_seed(loss):
+    """The gradient autograd seeds loss.backward() with (ones_like(loss)), one cached device tensor per
+    (device, dtype): a captured step then holds no fill launch for it."""
+    key = (loss.device, loss.dtype, tuple(loss.shape))
+    t = _LOSS_SEEDS.get(key)
+    if t is None:
+        t = _LOSS_SEEDS[key] = torch.ones(loss.shape, device=loss.device, dtype=loss.dtype)
+    return t
+
+
+_LOSS_SEEDS: dict = {}
+
+
 def ctc_loss(logits, targets, in_lens, tgt_lens, blank=0):
     """log_softmax(logits) -> nn.CTCLoss(blank, reduction='mean', zero_infinity=True);
     logits (B,T,C) batch-first. targets int64 (B,S); in_lens int32; tgt_lens int64."""

@@ -82,8 +82,9 @@ class B2P2TModel(B2TModel):
         strided_inputs = Fn.Unfolded(s, self.config.unfolder_kernel_len, self.config.unfolder_stride_len)
         preprocessed_batch = batch.copy_and_change(input=strided_inputs)
         if hasattr(batch, "input_lens"):
-            processed_in_lens = ((batch.input_lens - self.config.unfolder_kernel_len)
-                                 / self.config.unfolder_stride_len).to(torch.int32)
+            # ((input_lens - k) / stride).to(torch.int32), reference :170-173
+            processed_in_lens = Fn.unfold_lens(batch.input_lens, self.config.unfolder_kernel_len,
+                                               self.config.unfolder_stride_len)
             preprocessed_batch.input_lens = processed_in_lens
             out = self.neural_decoder.forward(preprocessed_batch)
             out.logit_lens = processed_in_lens

@@ -192,7 +192,7 @@ class W2VConformerBrainEncoderModel(B2TModel):
             encoded_brain = self.brain_encoder.forward(batch)
         targets = batch.target
         assert targets is not None
-        targets = targets.masked_fill(targets < 1, -100)
+        targets = Fn.ctc_targets(targets)   # reference: where(targets < 1, -100, targets)
         import torch.distributed as dist
         from ..train.ddp import dp_active
         sync = self.training and self.sync_batchnorm and dp_active(self.process_group)

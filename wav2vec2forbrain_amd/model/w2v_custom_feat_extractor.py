@@ -282,7 +282,7 @@ class W2VBrainEncoderModel(B2TModel):
             encoded_brain = self.brain_encoder.forward(batch)
         targets = batch.target
         assert targets is not None
-        targets = targets.masked_fill(targets < 1, -100)
+        targets = Fn.ctc_targets(targets)   # reference: where(targets < 1, -100, targets)
         with Fn.forward_f16(self.forward_f16):
             w2v_output, hidden_states = self.w2v_encoder.forward(encoded_brain.logits)
         ctc_loss = (

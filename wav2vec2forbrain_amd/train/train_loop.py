@@ -256,7 +256,7 @@ class Trainer:
         with torch.enable_grad():
             outputs = self.model.forward(batch)
         loss = cast(torch.Tensor, outputs.loss)
-        loss.backward()
+        loss.backward(Fn.loss_seed(loss))   # = loss.backward(): the seed is a cached ones tensor
         Fn.join_wgrad()
         if in_graph and self.reducer is not None:
             return _detached(outputs)
