@@ -1,0 +1,16 @@
+set -u
+# frozen LayerNorm parameter gradients left as block partials for the side stream's batched accumulation
+# (B2P_LN_LAZY): model / trainer / LayerDrop / wgrad tests, step-time A/B
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
+O=gpurun_out/r05an; mkdir -p $O
+timeout -k 10 700 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_model_gpu.py tests/test_trainer_gpu.py \
+  tests/test_layerdrop_gpu.py tests/test_wgrad_batch_gpu.py > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+run() {  # tag config env...
+  local tag=$1 C=$2; shift 2
+  env "$@" timeout -k 10 300 python3 bench.py --config $C --steps 20 --warmup 5 --no-cpu-baseline --no-parity \
+    --no-conformer --no-extra --no-roofline > $O/b_$tag.json 2> $O/b_$tag.err || { tail -5 $O/b_$tag.err; return 1; }
+  echo "$tag $(python3 -c "import json; print(json.loads(open('$O/b_$tag.json').read().strip().splitlines()[-1])['ms_per_step'])") ms"
+}
+run base_lz1 base && run base_lz0 base B2P_LN_LAZY=0 && run base_lz1b base && \
+run conf_lz1 conformer && run conf_lz0 conformer B2P_LN_LAZY=0 && run conf_lz1b conformer || exit 1

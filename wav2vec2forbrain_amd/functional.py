@@ -1065,19 +1065,42 @@ def _ln_fwd(x2d, g, b, eps, drop_p=0.0, seed=0):
     return y, mean, rstd
 
 
+_LN_BWD_ROWS = 16   # rows per block of ln_bwd_k (csrc/elementwise.hip LN_BWD_ROWS): the partials' row count
+_LN_LAZY = os.environ.get("B2P_LN_LAZY", "1") != "0"   # B2P_LN_LAZY=0: reduce them on the main stream (A/B)
+
+
+def _ln_lazy(lazy, need_params, dbias_in) -> bool:
+    """The LayerNorm backward leaves its parameter gradients as block partials (ColsumParts, finished in
+    the side stream's batched accumulation) when every parameter they belong to is a deferred frozen
+    one: lazy = (gamma, beta, the dropout-input bias or None), matching dbias_in."""
+    return (_LAZY_COLSUM and _LN_LAZY and lazy is not None and need_params and (dbias_in is None) == (lazy[2] is None)
+            and all(_defer_ok(q) for q in lazy if q is not None))
+
+
+def _ln_parts(ws, rows, cols, q):
+    nblk = -(-rows // _LN_BWD_ROWS)
+    return ColsumParts(ws[q * nblk * cols:(q + 1) * nblk * cols].view(nblk, cols))
+
+
 def _ln_bwd(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, seed=0, in_drop_p=-1.0,
-            in_seed=0, dbias_in=None, dx_accum2=None):
-    """dx_accum2: a second accumulator added to dx alone (LayerDrop's skip gradient, _skip_take)."""
+            in_seed=0, dbias_in=None, dx_accum2=None, lazy=None):
+    """dx_accum2: a second accumulator added to dx alone (LayerDrop's skip gradient, _skip_take).
+    lazy (see _ln_lazy): dg / db come back as ColsumParts (no ln_param_reduce launch on the main stream),
+    and the result gains a fifth entry, the dropout-input bias gradient (dbias_in or its ColsumParts)."""
     rows, cols = x.shape
+    lz = _ln_lazy(lazy, need_params, dbias_in)
     dx = torch.empty_like(x)
-    dg = torch.empty(cols, device=x.device) if need_params else None
-    db = torch.empty(cols, device=x.device) if need_params else None
+    dg = torch.empty(cols, device=x.device) if need_params and not lz else None
+    db = torch.empty(cols, device=x.device) if need_params and not lz else None
     ws = torch.empty(int(_lib.load().b2p_layernorm_bwd_workspace(rows, cols)), device=x.device)
     dxd = torch.empty_like(x) if in_drop_p >= 0.0 else None
     _lib.call("b2p_layernorm_bwd_acc2", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows,
               cols, _p(dx_accum), _p(dx_accum2), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed,
-              _p(dbias_in), None, _p(ws), _st())
-    return dx, dg, db, dxd
+              None if lz else _p(dbias_in), None, _p(ws), _st())
+    if lz:
+        dg, db = _ln_parts(ws, rows, cols, 0), _ln_parts(ws, rows, cols, 1)
+        dbias_in = _ln_parts(ws, rows, cols, 2) if dbias_in is not None else None
+    return (dx, dg, db, dxd) if lazy is None else (dx, dg, db, dxd, dbias_in)
 
 
 
@@ -1267,19 +1290,24 @@ def _ln_fwd16(x2d, g, b, eps, drop_p=0.0, seed=0):
 
 
 def _ln_bwd16(dy, x, g, mean, rstd, need_params=True, dx_accum=None, drop_p=0.0, seed=0, in_drop_p=-1.0,
-              in_seed=0, dbias_in=None, dx_accum2=None):
-    """as _ln_bwd, plus d16 = bf16(dx_dropped if in_drop_p >= 0 else dx)"""
+              in_seed=0, dbias_in=None, dx_accum2=None, lazy=None):
+    """as _ln_bwd, plus d16 = bf16(dx_dropped if in_drop_p >= 0 else dx) (lazy: a sixth entry, the
+    dropout-input bias gradient)"""
     rows, cols = x.shape
+    lz = _ln_lazy(lazy, need_params, dbias_in)
     dx = torch.empty_like(x)
-    dg = torch.empty(cols, device=x.device) if need_params else None
-    db = torch.empty(cols, device=x.device) if need_params else None
+    dg = torch.empty(cols, device=x.device) if need_params and not lz else None
+    db = torch.empty(cols, device=x.device) if need_params and not lz else None
     ws = torch.empty(int(_lib.load().b2p_layernorm_bwd_workspace(rows, cols)), device=x.device)
     dxd = torch.empty_like(x) if in_drop_p >= 0.0 else None
     d16 = torch.empty(rows, cols, device=x.device, dtype=BF16)
     _lib.call("b2p_layernorm_bwd_acc2", _p(dy), _p(x), _p(g), _p(mean), _p(rstd), _p(dx), _p(dg), _p(db), rows,
               cols, _p(dx_accum), _p(dx_accum2), float(drop_p), seed, _p(dxd), float(max(in_drop_p, 0.0)), in_seed,
-              _p(dbias_in), _p(d16), _p(ws), _st())
-    return dx, dg, db, dxd, d16
+              None if lz else _p(dbias_in), _p(d16), _p(ws), _st())
+    if lz:
+        dg, db = _ln_parts(ws, rows, cols, 0), _ln_parts(ws, rows, cols, 1)
+        dbias_in = _ln_parts(ws, rows, cols, 2) if dbias_in is not None else None
+    return (dx, dg, db, dxd, d16) if lazy is None else (dx, dg, db, dxd, d16, dbias_in)
 
 
 # =====================================================================================
@@ -2528,10 +2556,10 @@ class _EncoderLayer16(torch.autograd.Function):
         w1t16, w2t16, wot16, wqkvt16 = weight16t(w1), weight16t(w2), weight16t(wo), weight16t(wq, wk, wv)
         # LN2 backward -> dy2 ; dz2 = dropout-mask(dy2) (output dropout of the FFN), bf16 copy dz2_16
         db2 = torch.empty(D, device=dev) if ng[15] else None
-        dy2, dg2, dbe2, _dz2, dz2_16 = _ln_bwd16(dout, y2, g2, m2, r2, True, in_drop_p=p_hid, in_seed=seeds[3],
-                                                 dbias_in=db2)
-        del _dz2
         prm = ctx.prm
+        dy2, dg2, dbe2, _dz2, dz2_16, db2 = _ln_bwd16(dout, y2, g2, m2, r2, True, in_drop_p=p_hid, in_seed=seeds[3],
+                                                      dbias_in=db2, lazy=(prm[14], prm[15], prm[13] if ng[15] else None))
+        del _dz2
         dw2 = None
         if ng[14]:
             if _defer_ok(w2):
@@ -2559,8 +2587,9 @@ class _EncoderLayer16(torch.autograd.Function):
         del dpre16
         # LN1 backward -> dy1 ; dz1 = dropout-mask(dy1) (attention output dropout)
         dbo = torch.empty(D, device=dev) if ng[9] else None
-        dy1, dg1, dbe1, _dz1, dz1_16 = _ln_bwd16(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1],
-                                                 dbias_in=dbo, dx_accum2=_skip_take(ctx.skip))
+        dy1, dg1, dbe1, _dz1, dz1_16, dbo = _ln_bwd16(dx1, y1, g1, m1, r1, True, in_drop_p=p_hid, in_seed=seeds[1],
+                                                      dbias_in=dbo, dx_accum2=_skip_take(ctx.skip),
+                                                      lazy=(prm[8], prm[9], prm[7] if ng[9] else None))
         del _dz1
         dwo = None
         if ng[8]:
@@ -2989,7 +3018,8 @@ class _FFNBlock(torch.autograd.Function):
             colsum(dpre, NT, F, db1)
         dh = torch.empty(NT, D, device=dev)
         mm_nn(dpre, w1, dh)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip))
+        dx, dg, db, _, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip),
+                                   lazy=(ctx.prm[0], ctx.prm[1], None))
         return (dx.view(ctx.shape), *_defer_small(ctx.prm, (dg, db, dw1, db1, dw2, db2)), None)
 
     @staticmethod
@@ -3018,7 +3048,8 @@ class _FFNBlock(torch.autograd.Function):
         dw1 = _wgrad16(w1, ng[3], dpre16, F, h if h.dtype == BF16 else cast16(h), D, NT)
         dh = torch.empty(NT, D, device=dev)
         gemm(NT, D, F, op(dpre16, 0, F, True), op(weight16t(w1), 0, F, True), dh, D)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip))
+        dx, dg, db, _, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip),
+                                   lazy=(ctx.prm[0], ctx.prm[1], None))
         return (dx.view(ctx.shape), *_defer_small(ctx.prm, (dg, db, dw1, db1, dw2, db2)), None)
 
 
@@ -3186,7 +3217,8 @@ class _ConformerAttnBlock(torch.autograd.Function):
         else:
             for i, w in enumerate((wq, wk, wv)):
                 gemm(NT, D, D, op(dqkv, i * D, 3 * D, True), op(w, 0, D, False), dh, D, beta=0.0 if i == 0 else 1.0)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip))
+        dx, dg, db, _, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip),
+                                   lazy=(ctx.prm[0], ctx.prm[1], None))
         return (dx.view(B, T, D), *_defer_small(ctx.prm, (dg, db, *grads, dwo, dbo)), None, None, None)
 
     @staticmethod
@@ -3246,7 +3278,8 @@ class _ConformerAttnBlock(torch.autograd.Function):
             gemm(NT, D, D, op(dqkv16, 2 * D, 3 * D, True), op(weight16t(wv), 0, D, True), dh, D, beta=1.0)
         else:
             gemm(NT, D, 3 * D, op(dqkv16, 0, 3 * D, True), op(weight16t(wq, wk, wv), 0, 3 * D, True), dh, D)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip))
+        dx, dg, db, _, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, dx_accum2=_skip_take(ctx.skip),
+                                   lazy=(ctx.prm[0], ctx.prm[1], None))
         return (dx.view(B, T, D), *_defer_small(ctx.prm, (dg, db, *grads, dwo, dbo)), None, None, None)
 
 
@@ -3431,7 +3464,7 @@ class _ConvModule(torch.autograd.Function):
                 dpw1 = torch.empty_like(w_pw1)
                 mm_tn(da, h, dpw1.view(2 * D, D))
             mm_nn(da, w_pw1.view(2 * D, D), dh)
-        dx, dg, db, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy)
+        dx, dg, db, _, _ = _ln_bwd(dh, x2, g, mean, rstd, True, dx_accum=dy, lazy=(ctx.prm[0], ctx.prm[1], None))
         return (dx.view(B, T, D), *_defer_small(ctx.prm, (dg, db, dpw1, ddw, dbn_g, dbn_b, dpw2)), None, None, None)
 
 
