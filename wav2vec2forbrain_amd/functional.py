@@ -368,6 +368,16 @@ def _defer_wgemm_rows(ps, fn, *tensors) -> None:
     _Deferred.queue.append((_gate_wrap(run), tensors, id(ps[0]), None))
 
 
+def _defer_bias_rows(ps, x, M, N) -> bool:
+    """The column sums of x (M x N fp32, N = the concatenated lengths of the bias vectors ps) as the
+    gradients of frozen biases: queued for the side stream (the same b2p_colsum launch, accumulating into
+    their .grad) instead of run on the main stream. False when a bias is not a deferred frozen one."""
+    if not (_LAZY_COLSUM and all(_defer_ok(q) for q in ps)):
+        return False
+    _defer_wgemm_rows(ps, lambda out, beta: colsum(x, M, N, out, accumulate=beta == 1.0), x)
+    return True
+
+
 def _defer_wgemm(p, fn, *tensors) -> None:
     """Queue fn(out, beta): a weight-gradient GEMM writing (beta 0) or accumulating (beta 1) p.grad."""
     prec = _prec()
@@ -2617,7 +2627,10 @@ class _EncoderLayer16(torch.autograd.Function):
             for i in range(3):
                 if ng[2 + 2 * i]:
                     grads_w[2 * i] = dwqkv[i * D:(i + 1) * D]
-        if any(ctx.has_b[i] and ng[3 + 2 * i] for i in range(3)):
+        if all(ctx.has_b[i] and ng[3 + 2 * i] for i in range(3)) and _defer_bias_rows((prm[1], prm[3], prm[5]), dqkv, NT,
+                                                                                        3 * D):
+            pass   # frozen Q/K/V biases: their column sums run on the side stream
+        elif any(ctx.has_b[i] and ng[3 + 2 * i] for i in range(3)):
             dbqkv = torch.empty(3 * D, device=dev)
             colsum(dqkv, NT, 3 * D, dbqkv)
             for i in range(3):
@@ -3257,12 +3270,15 @@ class _ConformerAttnBlock(torch.autograd.Function):
         grads = []
         need_b = [ctx.has_b[i] and ng[4 + 2 * i] for i in range(3)]
         dbqkv = None
-        if all(need_b):   # the three bias gradients as one column reduction over dqkv
+        b_side = all(need_b) and _defer_bias_rows((ctx.prm[3], ctx.prm[5], ctx.prm[7]), dqkv, NT, 3 * D)
+        if all(need_b) and not b_side:   # the three bias gradients as one column reduction over dqkv
             dbqkv = torch.empty(3 * D, device=dev)
             colsum(dqkv, NT, 3 * D, dbqkv)
         for i, (w, src16) in enumerate(((wq, hr16), (wk, hr16), (wv, h16))):
             gb = None
-            if dbqkv is not None:
+            if b_side:
+                pass
+            elif dbqkv is not None:
                 gb = dbqkv[i * D:(i + 1) * D]
             elif need_b[i]:
                 gb = torch.empty(D, device=dev)
