@@ -378,6 +378,18 @@ def _defer_bias_rows(ps, x, M, N) -> bool:
     return True
 
 
+def _defer_dwconv_wgrad(w, u, dc, B, T, D, K) -> None:
+    """The depthwise-conv weight gradient of a frozen Conformer conv module (b2p_dwconv_bwd with no input
+    gradient: tile partials, their column sum, the [C][K] transpose) queued for the side stream; the
+    result joins the flush's batched accumulation into w.grad."""
+    def run():
+        ws = torch.empty(int(_lib.load().b2p_dwconv_bwd_workspace(B, T, D, K)), device=u.device)
+        g = torch.empty_like(w)
+        _lib.call("b2p_dwconv_bwd", _p(u), _p(w), _p(dc), None, _p(g), B, T, D, K, _p(ws), _st())
+        _defer_acc(w, g)
+    _Deferred.queue.append((_gate_wrap(run), (u, dc), id(w), None))
+
+
 def _defer_wgemm(p, fn, *tensors) -> None:
     """Queue fn(out, beta): a weight-gradient GEMM writing (beta 0) or accumulating (beta 1) p.grad."""
     prec = _prec()
@@ -2068,15 +2080,27 @@ def _posconv16_bwd(ctx, e16, wg, wv, w, norms, pre, dxsum, dlg, dlb):
     dcb = torch.empty(O, device=dev)
     colsum(part, B, D, dcb)
     dg = dv = None
-    if ng[1] or ng[2]:
+
+    def wgrad():
         dwp = torch.empty(O, K * Ig, device=dev)
         _lib.call("b2p_posconv16_wgrad", _p(dpre16), _p(e16), _p(dwp), B, T, D, groups, _st())
         dw = torch.empty_like(wv)
         _lib.call("b2p_conv_weight_permute", _p(dwp), _p(dw), O, Ig, K, 1, _st())
         ws = torch.empty(int(_lib.load().b2p_weight_norm_workspace(O, Ig, K)), device=dev)
-        dg = torch.empty_like(wg)
-        dv = torch.empty_like(wv)
-        _lib.call("b2p_weight_norm_bwd", _p(wg), _p(wv), _p(norms), _p(dw), _p(dg), _p(dv), O, Ig, K, _p(ws), _st())
+        g_, v_ = torch.empty_like(wg), torch.empty_like(wv)
+        _lib.call("b2p_weight_norm_bwd", _p(wg), _p(wv), _p(norms), _p(dw), _p(g_), _p(v_), O, Ig, K, _p(ws), _st())
+        return g_, v_
+
+    if ng[1] and ng[2] and _LAZY_COLSUM and _defer_ok(ctx.prm[0]) and _defer_ok(ctx.prm[1]):
+        # frozen weight-normed pos-conv: its weight gradient (conv wgrad, permute, weight-norm backward)
+        # runs on the side stream and joins the flush's batched accumulation
+        def run():
+            g_, v_ = wgrad()
+            _defer_acc(ctx.prm[0], g_)
+            _defer_acc(ctx.prm[1], v_)
+        _Deferred.queue.append((_gate_wrap(run), (dpre16, e16, norms), id(ctx.prm[0]), None))
+    elif ng[1] or ng[2]:
+        dg, dv = wgrad()
     # frozen parameters' gradients join the batched side-stream accumulation (no autograd adds)
     dg, dv, dcb, dlg, dlb = _defer_small(ctx.prm, (dg, dv, dcb, dlg, dlb))
     return (de if ng[0] else None), dg, dv, dcb, dlg, dlb, None, None, None, None
@@ -3463,7 +3487,12 @@ class _ConvModule(torch.autograd.Function):
             _lib.call("b2p_batchnorm_bwd", _p(ds), _p(pre), _p(c), _p(bm), _p(br), _p(bn_g), _p(dc), _p(dbn_g),
                       _p(dbn_b), NT, D, act, _p(ws), _st())
         du = torch.empty(NT, D, device=dev)
-        ddw = torch.empty_like(w_dw) if ng[4] else None
+        ddw = None
+        if ng[4]:
+            if _defer_ok(w_dw) and _LAZY_COLSUM:
+                _defer_dwconv_wgrad(w_dw, u, dc, B, T, D, K)   # frozen taps: their three launches on the side stream
+            else:
+                ddw = torch.empty_like(w_dw)
         wsd = torch.empty(int(_lib.load().b2p_dwconv_bwd_workspace(B, T, D, K)), device=dev)
         _lib.call("b2p_dwconv_bwd", _p(u), _p(w_dw), _p(dc), _p(du), _p(ddw), B, T, D, K, _p(wsd), _st())
         dh = torch.empty(NT, D, device=dev)
