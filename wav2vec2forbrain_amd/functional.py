@@ -187,6 +187,9 @@ def _prec_follow(cls):
 # accumulate into p.grad in the GEMM epilogue (beta = 1) instead of autograd's separate add.
 # join_wgrad() orders the side stream back into the main stream (train step, optimizer).
 _DIAG_SKIP_ACC = os.environ.get("B2P_DIAG_SKIP_SMALL_ACC") == "1"   # diagnostic only
+# diagnostic only (never a bench setting): drop the queued frozen weight-gradient launches, to measure how
+# much of the step's tail the side stream holds
+_DIAG_SKIP_WGRAD = os.environ.get("B2P_DIAG_SKIP_WGRAD") == "1"
 # workgroups a 128 x 128 split-K GEMM aims for (the split count is capped at one slice per 1024 of K)
 _SPLITK_WGS = int(os.environ.get("B2P_SPLITK_WGS", "512"))
 _PP_SPLIT = os.environ.get("B2P_PP_SPLIT", "0") == "1"   # every eligible split-K GEMM on the ping-pong kernel
@@ -619,6 +622,8 @@ def flush_wgrad(after=None) -> None:
     if _WGRAD_DEBUG:
         print(f"flush_wgrad: {len(_Deferred.queue)} queued, {len(_Deferred.accs)} accs, after={after is not None}, "
               f"capturing={capturing()}", flush=True)
+    if _DIAG_SKIP_WGRAD:
+        _Deferred.queue.clear()
     if not _Deferred.queue and not _Deferred.accs:
         return
     main = torch.cuda.current_stream()
