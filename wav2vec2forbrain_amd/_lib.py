@@ -183,6 +183,7 @@ _SIGS = {
     "b2p_batchnorm_bwd_dx": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i64, c_p]),
     "b2p_layerdrop_keep": (c_i32, [c_f32, c_u64, c_u64, c_i32, ctypes.POINTER(c_i32)]),
     "b2p_layerdrop_select": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_f32, c_u64, c_p]),
+    "b2p_layerdrop_select_h": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_f32, c_u64, c_p]),
     "b2p_layerdrop_route": (c_i32, [c_p, c_p, c_p, c_i64, c_f32, c_u64, c_p]),
     "b2p_set_gate": (c_i32, [c_p]),
     "b2p_layerdrop_flag": (c_i32, [c_p, c_f32, c_u64, c_p]),

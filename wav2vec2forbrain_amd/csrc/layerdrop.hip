@@ -36,10 +36,13 @@ __device__ __forceinline__ bool dev_keep(uint64_t seed, const uint64_t* epoch, u
 
 // n4 float4 groups; 16-bit copies (optional) as 4 x bf16 per group
 // no __restrict__: out may alias keepv or skipv (in-place select of BatchNorm running statistics)
+// outh (optional): the fp16 copy as well (the next post-LN layer's forward_f16 operand), from skiph /
+// keeph or packed from the selected values
 __global__ void __launch_bounds__(256) ld_select_k(const float4* skipv, const float4* keepv, float4* out,
                                                    const uint2* skip16, const uint2* keep16, uint2* out16,
                                                    int64_t n4, uint32_t thr, uint64_t seed,
-                                                   const uint64_t* __restrict__ epoch) {
+                                                   const uint64_t* __restrict__ epoch, const uint2* skiph = nullptr,
+                                                   const uint2* keeph = nullptr, uint2* outh = nullptr) {
   const bool keep = dev_keep(seed, epoch, thr);
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     const float4 v = keep ? keepv[i] : skipv[i];
@@ -47,6 +50,10 @@ __global__ void __launch_bounds__(256) ld_select_k(const float4* skipv, const fl
     if (out16) {
       const uint2* s16 = keep ? keep16 : skip16;
       out16[i] = s16 ? s16[i] : b2p_pack_bf16x4(v);
+    }
+    if (outh) {
+      const uint2* sh = keep ? keeph : skiph;
+      outh[i] = sh ? sh[i] : b2p_pack16x4(v, true);
     }
   }
 }
@@ -85,6 +92,16 @@ extern "C" int b2p_layerdrop_keep(float p, uint64_t seed, uint64_t epoch, int ha
 extern "C" int b2p_layerdrop_select(const float* skip_val, const float* keep_val, float* out,
                                     const uint16_t* skip16, const uint16_t* keep16, uint16_t* out16, int64_t n,
                                     float p, uint64_t seed, b2p_stream_t stream) {
+  return b2p_layerdrop_select_h(skip_val, keep_val, out, skip16, keep16, out16, nullptr, nullptr, nullptr, n, p, seed,
+                                stream);
+}
+
+extern "C" int b2p_layerdrop_select_h(const float* skip_val, const float* keep_val, float* out,
+                                      const uint16_t* skip16, const uint16_t* keep16, uint16_t* out16,
+                                      const uint16_t* skiph, const uint16_t* keeph, uint16_t* outh, int64_t n,
+                                      float p, uint64_t seed, b2p_stream_t stream) {
+  B2P_CHECK_ARG((((uintptr_t)skiph | (uintptr_t)keeph | (uintptr_t)outh) & 7u) == 0,
+                "layerdrop_select: fp16 buffers must be 8-byte aligned");
   B2P_CHECK_ARG(skip_val && keep_val && out, "layerdrop_select: NULL pointer");
   B2P_CHECK_ARG(p >= 0.f && p < 1.f, "layerdrop_select: p must be in [0,1)");
   B2P_CHECK_ARG(n % 4 == 0, "layerdrop_select: n must be a multiple of 4");
@@ -96,7 +113,8 @@ extern "C" int b2p_layerdrop_select(const float* skip_val, const float* keep_val
   if (n4 <= 0) return 0;
   hipLaunchKernelGGL(ld_select_k, dim3(grid_for(n4)), dim3(256), 0, (hipStream_t)stream, (const float4*)skip_val,
                      (const float4*)keep_val, (float4*)out, (const uint2*)skip16, (const uint2*)keep16, (uint2*)out16,
-                     n4, b2p_dropout_threshold(p), seed, b2p_seed_epoch());
+                     n4, b2p_dropout_threshold(p), seed, b2p_seed_epoch(), (const uint2*)skiph, (const uint2*)keeph,
+                     (uint2*)outh);
   B2P_CHECK_LAUNCH();
   return 0;
 }

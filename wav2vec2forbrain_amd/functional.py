@@ -1835,6 +1835,11 @@ def _b16_of(x):
     return t[1] if t is not None and t[0] == x._version else None
 
 
+def _h16_of(x):
+    t = getattr(x, "_h16", None)
+    return t[1] if t is not None and t[0] == x._version else None
+
+
 class _SkipSlot:
     """The skip-path gradient of one LayerDrop-selected layer, handed from the select's backward to the
     layer Function that consumes the layer input (it adds it to its input gradient inside its last
@@ -1886,11 +1891,16 @@ class _LayerDropSelect(torch.autograd.Function):
         out = torch.empty_like(y)
         out16 = torch.empty(y.shape, device=y.device, dtype=BF16) if bf16_mode() else None
         x16, y16 = (_b16_of(x), _b16_of(y)) if out16 is not None else (None, None)
-        _lib.call("b2p_layerdrop_select", _p(x), _p(y), _p(out), _p(x16), _p(y16), _p(out16), y.numel(), float(p),
-                  seed, _st())
+        # the fp16 copy too when the layer made one (post-LN forward_f16): the next layer reads it uncast
+        yh = _h16_of(y) if out16 is not None and _LD_SELECT_H else None
+        outh = torch.empty(y.shape, device=y.device, dtype=torch.float16) if yh is not None else None
+        _lib.call("b2p_layerdrop_select_h", _p(x), _p(y), _p(out), _p(x16), _p(y16), _p(out16),
+                  _p(_h16_of(x)) if outh is not None else None, _p(yh), _p(outh), y.numel(), float(p), seed, _st())
         ctx.p, ctx.seed, ctx.slot = p, seed, slot
         if out16 is not None:
             attach16(out, out16)
+        if outh is not None:
+            attach16h(out, outh)
         return out
 
     @staticmethod
@@ -1905,6 +1915,7 @@ class _LayerDropSelect(torch.autograd.Function):
         return d_skip, d_keep, None, None, None
 
 
+_LD_SELECT_H = os.environ.get("B2P_LD_SELECT_H", "1") != "0"   # 0: no fp16 copy from the select (A/B)
 LAYERDROP_LOG = None   # tests: when a list, layerdrop_layer appends each layer's draw seed
 # diagnostic only (B2P_GRAPH_LAYERDROP=0): a captured step keeps the host draw made at capture time
 GRAPH_LAYERDROP = os.environ.get("B2P_GRAPH_LAYERDROP", "1") != "0"
