@@ -1770,6 +1770,9 @@ def gru_layer(x, H, ndir, weights, h0=None):
 # =====================================================================================
 # Linear / dropout
 # =====================================================================================
+_LINEAR_DEFER = os.environ.get("B2P_LINEAR_WGRAD_DEFER", "0") == "1"   # 1: frozen Linear dW on the side stream (measured neutral: base 14.03 either way, Conformer 64.79 / 64.80 ms)
+
+
 @_prec_follow
 class _Linear(torch.autograd.Function):
     @staticmethod
@@ -1798,9 +1801,14 @@ class _Linear(torch.autograd.Function):
             dx = torch.empty_like(x)
             mm_nn(dy, W, dx)
         if ctx.needs_input_grad[1]:
-            dW = torch.empty_like(W)
-            mm_tn(dy, x, dW)
-        if ctx.has_b and ctx.needs_input_grad[2]:
+            if _LAZY_COLSUM and _LINEAR_DEFER and _defer_ok(ctx.prm[0]):
+                # frozen weight (lm_head in configs 1-3): the weight-gradient GEMM itself on the side stream,
+                # accumulating into .grad (it ran on 6 workgroups for ~47 us on the main stream)
+                _defer_wgemm(ctx.prm[0], lambda out, beta, dy=dy, x=x: mm_tn(dy, x, out, beta=beta), dy, x)
+            else:
+                dW = torch.empty_like(W)
+                mm_tn(dy, x, dW)
+        if ctx.has_b and ctx.needs_input_grad[2] and not _defer_bias_rows((ctx.prm[1],), dy, dy.numel() // N, N):
             db = torch.empty(N, device=x.device)
             colsum(dy, dy.numel() // N, N, db)
         dW, db = _defer_small(ctx.prm, (dW, db))   # frozen: one batched side-stream add, not autograd's
