@@ -422,8 +422,19 @@ class _WSpec:
         self.gate, self.prec = _state.gate, _prec()
 
     def key(self):
+        # parameters by (rows, numel), not shape: a Conformer's out-projection weight (D, D) and its
+        # pointwise conv-2 weight (D, D, 1) share one batched launch (two 1.5-round grids -> one of 3)
         return (self.M, self.N, self.K, self.lda, self.ldb, self.a.dtype, self.b.dtype, self.prec,
-                tuple(tuple(p.shape) for p in self.ps))
+                tuple(_pkey(p) for p in self.ps))
+
+
+# B2P_WGRAD_MERGE=1: batch groups keyed by (rows, numel) per parameter instead of the full shapes (measured
+# neutral on Conformer-large: 64.93 / 65.12 vs 65.14 / 65.06 ms, profiles/r05aw_wgrad_merge_ab.txt)
+_WGRAD_MERGE = os.environ.get("B2P_WGRAD_MERGE", "0") == "1"
+
+
+def _pkey(p):
+    return (p.shape[0], p.numel()) if _WGRAD_MERGE else tuple(p.shape)
 
 
 # B2P_WGRAD_BATCH=0: every deferred frozen weight gradient is its own (split-K) launch
@@ -564,8 +575,8 @@ def _run_wspecs(specs) -> bool:
         if cap:   # a home is allocated (zeroed) outside captures only
             _wdbg("no home before the capture", specs)
             return False
-        shape0 = tuple(s0.ps[0].shape)
-        nfrozen = sum(1 for q in _FROZEN_PTR.values() if tuple(q.shape) == shape0)
+        shape0 = _pkey(s0.ps[0])
+        nfrozen = sum(1 for q in _FROZEN_PTR.values() if _pkey(q) == shape0)
         home = _HOMES[key] = _Home(M, N, max(1, -(-nfrozen // len(s0.ps))), dev)
     at = {}
     for sp in specs:
