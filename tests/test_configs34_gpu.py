@@ -32,6 +32,10 @@ pytestmark = pytest.mark.gpu
 LOSS_RTOL = 1e-3        # BASELINE.json north_star: the loss at the reference's weights
 FP32_TRAJ_RTOL = 1e-4   # exact-fp32 mode, every step of the trajectory
 # bf16 mode (with the Trainer's precision policy), steps after the first Adam update: the north-star 1e-3
+# sign-weighted lost update share per parameter family (brain_encoder / w2v), printed by the test; measured
+# (round 5): fp32 mode <= 1.2e-6; default mode brain_encoder 1.0e-3 / 1.8e-3 / 2.8e-3 (configs 1-3, bf16),
+# configs[4] (bf16x3 policy) w2v 2.7e-6, brain_encoder 4.1e-7
+SIGN_LOST_MAX = {"fp32": 1e-4, "bf16": 1e-2}
 BF16_TRAJ_RTOL = {"base_bs32": 1e-3, "conformer_large_bs32": 1e-3, "large960_bs32": 1e-3,
                   "conformer_large_ft_bs8": 1e-3}
 # the precision the policy picks per fixture (the w2v encoder trained -> bf16x3)
@@ -82,6 +86,7 @@ def test_adam_trajectory_matches_reference(name, mode):
     # every parameter it left alone (unused inpLayer* / hidden_start / conformer pos_conv_embed:
     # grad None) stayed bit-identical
     worst = 0.0
+    lost = {"brain_encoder": [0.0, 0.0], "w2v": [0.0, 0.0]}   # sign-weighted lost descent of the updates
     for n in fx["param_names"]:
         dref = float(fx["dnorm/" + n])
         d = deltas[n]
@@ -98,7 +103,16 @@ def test_adam_trajectory_matches_reference(name, mode):
         # under bf16 rounding, so the sampled entries are compared by their correlation
         c = float(np.dot(v, r) / (np.linalg.norm(v) * np.linalg.norm(r) + 1e-30))
         assert c >= (0.99 if mode == "fp32" else 0.9), (n, c)
-    print(f"{name}: worst relative update-norm error {worst:.3e}")
+        # Adam's updates are ~lr * sign(m / sqrt(v)): the share of the reference's update magnitude whose
+        # direction flipped here (the w2v updates of the full fine-tune, configs[4])
+        part = lost["brain_encoder" if n.startswith("brain_encoder.") else "w2v"]
+        part[0] += float(np.abs(r)[np.sign(v) != np.sign(r)].sum())
+        part[1] += float(np.abs(r).sum())
+    shares = {k: (a / b if b > 0 else 0.0) for k, (a, b) in lost.items()}
+    print(f"{name} [{mode}]: worst relative update-norm error {worst:.3e}; sign-lost update share "
+          + ", ".join(f"{k} {v:.2e}" for k, v in shares.items()))
+    for k, v in shares.items():
+        assert v <= SIGN_LOST_MAX[mode], (k, v)
     assert worst <= 0.1, worst
     # the optimizer's per-parameter step counters: one per update for every used parameter
     opt = trainer.optimizer
