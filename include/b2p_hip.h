@@ -614,12 +614,6 @@ int64_t b2p_batchnorm_workspace(int64_t M, int64_t C);
  * unless the LayerDrop gate (b2p_set_gate) is closed -- torch _BatchNorm.forward's
  * num_batches_tracked.add_(1) without a separate launch. NULL clears it. */
 int b2p_batchnorm_count_next(int64_t* num_batches_tracked);
-/* Plain 16-bit GEMMs of b2p_gemm (epilogue alpha / beta / residual only, one output, one batch member,
- * dense operands, no split-K) run through hipBLASLt (csrc/blaslt.cpp); every fused GEMM stays on the
- * hand-written kernels. b2p_blaslt_enable(0) (or B2P_BLASLT=0) routes everything to the hand-written
- * kernels; b2p_blaslt_calls returns the launches that went to the library (reset: zero it). */
-int b2p_blaslt_enable(int on);
-int64_t b2p_blaslt_calls(int reset);
 int b2p_batchnorm_fwd(const float* x, const float* gamma, const float* beta, float* running_mean,
                       float* running_var, float* y, float* pre, float* mean, float* rstd, int64_t M,
                       int64_t C, float eps, float momentum, int act, float* workspace,

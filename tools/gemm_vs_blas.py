@@ -25,7 +25,6 @@ def timeit(fn, iters=30):
 
 def main():
     torch.manual_seed(0)
-    Fn.blaslt(False)   # "ours" = the hand-written kernels (b2p_gemm would route plain GEMMs to hipBLASLt)
     dev = "cuda"
     NT, D, F = 7968, 768, 3072
     shapes = [("nt", NT, D, D), ("nt", NT, F, D), ("nt", NT, D, F), ("nt", NT, 3 * D, D),

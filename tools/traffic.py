@@ -18,7 +18,7 @@ def per_kernel(db, counter):
 def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
-    # our GEMM kernels and the hipBLASLt kernels b2p_gemm routes the plain 16-bit GEMMs to (csrc/blaslt.cpp)
+    # our GEMM kernels
     isg = lambda n: "gemm16_kernel<" in n or "gemm_kernel<" in n or "gemm16_pp_kernel<" in n or n.startswith("Cijk_")
     f = [v for _, n, v in fetch if isg(n)]
     w = [v for _, n, v in write if isg(n)]

@@ -175,8 +175,6 @@ _SIGS = {
     "b2p_batchnorm_fwd16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32,
                                     c_f32, c_i32, c_p, c_p]),
     "b2p_batchnorm_apply16": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i32, c_p, c_p, c_i64, c_i64, c_i32, c_p]),
-    "b2p_blaslt_enable": (c_i32, [c_i32]),
-    "b2p_blaslt_calls": (c_i64, [c_i32]),
     "b2p_batchnorm_finalize": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_f32, c_f32, c_i32, c_p]),
     "b2p_batchnorm_apply": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p]),
     "b2p_batchnorm_bwd_sums": (c_i32, [c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_p, c_i64, c_i64, c_i32, c_p, c_p]),

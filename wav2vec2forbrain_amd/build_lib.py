@@ -1,9 +1,14 @@
 """Builds libb2p_hip.so (the C-ABI HIP library) in-tree with hipcc for gfx950.
 
-Each csrc/*.hip / *.cpp file is compiled to an object under build/ (rebuilt when the source or
-any header is newer) and linked into wav2vec2forbrain_amd/libb2p_hip.so. The library links the
-HIP runtime by SONAME (libamdhip64.so.7), so inside a process that imported torch it binds to
-the runtime torch already loaded.
+Each csrc/*.hip / *.cpp file is compiled to an object under build/ and linked into
+wav2vec2forbrain_amd/libb2p_hip.so. Staleness is decided by content, not by mtime: every object
+carries a SHA-256 stamp of its source, the csrc/*.inc templates it includes, every header and the
+compiler flags (`<obj>.sha`), and the library carries the hash of all of them
+(`libb2p_hip.so.sha`). A library whose stamp matches the sources is current whatever the file times
+say (a snapshot copied to the GPU box keeps the .so and its stamp); one whose stamp differs is
+rebuilt even when it is newer than an edited source. The library links only the HIP runtime, by
+SONAME (libamdhip64.so.7), so inside a process that imported torch it binds to the runtime torch
+already loaded.
 """
 from __future__ import annotations
 
@@ -24,26 +29,47 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-at
          "-Wno-unused-result"]
 
 
-def _headers_mtime() -> float:
-    hs = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))
-    return max((os.path.getmtime(h) for h in hs), default=0.0)
+LIB_STAMP = LIB + ".sha"
 
 
-def _inc_mtime(src: str) -> float:
-    """Newest mtime of the csrc/*.inc files a source includes (kernel templates shared by several
-    instantiation units: only their includers rebuild when they change)."""
+def _read(path: str) -> bytes:
+    with open(path, "rb") as f:
+        return f.read()
+
+
+def _headers_hash() -> str:
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted(glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(ROOT, "include", "*.h"))):
+        h.update(os.path.basename(p).encode() + b"\0" + _read(p))
+    return h.hexdigest()
+
+
+def _src_hash(src: str, hh: str) -> str:
+    """Stamp of one object: its source, the csrc/*.inc kernel templates it includes (shared by several
+    instantiation units: only their includers rebuild when they change), every header, the flags."""
+    import hashlib
     import re
-    t = 0.0
-    for name in re.findall(r'#include "([^"]+\.inc)"', open(src).read()):
-        f = os.path.join(CSRC, name)
+    h = hashlib.sha256(" ".join([HIPCC, *FLAGS]).encode() + hh.encode())
+    text = _read(src)
+    h.update(text)
+    for name in re.findall(rb'#include "([^"]+\.inc)"', text):
+        f = os.path.join(CSRC, name.decode())
         if os.path.exists(f):
-            t = max(t, os.path.getmtime(f))
-    return t
+            h.update(_read(f))
+    return h.hexdigest()
 
 
-def _compile(src: str, hmt: float, verbose: bool) -> str:
+def _stamp(path: str) -> str:
+    try:
+        return open(path).read().strip()
+    except OSError:
+        return ""
+
+
+def _compile(src: str, sh: str, verbose: bool) -> str:
     obj = os.path.join(BUILD, os.path.basename(src) + ".o")
-    if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(src), hmt, _inc_mtime(src)):
+    if os.path.exists(obj) and _stamp(obj + ".sha") == sh:
         return obj
     cmd = [HIPCC, *FLAGS, "-c", src, "-o", obj]
     audit = os.environ.get("B2P_BUILD_AUDIT") == "1"
@@ -57,6 +83,8 @@ def _compile(src: str, hmt: float, verbose: bool) -> str:
     if audit:
         with open(obj + ".audit", "w") as f:
             f.write(r.stdout + r.stderr)
+    with open(obj + ".sha", "w") as f:
+        f.write(sh + "\n")
     return obj
 
 
@@ -83,29 +111,29 @@ def ensure_built() -> str:
 
 
 def _build_locked(verbose: bool, jobs: int | None) -> str:
+    import hashlib
     srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")))
-    hmt = _headers_mtime()
-    # a library newer than every source, header and kernel template is current even without the
-    # objects (a snapshot that carries the built .so but not build/)
-    newest_src = max([hmt] + [max(os.path.getmtime(s), _inc_mtime(s)) for s in srcs])
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= newest_src:
+    hh = _headers_hash()
+    shas = [_src_hash(s, hh) for s in srcs]
+    lib_sha = hashlib.sha256("".join(os.path.basename(s) + ":" + h + ";" for s, h in zip(srcs, shas)).encode()).hexdigest()
+    # a library whose stamp matches is current even without the objects (a snapshot that carries the
+    # built .so but not build/)
+    if os.path.exists(LIB) and _stamp(LIB_STAMP) == lib_sha:
         return LIB
     # the GPU box reports the whole machine's CPUs; its share is 16
     jobs = jobs or min(16, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
-        objs = list(ex.map(lambda s: _compile(s, hmt, verbose), srcs))
-    newest = max(os.path.getmtime(o) for o in objs)
-    if os.path.exists(LIB) and os.path.getmtime(LIB) >= newest:
-        return LIB
+        objs = list(ex.map(lambda a: _compile(a[0], a[1], verbose), zip(srcs, shas)))
     tmp = LIB + ".tmp"
-    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs, "-L/opt/rocm/lib", "-lhipblaslt",
-           "-Wl,-rpath,/opt/rocm/lib"]
+    cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     if verbose:
         print(" ".join(cmd), file=sys.stderr, flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stdout}\n{r.stderr}")
     os.replace(tmp, LIB)
+    with open(LIB_STAMP, "w") as f:
+        f.write(lib_sha + "\n")
     return LIB
 
 

@@ -511,13 +511,9 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
   b2p_timing_begin(d.timing_family, st);
   const bool AK = d.A.inner_is_k != 0, BKn = d.B.inner_is_k != 0;
   int rc;
-  bool lib = false;   // launched through hipBLASLt (blaslt.cpp: plain 16-bit GEMMs)
   if (bf16_ops) {
     B2P_CHECK_ARG(AK || !BKn, "gemm: A inner=m with B inner=k layout not supported");
-    const int l = d.ksplit > 1 ? 0 : b2p_blaslt_gemm(d, st);
-    if (l < 0) return 1;
-    lib = l > 0;
-    rc = lib ? 0 : b2p_gemm16_launch(d, st);
+    rc = b2p_gemm16_launch(d, st);
   } else if (AK && BKn) {
     if (d.A.conv) rc = launch_tiles<true, true, true, false>(d, ea, st);
     else if (d.B.conv) { b2p_set_error("gemm: conv view on B requires B inner=n"); return 1; }
@@ -534,7 +530,7 @@ extern "C" int b2p_gemm(const b2p_gemm_desc* dp, b2p_stream_t stream) {
     return 1;
   }
   if (rc) return rc;
-  if (!lib && d.ksplit > 1 && !(bf16_ops && gemm16_splitk_fused(d))) {
+  if (d.ksplit > 1 && !(bf16_ops && gemm16_splitk_fused(d))) {
     const int64_t total = (int64_t)d.nz1 * d.nz2 * d.M * d.N;
     const b2p_epilogue& e = d.ep;
     const bool v4 = d.N % 4 == 0 && e.ldc % 4 == 0 && e.cbs1 % 4 == 0 && e.cbs2 % 4 == 0 &&

@@ -206,8 +206,6 @@ inline EpiArgs make_epi_args(const b2p_gemm_desc& d) {
 
 }  // namespace
 
-// plain 16-bit GEMMs through hipBLASLt (blaslt.cpp): 1 launched, 0 not taken, -1 error
-int b2p_blaslt_gemm(const b2p_gemm_desc& d, hipStream_t st);
 // bf16-operand (LDS-DMA) GEMM launcher, gemm16.hip; arguments already validated by b2p_gemm.
 int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st);
 // true when the gemm16 launch of d sums its split-K slabs itself (no reduce launch after it)

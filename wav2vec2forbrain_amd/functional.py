@@ -868,10 +868,6 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     ws = None
     plain = (bias is None and pre_out is None and act == 0 and act_bwd == 0 and drop_p == 0.0 and residual is None
              and colsum_part is None and pre16 is None and C16b is None)
-    if (plain and _BLASLT[0] and A.dtype != 0 and B.dtype == A.dtype and nz1 * nz2 == 1 and A.inner_is_k
-            and not (A.conv or B.conv or A.gather1 or B.gather1) and (C is None) != (C16 is None)
-            and min(M, N, K) >= 64 and A.ld >= K and B.ld >= (K if B.inner_is_k else N)):
-        plain = False   # csrc/blaslt.cpp takes it whole (hipBLASLt): no split-K slabs
     if plain and K >= 2048 and not _state.nosplit:
         b16 = A.dtype != 0
         bn = 64 if (N <= 64 and not b16) else 128
@@ -910,17 +906,6 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
                                                             + 4 * (residual is not None) + 4 * (beta != 0.0)
                                                             + (2 if aux16 is not None else 4 if aux is not None else 0))))
     _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
-
-
-# plain 16-bit GEMMs go to hipBLASLt inside b2p_gemm (csrc/blaslt.cpp); B2P_BLASLT=0: every GEMM on the
-# hand-written kernels
-_BLASLT = [os.environ.get("B2P_BLASLT", "1") != "0"]
-
-
-def blaslt(on: bool) -> None:
-    """Route plain 16-bit GEMMs through hipBLASLt (True) or keep every GEMM on the hand-written kernels."""
-    _BLASLT[0] = bool(on)
-    _lib.load().b2p_blaslt_enable(int(bool(on)))
 
 
 # bf16x3 mode: large plain fp32-operand GEMMs run as one bf16 GEMM over split-bf16 operand images
