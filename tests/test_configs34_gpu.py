@@ -31,11 +31,13 @@ pytestmark = pytest.mark.gpu
 
 LOSS_RTOL = 1e-3        # BASELINE.json north_star: the loss at the reference's weights
 FP32_TRAJ_RTOL = 1e-4   # exact-fp32 mode, every step of the trajectory
-# bf16 mode (with the Trainer's precision policy), steps after the first Adam update: the north-star 1e-3
-# sign-weighted lost update share per parameter family (brain_encoder / w2v), printed by the test; measured
-# (round 5): fp32 mode <= 1.2e-6; default mode brain_encoder 1.0e-3 / 1.8e-3 / 2.8e-3 (configs 1-3, bf16),
-# configs[4] (bf16x3 policy) w2v 2.7e-6, brain_encoder 4.1e-7
-SIGN_LOST_MAX = {"fp32": 1e-4, "bf16": 1e-2}
+# Sign-weighted lost share of the reference's parameter updates per family (brain_encoder / w2v) after the
+# first Adam update, printed by the test. Adam's first updates are ~lr * sign(g), so this is the share of
+# the update magnitude whose direction the 16-bit rounding flipped. Measured (round 5): fp32 mode <= 1.2e-6;
+# default mode brain_encoder 1.0e-3 / 1.8e-3 / 2.8e-3 (configs 1-3, bf16), configs[4] (bf16x3 policy) w2v
+# 2.7e-6, brain_encoder 4.1e-7. The bf16 gate sits at ~1.8x the worst measured value (not at the north
+# star's 1e-3, which bounds the loss, not this share).
+SIGN_LOST_MAX = {"fp32": 1e-4, "bf16": 5e-3}
 BF16_TRAJ_RTOL = {"base_bs32": 1e-3, "conformer_large_bs32": 1e-3, "large960_bs32": 1e-3,
                   "conformer_large_ft_bs8": 1e-3}
 # the precision the policy picks per fixture (the w2v encoder trained -> bf16x3)

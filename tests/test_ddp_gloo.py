@@ -153,3 +153,54 @@ def test_reducer_used_gates_world2_gloo():
         assert res[r]["eager"] == [1, 1, 1, 1, 0, 0], res
         assert res[r]["replay"] == [1, 1, 1, 1, 1, 1], res
         assert res[r]["replay2"] == [1, 1, 1, 1, 0, 0], res
+
+
+def _regroup_worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from wav2vec2forbrain_amd.train.ddp import GradBucketReducer
+        m = _model()
+        params = _params(m)
+        first = params[:2]   # the first param group; the rest joins later (add_param_group)
+        red = GradBucketReducer(first, bucket_mb=0.001)
+        red.zero_grad()
+        _loss(m, rank, _data(rank)).backward()
+        red.finish()
+        # the Trainer's rebuild: the old reducer lets go of its parameters, a new one takes all of them
+        red.close()
+        for p in params:
+            p.grad = None
+        red2 = GradBucketReducer(params, bucket_mb=0.001)
+        red2.zero_grad()
+        red.launch_log.clear()
+        _loss(m, rank, _data(rank)).backward()
+        red2.finish()
+        exp = []
+        for r in range(world):
+            mr = _model()
+            _loss(mr, r, _data(r)).backward()
+            exp.append([p.grad if p.grad is not None else torch.zeros_like(p) for p in _params(mr)])
+        ok = all(torch.allclose(p.grad, sum(e[i] for e in exp) / world, rtol=1e-5, atol=1e-7)
+                 for i, p in enumerate(params))
+        q.put((rank, ok, len(red.launch_log), list(red2.launch_log) == list(range(len(red2.buckets)))))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_reducer_rebuilt_for_a_new_param_group_world2_gloo():
+    """when the optimizer gains a param group under data parallelism the Trainer replaces its
+    reducers (train_loop.Trainer._setup_dp). The replaced reducer's hooks are gone (it launches nothing
+    more) and the new one averages every parameter, the new group's included."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_regroup_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, old_launches, in_order in res:
+        assert ok and old_launches == 0 and in_order, res

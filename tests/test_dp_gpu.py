@@ -403,3 +403,84 @@ def test_dp_layerdrop_same_layers_on_every_rank(tmp_path):
     assert skipped > 0, res[0]["record"]   # the draws did skip layers (the test is not vacuous)
     for n in res[0]["params"]:
         assert torch.equal(res[0]["params"][n], res[1]["params"][n]), n
+
+
+def _regroup_steps(model, batches, split):
+    """Trainer steps whose optimizer starts with the first `split` brain-encoder parameters and gains
+    the rest (HipAdam.add_param_group) after two steps; returns the losses."""
+    from wav2vec2forbrain_amd import functional as Fn
+    from wav2vec2forbrain_amd.optim import HipAdam
+    from wav2vec2forbrain_amd.train.train_loop import Trainer
+    from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+    ps = list(model.brain_encoder.parameters())
+
+    class Exp(SyntheticStepExperiment):
+        def create_optimizer(self):
+            return HipAdam([{"params": ps[:split]}], lr=self.base_config.learning_rate)
+
+    with Fn.precision("fp32"):
+        trainer = Trainer(Exp(model, lr=1e-3))
+        trainer.capture_after = 1
+        losses = []
+        for i, b in enumerate(batches):
+            if i == 2:
+                trainer.optimizer.add_param_group({"params": ps[split:]})
+            losses.append(float(trainer.train_step(b).loss))
+    torch.cuda.synchronize()
+    counts = (trainer.eager_steps, trainer.graph_steps)
+    trainer.release_graphs()
+    Fn.set_deferred_wgrad([])
+    return losses, counts
+
+
+def _regroup_worker(rank, name, port, out_dir, split):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=WORLD)
+    try:
+        cfg = _cfg(name)
+        model = build_model(cfg)
+        model.train()
+        model.sync_metrics = False
+        per = cfg["B"] // WORLD
+        b = _batch(cfg, (rank * per, (rank + 1) * per))
+        losses, counts = _regroup_steps(model, [b] * 4, split)
+        torch.save({"losses": losses, "counts": counts,
+                    "params": {n: p.detach().cpu() for n, p in _trainable(model)}},
+                   os.path.join(out_dir, f"regroup_rank{rank}.pt"))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_trainer_param_group_added_between_steps(tmp_path):
+    """a param group added mid-run (HipAdam.add_param_group) under data parallelism.
+    The Trainer rebuilds its bucket reducer, frozen reducer and optimizer gates for the new parameter set
+    (train_loop.Trainer._setup_dp), so the new group's gradients are all-reduced: two ranks on half
+    batches end with the parameters of the single-process global-batch run, and equal on both ranks."""
+    import torch.multiprocessing as mp
+    name = "tiny_a"
+    cfg = _cfg(name)
+    ref = build_model(cfg)
+    ref.train()
+    split = len(list(ref.brain_encoder.parameters())) // 2
+    ref_losses, ref_counts = _regroup_steps(ref, [_batch(cfg, (0, cfg["B"]))] * 4, split)
+    params = {n: p.detach().cpu() for n, p in _trainable(ref)}
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_regroup_worker, args=(r, name, port, str(tmp_path), split)) for r in range(WORLD)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [torch.load(tmp_path / f"regroup_rank{r}.pt", weights_only=True) for r in range(WORLD)]
+    for r in res:
+        assert tuple(r["counts"]) == tuple(ref_counts) and r["counts"][1] >= 1, (r["counts"], ref_counts)
+    for k in range(4):
+        glob = (res[0]["losses"][k] + res[1]["losses"][k]) / 2
+        assert abs(glob - ref_losses[k]) <= 2e-5 * abs(ref_losses[k]), (k, glob, ref_losses[k])
+    for n, p in params.items():
+        for r in res:
+            d = float((r["params"][n] - p).norm())
+            assert d <= 1e-4 * float(p.norm()) + 1e-6, (n, d)
+        assert torch.equal(res[0]["params"][n], res[1]["params"][n]), n

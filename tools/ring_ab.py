@@ -1,9 +1,8 @@
-"""A/B of the 256 x 256 GEMM kernels (b2p_gemm16_variant: 0 = the 2-buffer 64-deep ping-pong kernel, 1 =
-the 4-stage 32-deep ring "p4") on the step's shapes, in one process with interleaved rounds (guide
-§5.4 rule 24): every shape is forced onto the 256 x 256 family (B2P_GEMM16_PP=2), the two variants'
-outputs are compared bitwise (same MFMA accumulation order), and the default dispatch (whatever
-kernel the step uses for that shape today) is timed beside them.
-usage: B2P_GEMM16_PP=2 python tools/p4_ab.py [rounds]"""
+"""A/B of the 256-column GEMM kernels (b2p_gemm16_variant: 0 = the 2-buffer 64-deep ping-pong kernel, 1 =
+the 5-slot ring kernel) on the step's shapes, in one process with interleaved rounds (guide §5.4 rule
+24). With B2P_GEMM16_PP=2 every shape is forced onto the 256-column family; the two variants' outputs are
+compared bitwise (same MFMA accumulation order).
+usage: B2P_GEMM16_PP=2 python tools/ring_ab.py [rounds]"""
 import os
 import sys
 
@@ -23,7 +22,9 @@ SHAPES = [("nt", NT, F, D, "f"), ("nt", NT, D, F, "f"), ("nt", NT, 3 * D, D, "f"
           ("nt", NT, Fc, Dc, "f"), ("nt", NT, Dc, Fc, "f"), ("nt", NT, 3 * Dc, Dc, "f"), ("nt", NT, Dc, Dc, "f"),
           ("nn", NT, D, F, "f"), ("nn", NT, Fc, Dc, "f"),
           ("tn", D, F, NT, "f"), ("tn", Fc, Dc, NT, "f"), ("tn", Dc, Dc, NT, "f"),
-          ("nt", 4096, 4096, 4096, "f"), ("nt", 8192, 8192, 8192, "f"), ("nt", NT, F, D, "bdrh")]
+          ("tn", F, D, NT, "f"), ("tn", D, D, NT, "f"), ("tn", 4096, 4096, 7968, "f"),
+          ("nt", 4096, 4096, 4096, "f"), ("nt", 8192, 8192, 8192, "f"), ("nt", NT, F, D, "bdrh"), ("nt", 8000, 3072, 776, "f"),
+          ("tn", 1000, 3000, 1000, "f")]
 
 
 def operands(kind, M, N, K, dev="cuda"):
@@ -83,7 +84,7 @@ def main():
             fl = 2.0 * M * N * K
             t0, t1 = sorted(times[0])[len(times[0]) // 2], sorted(times[1])[len(times[1]) // 2]
             msg = (f"{kind} {M}x{N}x{K} [{epi}]  pp {t0:8.1f} us {fl / t0 / 1e6:7.1f} TF   p4 {t1:8.1f} us "
-                   f"{fl / t1 / 1e6:7.1f} TF   p4/pp {t1 / t0:5.3f}   bitwise {same}")
+                   f"{fl / t1 / 1e6:7.1f} TF   ring/pp {t1 / t0:5.3f}   bitwise {same}")
             if ref is not None and "b" not in epi:
                 for v in (0, 1):
                     msg += f"  relerr[{v}] {float((outs[v][0] - ref).norm() / ref.norm()):.2e}"

@@ -68,14 +68,16 @@ bool gemm16_splitk_fused(const b2p_gemm_desc& d) {
   return v4 && d.workspace_floats >= need;
 }
 
-static int g_gemm16_variant = -1;
-int b2p_gemm16_variant_get() {
-  if (g_gemm16_variant < 0) g_gemm16_variant = getenv("B2P_GEMM16_P4") ? atoi(getenv("B2P_GEMM16_P4")) : 0;
-  return g_gemm16_variant;
+// 256-column kernel of the "pp" launches (B2P_GEMM16_RING): 0 = the 2-buffer ping-pong kernel, 1 = the
+// 5-slot ring kernel (gemm16_impl.inc). b2p_gemm16_variant sets it at run time (tests / A-B tools).
+static int g_ring_mode = -1;
+int gemm16_ring_mode() {
+  if (g_ring_mode < 0) g_ring_mode = getenv("B2P_GEMM16_RING") ? atoi(getenv("B2P_GEMM16_RING")) : 0;
+  return g_ring_mode;
 }
 extern "C" int b2p_gemm16_variant(int v) {
-  const int old = b2p_gemm16_variant_get();
-  if (v >= 0) g_gemm16_variant = v;
+  const int old = gemm16_ring_mode();
+  if (v >= 0) g_ring_mode = v;
   return old;
 }
 

@@ -218,14 +218,22 @@ class _Deferred:
     split = os.environ.get("B2P_DEFER_SPLIT", "1") == "1"   # split-K for the deferred GEMMs
 
 
-def set_deferred_wgrad(params) -> None:
-    """Parameters whose gradients may be deferred (frozen: not optimised, not all-reduced)."""
+def set_deferred_wgrad(params, names=None) -> None:
+    """Parameters whose gradients may be deferred (frozen: not optimised, not all-reduced). names
+    (optional, {id(p): qualified name}): the layer-independent role of each parameter (the name with its
+    layer indices masked), which sizes the batched weight-gradient slot buffers (_Home) by the number of
+    layers that hold a parameter of that role, not by every frozen parameter of the same shape."""
+    import re
     _Deferred.ids = {id(p) for p in params if p is not None}
     # frozen parameters by storage address: their staged 16-bit GEMM operand copies are cached
     # (keyed by the tensor version, so an in-place load still invalidates them)
     _CAST_CACHE.clear()
     _FROZEN_PTR.clear()
     _FROZEN_PTR.update({p.data_ptr(): p for p in params if p is not None and p.is_cuda})
+    _FROZEN_ROLE.clear()
+    if names:
+        _FROZEN_ROLE.update({id(p): re.sub(r"\.\d+\.", ".#.", names[id(p)]) for p in params
+                             if p is not None and id(p) in names})
     _HOMES.clear()
 
 
@@ -575,9 +583,14 @@ def _run_wspecs(specs) -> bool:
         if cap:   # a home is allocated (zeroed) outside captures only
             _wdbg("no home before the capture", specs)
             return False
-        shape0 = _pkey(s0.ps[0])
-        nfrozen = sum(1 for q in _FROZEN_PTR.values() if _pkey(q) == shape0)
-        home = _HOMES[key] = _Home(M, N, max(1, -(-nfrozen // len(s0.ps))), dev)
+        # slots: one per layer holding this role (Wq / Wk / Wv / Wo share a shape; without roles every
+        # frozen parameter of the shape counts, divided over the members of a slot)
+        shape0, role0 = _pkey(s0.ps[0]), _FROZEN_ROLE.get(id(s0.ps[0]))
+        if role0 is not None:
+            nslots = sum(1 for q in _FROZEN_PTR.values() if _pkey(q) == shape0 and _FROZEN_ROLE.get(id(q)) == role0)
+        else:
+            nslots = -(-sum(1 for q in _FROZEN_PTR.values() if _pkey(q) == shape0) // len(s0.ps))
+        home = _HOMES[key] = _Home(M, N, max(1, nslots), dev)
     at = {}
     for sp in specs:
         i = home.ensure(sp.ps)
@@ -588,21 +601,26 @@ def _run_wspecs(specs) -> bool:
     for i, sp in at.items():
         home.bind(i, sp.ps)
     nslot = len(home.members)
+    # every chunk's gathered operands first: a chunk that cannot be gathered (operands not 16-byte
+    # aligned) makes the caller run ALL the specs one by one, so nothing may have been launched yet
+    chunks = []
+    for c0 in range(0, nslot, 64):
+        c1 = min(nslot, c0 + 64)
+        mem = [at.get(i) for i in range(c0, c1)]
+        if all(m is None for m in mem):
+            continue
+        fill = next(m for m in mem if m is not None)
+        A, ia = _gathered_op([(m or fill).a for m in mem], [(m or fill).a_off for m in mem], s0.lda, s0.a.dtype)
+        B, ib = _gathered_op([(m or fill).b for m in mem], [0] * len(mem), s0.ldb, s0.b.dtype)
+        if A is None or B is None:
+            _wdbg("operands not 16-byte aligned", specs)
+            return False
+        chunks.append((c0, c1, mem, A, ia, B, ib))
     old_prec, old_split = _state.prec, _state.nosplit
     _state.prec = s0.prec
     try:
-        for c0 in range(0, nslot, 64):
-            c1 = min(nslot, c0 + 64)
+        for c0, c1, mem, A, ia, B, ib in chunks:
             n = c1 - c0
-            mem = [at.get(i) for i in range(c0, c1)]
-            if all(m is None for m in mem):
-                continue
-            fill = next(m for m in mem if m is not None)
-            A, ia = _gathered_op([(m or fill).a for m in mem], [(m or fill).a_off for m in mem], s0.lda, s0.a.dtype)
-            B, ib = _gathered_op([(m or fill).b for m in mem], [0] * n, s0.ldb, s0.b.dtype)
-            if A is None or B is None:
-                _wdbg("operands not 16-byte aligned", specs)
-                return False
             zg = _zero_gate(dev)
             gates = [zg if m is None else m.gate for m in mem]
             gp = (_i64_dev([0 if g is None else g.data_ptr() for g in gates], dev)
@@ -617,8 +635,9 @@ def _run_wspecs(specs) -> bool:
                 finally:
                     if gp is not None:
                         _lib.call("b2p_set_gate_batch", None)
-            del ia, ib, gp
+            del gp
             _wdbg(f"batched slots {c0}..{c1} ({sum(m is not None for m in mem)} present)", specs)
+        del chunks
     finally:
         _state.prec, _state.nosplit = old_prec, old_split
     return True
@@ -956,6 +975,7 @@ def _auto16_ok(M, N, K, A, B, nz1, nz2) -> bool:
 
 
 _FROZEN_PTR: dict = {}   # data_ptr -> frozen parameter (set_deferred_wgrad)
+_FROZEN_ROLE: dict = {}  # id -> the frozen parameter's name with layer indices masked (set_deferred_wgrad)
 _CAST_CACHE: dict = {}   # (ptr, rows, cols, ld, fp16) -> (version, buffer) for frozen parameters
 
 

@@ -115,11 +115,25 @@ class GradBucketReducer:
         self._layer_gates = None   # graph-replayed steps: the device LayerDrop flags (make_layer_gates)
         self._seen: set = set()
         self._reset()
+        self._hooks = []
         if self.active:
             for p in self.params:
-                p.register_post_accumulate_grad_hook(self._hook)
+                self._hooks.append(p.register_post_accumulate_grad_hook(self._hook))
         if grad_views:
             self.zero_grad()
+
+    def close(self) -> None:
+        """Detaches this reducer from its parameters (backward hooks removed, gradients unbound from the
+        bucket views), so another reducer can take them over (the Trainer rebuilds its reducers when
+        the optimizer gains a param group)."""
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        if self.grad_views:
+            for p in self.params:
+                if p.grad is not None and p.grad.data_ptr() == self.views[p].data_ptr():
+                    p.grad = None
+        self.active = False
 
     def make_layer_gates(self, param_flags: dict):
         """Graph-replayed steps (backward captured: no hook fires on a replay): the local "used" flag

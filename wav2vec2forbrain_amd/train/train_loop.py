@@ -43,24 +43,8 @@ class Trainer:
         self.reducer = None
         self.frozen_reducer = None
         opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
-        frozen = [p for p in self.model.parameters() if p.requires_grad and id(p) not in opt_ids]
-        if dp_active():
-            skip = unused_param_names(self.model)
-            params = [p for n, p in self.model.named_parameters() if id(p) in opt_ids and n not in skip]
-            self.reducer = GradBucketReducer(params, bucket_mb=float(os.environ.get("B2P_DP_BUCKET_MB", "64")))
-            if hasattr(self.optimizer, "make_capturable"):
-                # device-form update gated per parameter by "some rank used it" (LayerDrop: a
-                # parameter no rank used keeps its value and moments, as with grad=None)
-                self.optimizer.make_capturable(params[0].device)
-                self.optimizer.gates = self.reducer.gates
-            if self.config.gradient_clipping is not None:
-                # clip_grad_norm_ runs over model.parameters() (reference :72-75), frozen gradients
-                # included; averaging those too keeps every rank's clip coefficient equal to the
-                # single-process global-batch one (they accumulate across steps identically on all
-                # ranks once averaged, so averaging the running sum each step is exact)
-                self.frozen_reducer = GradBucketReducer(frozen, overlap=False, grad_views=False, track_used=False)
         # frozen parameters (not optimised): their gradient GEMMs run deferred beside the GRU backward
-        Fn.set_deferred_wgrad(frozen)
+        Fn.set_deferred_wgrad(self._setup_dp(opt_ids), names=self._param_names())
         # precision policy of the default (bf16) mode: with the w2v encoder trained (full fine-tuning,
         # unfreeze_strategy=brain_encoder+w2v) the step runs in the bf16x3 mode. Adam's first updates of
         # the ~600 M encoder parameters are ~lr * sign(g), and the 16-bit operands' rounding (bf16 or fp16,
@@ -84,6 +68,37 @@ class Trainer:
         self._epoch_counter = None
         self.graph_steps = 0
         self.eager_steps = 0
+
+    def _param_names(self) -> dict:
+        return {id(p): n for n, p in self.model.named_parameters()}
+
+    def _setup_dp(self, opt_ids: set) -> list:
+        """(Re)builds the data-parallel machinery for the optimised parameter set opt_ids: the bucket
+        reducer of the optimised gradients, the frozen-gradient reducer and the optimizer's device gates.
+        Returns the frozen (trainable, not optimised) parameters. Called again when the optimizer gains a
+        param group (HipAdam.add_param_group), so the new group's gradients are all-reduced and gated
+        like the others."""
+        for r in (self.reducer, self.frozen_reducer):
+            if r is not None:
+                r.close()
+        self.reducer = self.frozen_reducer = None
+        frozen = [p for p in self.model.parameters() if p.requires_grad and id(p) not in opt_ids]
+        if dp_active():
+            skip = unused_param_names(self.model)
+            params = [p for n, p in self.model.named_parameters() if id(p) in opt_ids and n not in skip]
+            self.reducer = GradBucketReducer(params, bucket_mb=float(os.environ.get("B2P_DP_BUCKET_MB", "64")))
+            if hasattr(self.optimizer, "make_capturable"):
+                # device-form update gated per parameter by "some rank used it" (LayerDrop: a
+                # parameter no rank used keeps its value and moments, as with grad=None)
+                self.optimizer.make_capturable(params[0].device)
+                self.optimizer.gates = self.reducer.gates
+            if self.config.gradient_clipping is not None:
+                # clip_grad_norm_ runs over model.parameters() (reference :72-75), frozen gradients
+                # included; averaging those too keeps every rank's clip coefficient equal to the
+                # single-process global-batch one (they accumulate across steps identically on all
+                # ranks once averaged, so averaging the running sum each step is exact)
+                self.frozen_reducer = GradBucketReducer(frozen, overlap=False, grad_views=False, track_used=False)
+        return frozen
 
     def _log_intermediate(self, batch: int, n_batches: int, evaluator):
         print(f"Batch {batch + 1}/{n_batches} loss: {evaluator.get_latest_loss():.2f} "
@@ -209,7 +224,9 @@ class Trainer:
             self.release_graphs()
             self._opt_generation = gen
             opt_ids = {id(p) for g in self.optimizer.param_groups for p in g["params"]}
-            Fn.set_deferred_wgrad([p for p in self.model.parameters() if p.requires_grad and id(p) not in opt_ids])
+            # data-parallel: the new group's gradients join the bucket reducer (and leave the frozen one),
+            # and the optimizer's gates follow the new parameter list
+            Fn.set_deferred_wgrad(self._setup_dp(opt_ids), names=self._param_names())
             enc = getattr(self.model, "w2v_encoder", None)
             self.encoder_trained = enc is not None and any(id(p) in opt_ids for p in enc.parameters())
         mode = self.step_precision()
