@@ -128,16 +128,19 @@ def _trainer_steps(model, batches, graphs, unfreeze="brain_encoder"):
         trainer = Trainer(SyntheticStepExperiment(model, unfreeze=unfreeze, lr=1e-3))
         trainer.use_graphs = graphs
         trainer.capture_after = 1
-        losses = []
+        losses, logs = [], []
         for b in batches:
             if trainer.reducer is not None:
                 trainer.reducer.launch_log.clear()
                 trainer.reducer.launch_tail.clear()
+                trainer.reducer.launch_pending.clear()
             losses.append(float(trainer.train_step(b).loss))
+            if trainer.reducer is not None:   # per step: the bucket launches the host issued (capture included)
+                logs.append((list(trainer.reducer.launch_log), list(trainer.reducer.launch_pending)))
     torch.cuda.synchronize()
     if trainer.reducer is not None:   # the last step's bucket launches (a replay when graphs are on)
         info.update(launch_log=list(trainer.reducer.launch_log), launch_tail=list(trainer.reducer.launch_tail),
-                    buckets=len(trainer.reducer.buckets))
+                    buckets=len(trainer.reducer.buckets), step_logs=logs, nparams=len(trainer.reducer.params))
     info["segments"] = [g["graph"].segments for g in trainer._graphs.values()]
     counts = (trainer.eager_steps, trainer.graph_steps)
     trainer.release_graphs()
@@ -277,7 +280,7 @@ def _nccl_world1_worker(port, out_dir, graphs, in_graph):
     """One rank, backend nccl (RCCL), B2P_DP_FORCE=1: every data-parallel code path runs over RCCL."""
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), B2P_DP_FORCE="1",
-                      B2P_GRAPH_COLLECTIVES="1" if in_graph else "0")
+                      B2P_GRAPH_COLLECTIVES="1" if in_graph else "0", B2P_DP_BUCKET_MB="0.05")
     torch.cuda.set_device(0)
     dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
@@ -325,6 +328,14 @@ def test_rccl_world1_captured_collectives(tmp_path):
             # one graph per step with the collectives inside; one segment per collective otherwise
             assert (r["info"]["segments"][0] == 1) == in_graph, (key, r["info"]["segments"])
             assert r["in_graph"] == in_graph
+        if graphs and in_graph:
+            # the RCCL graph holds the whole exchange: the capture (step 2) launched every
+            # bucket, the first while gradients of the backward were still to come (its all-reduce overlaps
+            # the rest of the backward in every replay); a replay (step 3) issues nothing from the host
+            cap_log, cap_pending = r["info"]["step_logs"][1]
+            assert sorted(cap_log) == list(range(r["info"]["buckets"])), (key, cap_log)
+            assert r["info"]["buckets"] > 1 and cap_pending[0] > 0, (key, cap_pending)
+            assert r["info"]["step_logs"][2] == ([], []), (key, r["info"]["step_logs"][2])
         for k in range(3):
             assert abs(r["losses"][k] - ref_losses[k]) <= 1e-5 * abs(ref_losses[k]), (key, k, r["losses"], ref_losses)
         worst = max(float((r["params"][n] - q).norm()) / (float(q.norm()) + 1e-30) for n, q in params.items()

@@ -29,6 +29,7 @@ def _run(name, batched, steps=5, graphs=True, layerdrop=0.5):
     enc.config.layerdrop = layerdrop
     b = batch_dict(cfg)
     batch = make_b2t_batch(b["x"], b["target"], b["day_idxs"], b["input_lens"], b["target_lens"]).cuda()
+    Fn.WGRAD_FALLBACKS[0] = 0
     try:
         with Fn.precision("bf16"):
             trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
@@ -43,6 +44,9 @@ def _run(name, batched, steps=5, graphs=True, layerdrop=0.5):
                  for n, p in model.named_parameters() if n.startswith("w2v_encoder.")}
         shared = len({p.grad.untyped_storage().data_ptr() for n, p in model.named_parameters()
                       if n.startswith("w2v_encoder.") and p.grad is not None and p.dim() >= 2})
+        # the batched path took every same-shape group (round 6: slot buffers sized by the roles of ONE
+        # spec made the Conformer's ffn1 / ffn2 home too small, and every group fell back silently)
+        assert not batched or Fn.WGRAD_FALLBACKS[0] == 0, Fn.WGRAD_FALLBACKS[0]
     finally:
         Fn._WGRAD_BATCH[0] = True
         Fn.set_deferred_wgrad([])

@@ -1,6 +1,7 @@
 """Breakdown of one step of a rocprofv3 kernel trace of bench.py, the step chosen by index among the
 spans between successive adam_rec_k launches: span, busy/idle, largest gaps, per-kernel totals.
-usage: python tools/step_breakdown.py <trace dir> <step index> [n_top]"""
+usage: python tools/step_breakdown.py <trace dir> <step index> [n_top] [--gemm]
+--gemm: also every GEMM launch of the step in issue order (kernel, workgroups, duration)."""
 import sys
 
 sys.path.insert(0, __file__.rsplit("/", 1)[0])
@@ -9,7 +10,8 @@ from trace_groups import dispatches  # noqa: E402
 
 def main():
     d, j = sys.argv[1], int(sys.argv[2])
-    ntop = int(sys.argv[3]) if len(sys.argv) > 3 else 30
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    ntop = int(args[2]) if len(args) > 2 else 30
     ks = sorted(dispatches(d), key=lambda r: r[3])
     ad = [i for i, k in enumerate(ks) if "adam_rec_k" in k[0] or "adam_gated_k" in k[0]]
     ad = [a for n, a in enumerate(ad) if n == 0 or a - ad[n - 1] > 4]
@@ -44,6 +46,12 @@ def main():
     tot = sum(k[4] for k in step)
     for n, (t, c) in sorted(agg.items(), key=lambda x: -x[1][0])[:ntop]:
         print(f"  {t / 1e3:8.1f} us {c:4d}x {100 * t / tot:5.1f}%  {n[:100]}")
+    if "--gemm" in sys.argv:
+        print("GEMM launches in issue order (start offset us, duration us, workgroups, kernel):")
+        for k in step:
+            if "gemm" in k[0] and "splitk" not in k[0]:
+                n = k[0].replace("(anonymous namespace)::", "").split("(")[0]
+                print(f"  {(k[3] - t0) / 1e3:9.1f} {k[4] / 1e3:8.1f} {k[1] // max(k[2], 1):6d}  {n[:90]}")
 
 
 if __name__ == "__main__":

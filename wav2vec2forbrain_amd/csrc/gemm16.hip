@@ -68,16 +68,12 @@ bool gemm16_splitk_fused(const b2p_gemm_desc& d) {
   return v4 && d.workspace_floats >= need;
 }
 
-// 256-column kernel of the "pp" launches (B2P_GEMM16_RING): 0 = the 2-buffer ping-pong kernel, 1 = the
-// 5-slot ring kernel (gemm16_impl.inc). b2p_gemm16_variant sets it at run time (tests / A-B tools).
-static int g_ring_mode = -1;
-int gemm16_ring_mode() {
-  if (g_ring_mode < 0) g_ring_mode = getenv("B2P_GEMM16_RING") ? atoi(getenv("B2P_GEMM16_RING")) : 0;
-  return g_ring_mode;
-}
+// Kernel family knob of the 256-column launches (b2p_gemm16_variant): a single family (the 2-buffer
+// ping-pong kernel) since round 6 -- the 5-slot ring kernel measured slower.
+static int g_variant = 0;
 extern "C" int b2p_gemm16_variant(int v) {
-  const int old = gemm16_ring_mode();
-  if (v >= 0) g_ring_mode = v;
+  const int old = g_variant;
+  if (v >= 0) g_variant = v;
   return old;
 }
 
@@ -128,7 +124,13 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   const int64_t tiles_pp = ((d.M + 255) / 256) * ((d.N + 255) / 256) * nz;
   const int64_t kper = ks > 1 ? (int64_t)d.kchunk : d.K;
   const bool nt = d.A.inner_is_k && d.B.inner_is_k;
-  const bool pp = !d.A.conv && (!h16 || nt) &&
+  // the 256-column kernels address each operand through a raw buffer resource with 32-bit offsets
+  // (SrcB, gemm16_impl.inc): every operand extent below 2^30 bytes
+  auto ext_ok = [&](const b2p_operand& o, int64_t mn) {
+    const int64_t rows = o.inner_is_k ? mn : d.K, cols = o.inner_is_k ? d.K : mn;
+    return ((rows - 1) * o.ld + cols) * 2 < (1ll << 30);
+  };
+  const bool pp = !d.A.conv && (!h16 || nt) && ext_ok(d.A, d.M) && ext_ok(d.B, d.N) &&
                   (pp_mode == 2 || (pp_mode == 1 && ((tiles_pp >= 192 && kper >= 2048) ||
                                                      (ks > 1 && tiles_pp >= 160 && kper >= 1024) ||
                                                      (nt && tiles_pp >= pp_tiles && kper >= 512))));

@@ -501,8 +501,8 @@ def _wdbg(msg, specs):
 
 class _Home:
     """The gradients of every frozen parameter (tuple) of one weight-gradient shape as slots of one
-    zero-initialised buffer [slots][M][N], sized once for all the frozen parameters of that shape (it is
-    never reallocated, so a captured step can rely on it): p.grad is a view of its slot, and any subset
+    zero-initialised buffer [slots][M][N], sized for the layers of the roles that use it (it grows only
+    outside captures, so a captured step can rely on it): p.grad is a view of its slot, and any subset
     of the layers (LayerDrop skips some in eager steps) is one batched launch over the slots, the
     absent members under a closed gate."""
 
@@ -512,6 +512,21 @@ class _Home:
         self.slot = {}        # tuple of parameter ids -> slot
         self.members = []     # slot -> tuple of parameters
         self.dirty = []       # slot -> its memory may hold a value (it was bound once)
+
+    def grow(self, cap) -> None:
+        """A bigger buffer (outside captures only): the slots' values move over and every member's p.grad
+        that was a slot view becomes the view of its new slot (a captured step never sees the old one:
+        homes grow in eager steps, which precede every capture of the shape)."""
+        old = self.buf
+        self.buf = torch.zeros(cap, self.M, self.N, device=old.device)
+        self.buf[:old.shape[0]].copy_(old)
+        for i, ps in enumerate(self.members):
+            r = 0
+            for p in ps:
+                ov = old[i, r:r + p.shape[0]].view(p.shape)
+                if p.grad is not None and p.grad.data_ptr() == ov.data_ptr():
+                    p.grad = self.view(i, p, r)
+                r += p.shape[0]
 
     def ensure(self, ps):
         k = tuple(id(p) for p in ps)
@@ -558,6 +573,9 @@ class _Home:
 
 
 _HOMES: dict = {}
+# same-shape groups of frozen weight gradients that could not run as one batched launch (no slot, unaligned
+# operands) and ran one launch per gradient instead: a slow path the tests require to stay unused
+WGRAD_FALLBACKS = [0]
 _ZERO_GATE: dict = {}   # device -> int32 0 (a closed LayerDrop gate for absent batch members)
 
 
@@ -583,14 +601,21 @@ def _run_wspecs(specs) -> bool:
         if cap:   # a home is allocated (zeroed) outside captures only
             _wdbg("no home before the capture", specs)
             return False
-        # slots: one per layer holding this role (Wq / Wk / Wv / Wo share a shape; without roles every
-        # frozen parameter of the shape counts, divided over the members of a slot)
-        shape0, role0 = _pkey(s0.ps[0]), _FROZEN_ROLE.get(id(s0.ps[0]))
-        if role0 is not None:
-            nslots = sum(1 for q in _FROZEN_PTR.values() if _pkey(q) == shape0 and _FROZEN_ROLE.get(id(q)) == role0)
+        # slots: one per layer holding a role that leads a slot of this shape (the roles of the specs'
+        # first parameters; the Conformer's ffn1 / ffn2 share a home, Wq / Wk / Wv / Wo share a shape but
+        # not a home; a role first met in a later eager step grows the home); without roles every frozen
+        # parameter of the shape counts, divided over a slot's members
+        shape0 = _pkey(s0.ps[0])
+        roles = {_FROZEN_ROLE.get(id(sp.ps[0])) for sp in specs}
+        if None not in roles:
+            nslots = sum(1 for q in _FROZEN_PTR.values() if _pkey(q) == shape0 and _FROZEN_ROLE.get(id(q)) in roles)
         else:
             nslots = -(-sum(1 for q in _FROZEN_PTR.values() if _pkey(q) == shape0) // len(s0.ps))
         home = _HOMES[key] = _Home(M, N, max(1, nslots), dev)
+    if not cap:   # members new to the home beyond its capacity: grow it once (eager steps only)
+        new = {tuple(id(p) for p in sp.ps) for sp in specs} - set(home.slot)
+        if len(home.members) + len(new) > home.buf.shape[0]:
+            home.grow(len(home.members) + len(new))
     at = {}
     for sp in specs:
         i = home.ensure(sp.ps)
@@ -687,7 +712,10 @@ def flush_wgrad(after=None) -> None:
             ents = groups[x] if kind == "g" else [x]
             sd = sides[_Deferred.lane.setdefault(ents[0][2], len(_Deferred.lane) % len(sides))]
             with torch.cuda.stream(sd):
-                if not (kind == "g" and _run_wspecs([e[3] for e in ents])):
+                batched = kind == "g" and _run_wspecs([e[3] for e in ents])
+                if kind == "g" and not batched:
+                    WGRAD_FALLBACKS[0] += 1
+                if not batched:
                     for fn, _, key, _ in ents:
                         with torch.cuda.stream(sides[_Deferred.lane.setdefault(key, len(_Deferred.lane) % len(sides))]):
                             fn()

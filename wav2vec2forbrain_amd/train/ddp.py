@@ -17,13 +17,15 @@ RCCL spreads one large all-reduce over all links with multiple channels, so fewe
 (default 64 MB) amortise the per-collective latency while still leaving several buckets to overlap
 for the full-fine-tune gradient sets (424 MB base, 2.47 GB Conformer-large).
 
-Graph-replayed steps: a bucket's launch goes through functional.collective(), so inside a segmented
-capture (train/step_graph.py) it splits the captured step there and each replay issues the bucket's
-all-reduce between the segments, beside the rest of the backward (full fine-tuning, config 5).
-Under unfreeze=brain_encoder (BASELINE configs 1-4) every trainable gradient is produced at the very
-end of backward (GRU, front end), beside the side-stream frozen-weight gradients a split would have
-to join, so the Trainer captures those with overlap=False and finish() exchanges the buckets after
-the replay: the 64 MB brain-encoder set, ~0.1 ms on 7 links.
+Graph-replayed steps over RCCL (the default for NCCL process groups, collectives_in_graph): the whole
+step is one graph. The backward hooks launch each bucket's all-reduce while the capture runs, so every
+replay issues it on RCCL's stream as soon as the bucket's last gradient is accumulated, beside the rest
+of the backward; the tail (remaining buckets, the used-flag MAX, the waits, the clip) and the Adam update
+are captured too, so a replay is one host call for the whole data-parallel step. gloo (host collectives):
+a bucket's launch goes through functional.collective(), so inside a segmented capture
+(train/step_graph.py) it splits the captured step there and each replay issues the bucket's all-reduce
+between the segments (full fine-tuning, config 5); with frozen-weight gradients on the side streams
+(configs 1-4) the buckets are exchanged after the replay, since a split would join those streams mid-GRU.
 """
 from __future__ import annotations
 
@@ -96,6 +98,7 @@ class GradBucketReducer:
         self.launch_log: deque = deque(maxlen=4096)    # bucket indices in the order their collectives were issued
         # per launch: the captured segments a replay still ran after it (> 0: overlapped the backward)
         self.launch_tail: deque = deque(maxlen=4096)
+        self.launch_pending: deque = deque(maxlen=4096)
         # "used by some rank this step" per parameter (int32, MAX-reduced in finish()): the gates
         # HipAdam's device form reads (opt.gates = reducer.gates), so a parameter no rank used —
         # every rank's LayerDrop dropped its layer — is left untouched, as torch.optim.Adam leaves a
@@ -156,7 +159,10 @@ class GradBucketReducer:
         # no LayerDrop flag at all (deterministic mode / no dropped layers): every parameter is
         # used — a replay fires no backward hook, so the hook-based flags would all read "unused"
         one = torch.ones(1, dtype=torch.int32, device=self.used.device)
-        idx = torch.tensor([len(flags) if s < 0 else s for s in src], dtype=torch.int64, device=self.used.device)
+        # a stream-ordered copy from pinned memory: the RCCL step calls this inside its capture
+        idx = torch.tensor([len(flags) if s < 0 else s for s in src], dtype=torch.int64)
+        if self.used.is_cuda:
+            idx = idx.pin_memory().to(self.used.device, non_blocking=True)
         return (flags + [one], idx)
 
     def use_layer_gates(self, state) -> None:
@@ -214,6 +220,8 @@ class GradBucketReducer:
         self.works[bi] = dist.all_reduce(self.flat[bi], op=op, group=self.pg, async_op=True)
         self.launch_log.append(bi)
         self.launch_tail.append(Fn.segments_remaining())
+        # parameters whose gradient was still to come when this bucket went out (> 0: issued mid-backward)
+        self.launch_pending.append(len(self.params) - len(self._seen))
 
     def _launch_all(self, bis):
         for bi in bis:

@@ -140,28 +140,43 @@ class Trainer:
             m.sync_metrics = False
         box = {}
         dp = self.reducer is not None
+        # RCCL: the whole data-parallel step is ONE graph: the step's collectives (SyncBN statistics, the
+        # gradient buckets as they complete during the backward, the used-flag MAX) are captured inside
+        # it, and so are the clip and the Adam update. gloo: segmented capture (a gloo collective is host
+        # code): the graph splits at every collective, which a replay issues between the segments
+        in_graph = dp and collectives_in_graph()
+        seg = dp and self.segmented and not in_graph
 
         def step():
             out = self._eager_body(static, in_graph=True)
+            if in_graph:
+                # the exchange tail inside the capture: remaining buckets, the used flags of this replay's
+                # LayerDrop draw (device flags), waits (stream joins), clip, update
+                self.reducer.use_layer_gates(self.reducer.make_layer_gates(Fn.layerdrop_param_gates()))
+                try:
+                    self.reducer.finish()
+                finally:
+                    self.reducer.use_layer_gates(None)
+                if self.frozen_reducer is not None:
+                    self.frozen_reducer.finish()
+                if self.config.gradient_clipping is not None:
+                    torch.nn.utils.clip_grad_norm_(self.model.parameters(), self.config.gradient_clipping)
+                self.optimizer.step()   # the device form (StepGraph made it capturable)
             box["out"] = out
             return out.loss.detach().reshape(1)
 
         if self._epoch_counter is None:
             self._epoch_counter = torch.zeros(1, dtype=torch.int64, device=batch.input.device)
-        # RCCL: the step's collectives (SyncBN statistics) are captured inside ONE graph; the gradient
-        # buckets are exchanged after each replay (finish()). gloo: segmented capture (a gloo
-        # collective is host code): the graph splits at every collective, which a replay issues
-        # between the segments
-        in_graph = dp and collectives_in_graph()
-        seg = dp and self.segmented and not in_graph
         if dp:
-            # bucket all-reduces between the segments of the backward only when no frozen-weight
-            # gradient work runs on the side streams (full fine-tuning): a split joins those streams,
-            # which would serialise them with the GRU backward they are meant to run beside.
-            # Otherwise every bucket is exchanged after the replay (finish()).
-            self.reducer.overlap = seg and not Fn.deferred_wgrad_active()
+            # bucket all-reduces from the backward hooks: inside the one RCCL graph they run on RCCL's
+            # stream beside the rest of the backward (the frozen-weight side streams are joined before the
+            # tail, so nothing waits for them early); segmented (gloo) only when no frozen-weight gradient
+            # work runs on the side streams (full fine-tuning): a split joins those streams, which would
+            # serialise them with the GRU backward they are meant to run beside. Otherwise every bucket is
+            # exchanged after the replay (finish()).
+            self.reducer.overlap = in_graph or (seg and not Fn.deferred_wgrad_active())
         try:
-            sg = StepGraph(step, None if dp else self.optimizer, warmup=0, warm_replays=0,
+            sg = StepGraph(step, None if (dp and not in_graph) else self.optimizer, warmup=0, warm_replays=0,
                            epoch=self._epoch_counter, segmented=seg)
             sg.capture()
         finally:
@@ -170,8 +185,8 @@ class Trainer:
                 self.reducer._reset()
             for m, o in zip(mods, olds):
                 m.sync_metrics = o
-        gates = self.reducer.make_layer_gates(Fn.layerdrop_param_gates()) if dp else None
-        return dict(graph=sg, batch=static, out=box["out"], gates=gates, sync=any(olds))
+        gates = self.reducer.make_layer_gates(Fn.layerdrop_param_gates()) if (dp and not in_graph) else None
+        return dict(graph=sg, batch=static, out=box["out"], gates=gates, sync=any(olds), tail=dp and not in_graph)
 
     def _replay(self, g, batch):
         st = g["batch"]
@@ -184,7 +199,7 @@ class Trainer:
             if isinstance(v, torch.Tensor):
                 getattr(st, a).copy_(v, non_blocking=True)
         g["graph"].replay()
-        if self.reducer is not None:
+        if g["tail"]:   # gloo: exchange, clip and update after the replay
             self.reducer.use_layer_gates(g["gates"])
             self._dp_tail()
         # the captured output's tensors are overwritten by the next replay
