@@ -68,9 +68,10 @@ bool gemm16_splitk_fused(const b2p_gemm_desc& d) {
   return v4 && d.workspace_floats >= need;
 }
 
-// Kernel family knob of the 256-column launches (b2p_gemm16_variant): a single family (the 2-buffer
-// ping-pong kernel) since round 6 -- the 5-slot ring kernel measured slower.
-static int g_variant = 0;
+// Kernel variant knob of the 256-column launches (b2p_gemm16_variant, B2P_GEMM16_VARIANT): 0 = default,
+// 1 = the ping-pong kernel without the quarter-scheduled DMA (A/B tools)
+static int g_variant = getenv("B2P_GEMM16_VARIANT") ? atoi(getenv("B2P_GEMM16_VARIANT")) : 0;
+int gemm16_variant_get() { return g_variant; }
 extern "C" int b2p_gemm16_variant(int v) {
   const int old = g_variant;
   if (v >= 0) g_variant = v;

@@ -114,6 +114,8 @@ class GradBucketReducer:
         self._loc_host = (torch.ones(max(len(self.params), 1), dtype=torch.int32).pin_memory()
                           if dev.type == "cuda" else None)
         self._loc_event = None
+        self._idx_host = (torch.zeros(max(len(self.params), 1), dtype=torch.int64).pin_memory()
+                          if dev.type == "cuda" else None)
         self._pos = {id(p): k for k, p in enumerate(self.params)}
         self._layer_gates = None   # graph-replayed steps: the device LayerDrop flags (make_layer_gates)
         self._seen: set = set()
@@ -159,10 +161,15 @@ class GradBucketReducer:
         # no LayerDrop flag at all (deterministic mode / no dropped layers): every parameter is
         # used — a replay fires no backward hook, so the hook-based flags would all read "unused"
         one = torch.ones(1, dtype=torch.int32, device=self.used.device)
-        # a stream-ordered copy from pinned memory: the RCCL step calls this inside its capture
-        idx = torch.tensor([len(flags) if s < 0 else s for s in src], dtype=torch.int64)
-        if self.used.is_cuda:
-            idx = idx.pin_memory().to(self.used.device, non_blocking=True)
+        vals = [len(flags) if s < 0 else s for s in src]
+        if self._idx_host is not None:
+            # a stream-ordered copy from the pinned buffer allocated with the reducer: the RCCL step calls
+            # this inside its capture, where no host memory can be pinned (every capture writes the same
+            # mapping: a parameter's layer does not change)
+            self._idx_host[:len(vals)] = torch.tensor(vals, dtype=torch.int64)
+            idx = self._idx_host[:len(vals)].to(self.used.device, non_blocking=True)
+        else:
+            idx = torch.tensor(vals, dtype=torch.int64, device=self.used.device)
         return (flags + [one], idx)
 
     def use_layer_gates(self, state) -> None:
