@@ -171,9 +171,9 @@ int b2p_set_gate_batch(const int64_t* dev_gate_ptrs);
 /* dst[0 .. n) = vals[0 .. n), n <= 64, by a kernel launch carrying the values (graph-capturable): the
  * pointer / offset tables of batched launches. */
 int b2p_i64_fill(int64_t* dst, const int64_t* vals, int n, b2p_stream_t stream);
-/* Variant knob of the 256-column GEMM launches (A/B tools, default from B2P_GEMM16_VARIANT): 0 = default,
- * 1 = the ping-pong kernel without the quarter-scheduled operand DMA; v < 0 only reads. Returns the
- * previous value. */
+/* Variant knob of the 16-bit GEMM launches (A/B tools, default from B2P_GEMM16_VARIANT), bits: 1 = the
+ * 256-column ping-pong kernel without the quarter-scheduled operand DMA, 2 = no narrow (PBM x 128) ping-pong
+ * kernel; v < 0 only reads. Returns the previous value. */
 int b2p_gemm16_variant(int v);
 int b2p_colsum_pin_begin(void);
 int64_t b2p_colsum_pin_end(void);

@@ -27,11 +27,10 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-Wno-unused-result"]
-# per-source codegen flags. attn16.hip: MFMA results in VGPRs (no v_accvgpr_read of every score / output
-# accumulator before the softmax VALU: 84 fewer VALU instructions per 16-query tile of the forward, 144 in
-# dQ; the same arithmetic, so bitwise the same results). The GRU kernels keep the default: their
-# W_hh fragments live in AGPRs beyond the 256 VGPRs (the VGPR form spilled to scratch).
-EXTRA_FLAGS = {"attn16.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form=1"]}
+# per-source codegen flags (none at present). Tried and reverted: attn16.hip with -mllvm
+# -amdgpu-mfma-vgpr-form=1 (no v_accvgpr_read of the score / output accumulators, 84 fewer VALU
+# instructions per forward tile) ran the forward 32.3 -> 34.1 us.
+EXTRA_FLAGS: dict = {}
 
 
 LIB_STAMP = LIB + ".sha"

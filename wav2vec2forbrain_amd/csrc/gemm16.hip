@@ -68,8 +68,8 @@ bool gemm16_splitk_fused(const b2p_gemm_desc& d) {
   return v4 && d.workspace_floats >= need;
 }
 
-// Kernel variant knob of the 256-column launches (b2p_gemm16_variant, B2P_GEMM16_VARIANT): 0 = default,
-// 1 = the ping-pong kernel without the quarter-scheduled DMA (A/B tools)
+// Kernel variant knob (b2p_gemm16_variant, B2P_GEMM16_VARIANT; A/B tools), bits: 1 = the 256-column ping-pong
+// kernel without the quarter-scheduled DMA, 2 = no narrow ping-pong kernel (those launches on 128 x 128)
 static int g_variant = getenv("B2P_GEMM16_VARIANT") ? atoi(getenv("B2P_GEMM16_VARIANT")) : 0;
 int gemm16_variant_get() { return g_variant; }
 extern "C" int b2p_gemm16_variant(int v) {
@@ -148,6 +148,19 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
         return run(d, st, G16_PP192, ek, (unsigned)t3, tm3, tn, gemm16_group(true));
     }
     return run(d, st, G16_PP, ek, (unsigned)tiles_pp, tm, tn, gemm16_group(true));
+  }
+  // narrow ping-pong tiles, PBM x 128 (B2P_GEMM16_PN: 0 off, 1 (default) for k-contiguous launches with
+  // N <= 1024, 2 for every k-contiguous launch): 192 rows where fewer CU-rounds x tile rows come out of it
+  // (N = 768: 252 tiles in one round), else 256 (N = 1024: 256 tiles); the LDS-staged (GENERIC) epilogue
+  // and 96-row column-sum bands stay on the other kernels
+  static int pn_mode = getenv("B2P_GEMM16_PN") ? atoi(getenv("B2P_GEMM16_PN")) : 1;
+  if (pn_mode && !(gemm16_variant_get() & 2) && nt && !d.A.conv && ek != EK_GENERIC && ext_ok(d.A, d.M) && ext_ok(d.B, d.N) &&
+      (ks == 1 || d.kchunk % 64 == 0) && (pn_mode == 2 || d.N <= 1024)) {
+    const int tn = (int)((d.N + 127) / 128), tm2 = (int)((d.M + 255) / 256), tm3 = (int)((d.M + 191) / 192);
+    const int64_t t256 = (int64_t)tm2 * tn * nz, t192 = (int64_t)tm3 * tn * nz;
+    const int64_t cost256 = (t256 + 255) / 256 * 256, cost192 = (t192 + 255) / 256 * 192;
+    if (!d.ep.colsum_part && cost192 < cost256) return run(d, st, G16_PN192, ek, (unsigned)t192, tm3, tn, gemm16_group(true));
+    return run(d, st, G16_PN256, ek, (unsigned)t256, tm2, tn, gemm16_group(true));
   }
   const int tm = (int)((d.M + 127) / 128), tn = (int)((d.N + 127) / 128);
   const int64_t nwg = (int64_t)tm * tn * nz;

@@ -24,6 +24,15 @@ int gemm16_run_nt_f16(const b2p_gemm_desc& d, hipStream_t st, int fam, uint32_t 
       default: if (ek == EK_GENERIC) launch_pp192<true, true, EK_GENERIC>(d, ea, st, nwg, tm, tn, grp); else launch_pp192<true, true, EK_RUNTIME>(d, ea, st, nwg, tm, tn, grp); return 0;
     }
   }
+  if (fam == G16_PN256 || fam == G16_PN192) {
+    const bool w = fam == G16_PN256;
+    switch (ek) {
+#define B2P_GO_(K) case K: if (w) launch_pn<256, true, K>(d, ea, st, nwg, tm, tn, grp); else launch_pn<192, true, K>(d, ea, st, nwg, tm, tn, grp); return 0;
+      B2P_KINDS_NT_F16(B2P_GO_)
+#undef B2P_GO_
+      default: if (w) launch_pn<256, true, EK_RUNTIME>(d, ea, st, nwg, tm, tn, grp); else launch_pn<192, true, EK_RUNTIME>(d, ea, st, nwg, tm, tn, grp); return 0;
+    }
+  }
   if (fam == G16_SMALL) {
     switch (ek) {
 #define B2P_GO_(K) case K: launch_small<CfgSmall, true, true, false, true, K>(d, ea, st, nwg, tm, tn, grp); return 0;
