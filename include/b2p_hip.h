@@ -96,8 +96,8 @@ typedef struct {
   /* bf16 LDS-DMA kernel only (both operands bf16), nz1*nz2 == 1, no split-K:                   */
   uint16_t* pre16;            /* optional bf16 pre-activation store (instead of pre_out)       */
   const uint16_t* aux16;      /* act_bwd operand in bf16 (instead of aux; strides of aux)      */
-  float* colsum_part;         /* optional: column sums of the final value per 64 output rows,
-                               * [ceil(M/64)][N] floats (fused bias gradient; b2p_colsum_parts) */
+  float* colsum_part;         /* optional: column sums of the final value per 32 output rows,
+                               * [ceil(M/32)][N] floats (fused bias gradient; b2p_colsum_parts) */
   uint16_t* C16b;             /* optional second copy in bf16 beside an fp16 C16 (strides of C): the
                                * forward's fp16 operand and the backward's bf16 weight-gradient
                                * operand from one epilogue                                        */

@@ -13,6 +13,7 @@ int main(int argc, char** argv) {
   const int M = argc > 1 ? atoi(argv[1]) : 8192, N = argc > 2 ? atoi(argv[2]) : 2048, K = argc > 3 ? atoi(argv[3]) : 256;
   const int c16 = argc > 4 ? atoi(argv[4]) : 0;   // 0: fp32 C, 1: bf16 C16 only, 2: both + bias
   const int act = argc > 5 ? atoi(argv[5]) : 0;   // B2P_ACT_* in the epilogue
+  const int tn = argc > 6 ? atoi(argv[6]) : 0;    // 1: both operands m/n-contiguous (the weight-gradient layout)
   std::vector<uint16_t> ha((size_t)M * K), hb((size_t)N * K);
   uint32_t x = 1;
   for (auto& v : ha) { x = x * 1664525u + 1013904223u; v = 0x3c00 + ((x >> 16) & 0x7f) + ((x >> 31) << 15); }
@@ -23,8 +24,8 @@ int main(int argc, char** argv) {
   hipMemcpy(b, hb.data(), hb.size() * 2, hipMemcpyHostToDevice);
   b2p_gemm_desc d{};
   d.M = M; d.N = N; d.K = K; d.nz1 = d.nz2 = 1;
-  d.A.ptr = a; d.A.ld = K; d.A.inner_is_k = 1; d.A.dtype = 1;
-  d.B.ptr = b; d.B.ld = K; d.B.inner_is_k = 1; d.B.dtype = 1;
+  d.A.ptr = a; d.A.ld = tn ? M : K; d.A.inner_is_k = tn ? 0 : 1; d.A.dtype = 1;
+  d.B.ptr = b; d.B.ld = tn ? N : K; d.B.inner_is_k = tn ? 0 : 1; d.B.dtype = 1;
   void *c2 = nullptr, *bias = nullptr;
   if (c16 == 1) d.ep.C16 = (uint16_t*)c;
   else d.ep.C = (float*)c;

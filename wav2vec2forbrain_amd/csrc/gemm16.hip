@@ -103,7 +103,11 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   const int ks = d.ksplit > 1 ? d.ksplit : 1;
   const int64_t nz = (int64_t)d.nz1 * d.nz2 * ks;
   const bool h16 = d.A.dtype == 2;
-  const uint32_t ek = epi_kind(d, ea);
+  uint32_t ek = epi_kind(d, ea);
+  // fused column sums only in their instantiated kinds (bf16, k-contiguous); anything else takes the
+  // LDS-staged epilogue, so the runtime-kind kernels carry no column-sum code
+  if ((ek & EK_CSUM) && !(d.A.inner_is_k && d.B.inner_is_k && d.A.dtype != 2 && (ek == K_GDH16CS || ek == K_GDH32CS)))
+    ek = EK_GENERIC;
   if (ea.gates && !(ek == K_F || ek == K_FB || ek == K_SLAB)) {
     b2p_set_error("gemm16: per-member gates need a plain (C or beta) epilogue");
     return 1;
@@ -138,9 +142,9 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   if (pp) {
     const int tm = (int)((d.M + 255) / 256), tn = (int)((d.N + 255) / 256);
     // 192 x 256 tiles (B2P_GEMM16_PP192: 0 off, 1 (default) when fewer rounds of the 256 CUs x tile rows
-    // come out at least 8 % lower, 2 always): k-contiguous A, no colsum (its partial rows are 64-row bands)
+    // come out at least 8 % lower, 2 always): k-contiguous A
     static int pp192 = getenv("B2P_GEMM16_PP192") ? atoi(getenv("B2P_GEMM16_PP192")) : 1;
-    if (pp192 && nt && !d.ep.colsum_part) {
+    if (pp192 && nt) {
       const int tm3 = (int)((d.M + 191) / 192);
       const int64_t t3 = (int64_t)tm3 * tn * nz;
       const int64_t cost256 = (tiles_pp + 255) / 256 * 256, cost192 = (t3 + 255) / 256 * 192;
@@ -152,14 +156,14 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
   // narrow ping-pong tiles, PBM x 128 (B2P_GEMM16_PN: 0 off, 1 (default) for k-contiguous launches with
   // N <= 1024, 2 for every k-contiguous launch): 192 rows where fewer CU-rounds x tile rows come out of it
   // (N = 768: 252 tiles in one round), else 256 (N = 1024: 256 tiles); the LDS-staged (GENERIC) epilogue
-  // and 96-row column-sum bands stay on the other kernels
+  // stays on the other kernels
   static int pn_mode = getenv("B2P_GEMM16_PN") ? atoi(getenv("B2P_GEMM16_PN")) : 1;
   if (pn_mode && !(gemm16_variant_get() & 2) && nt && !d.A.conv && ek != EK_GENERIC && ext_ok(d.A, d.M) && ext_ok(d.B, d.N) &&
       (ks == 1 || d.kchunk % 64 == 0) && (pn_mode == 2 || d.N <= 1024)) {
     const int tn = (int)((d.N + 127) / 128), tm2 = (int)((d.M + 255) / 256), tm3 = (int)((d.M + 191) / 192);
     const int64_t t256 = (int64_t)tm2 * tn * nz, t192 = (int64_t)tm3 * tn * nz;
     const int64_t cost256 = (t256 + 255) / 256 * 256, cost192 = (t192 + 255) / 256 * 192;
-    if (!d.ep.colsum_part && cost192 < cost256) return run(d, st, G16_PN192, ek, (unsigned)t192, tm3, tn, gemm16_group(true));
+    if (cost192 < cost256) return run(d, st, G16_PN192, ek, (unsigned)t192, tm3, tn, gemm16_group(true));
     return run(d, st, G16_PN256, ek, (unsigned)t256, tm2, tn, gemm16_group(true));
   }
   const int tm = (int)((d.M + 127) / 128), tn = (int)((d.N + 127) / 128);

@@ -1072,8 +1072,9 @@ def _colsum_ws(M, N, device):
 
 
 def colsum_parts_buf(M, N, device):
-    """Workspace for a GEMM epilogue's fused column sums (one row per 64 output rows)."""
-    return torch.empty(-(-M // 64), N, device=device)
+    """Workspace for a GEMM epilogue's fused column sums (one partial row per 32 output rows: every wave row
+    block of the GEMM kernels, 64 / 96 / 128 rows, starts on a 32-row band)."""
+    return torch.empty(-(-M // 32), N, device=device)
 
 
 def colsum_from_parts(parts, out):
