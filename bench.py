@@ -313,7 +313,7 @@ def timed_run(kind, args, world, rank, device, use_graph, steps=None, warmup=Non
         Fn.set_gemm_timing(True)
         if trainer.reducer is not None:
             trainer.reducer.use_layer_gates(None)
-        with Fn.precision(prec):
+        with trainer.precision_context():
             for _ in range(args.steps):
                 trainer._eager_body(batch)
         torch.cuda.synchronize()
@@ -584,8 +584,11 @@ def ft_record(args, device):
     r = timed_run("conformer_ft", args, 1, 0, device, graph, steps=10, warmup=3)
     x3 = r["precision"] == "bf16x3"
     roof = roofline_record(r["gemm"], "conformer_ft")
-    if x3:   # three bf16 MFMA products per algorithmic multiply-add
-        roof.update(mfma_work_per_flop=3, mfma_frac=round(3 * roof["frac"], 4))
+    if x3:   # bf16 MFMA products per algorithmic multiply-add under the policy's per-role forms
+        from wav2vec2forbrain_amd import functional as Fn
+        w = Fn.x3_mfma_work(Fn.X3_POLICY_FORMS)
+        roof.update(mfma_work_per_flop=round(w, 3), mfma_frac=round(w * roof["frac"], 4),
+                    x3_forms=",".join(sorted(Fn.X3_POLICY_FORMS)) or "three-term everywhere")
     rec = nested(r, "train steps/sec + CTC loss, b2p2t_gru+w2v_conformer-large unfreeze=brain_encoder+w2v bs=8 "
                     "seq=1024 (configs[4] per GPU)",
                  {"workload": WORKLOAD_TEXT["conformer"].replace("unfreeze=brain_encoder", "unfreeze=brain_encoder+w2v "
@@ -626,6 +629,7 @@ def fp32_mode_record(kind, args, device, steps=3):
             m.sync_metrics = False
     with Fn.precision("fp32"):
         trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+        graphs = trainer.use_graphs
         trainer.use_graphs = False
         batch = batch_on(cfg, device)
         trainer.train_step(batch)
@@ -636,12 +640,28 @@ def fp32_mode_record(kind, args, device, steps=3):
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
         loss = float(out.loss)
+        # the same step captured once and replayed (the bf16 records' step mode): no Python launch cost
+        rep = None
+        if graphs:
+            trainer.use_graphs, trainer.capture_after = True, 0
+            trainer.train_step(batch)    # capture (untimed)
+            torch.cuda.synchronize()
+            g0 = trainer.graph_steps
+            t0 = time.perf_counter()
+            for _ in range(steps):
+                out = trainer.train_step(batch)
+            torch.cuda.synchronize()
+            dtr = time.perf_counter() - t0
+            if trainer.graph_steps - g0 == steps:
+                rep = {"value": round(steps / dtr, 4), "ms_per_step": round(dtr / steps * 1e3, 2),
+                       "step_mode": "hip-graph replay of Trainer.train_step", "ctc_loss": round(float(out.loss), 5)}
+            trainer.release_graphs()
     Fn.set_deferred_wgrad([])
     del trainer, model, batch
     free_device()
     return {"value": round(steps / dt, 4), "unit": "steps/s", "ms_per_step": round(dt / steps * 1e3, 2),
             "steps": steps, "warmup": 1, "dtype": "fp32 (exact-fp32 MFMA, the reference's arithmetic)",
-            "step_mode": "eager Trainer.train_step", "ctc_loss": round(loss, 5)}
+            "step_mode": "eager Trainer.train_step", "ctc_loss": round(loss, 5), "replayed": rep}
 
 
 def gemm_traffic(kind="base"):

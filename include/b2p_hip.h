@@ -161,7 +161,8 @@ int b2p_colsum_batched(const float* X, const float* Y, int64_t batch, int64_t M,
 /* bf16x3 mode: the split-bf16 image of an R x C fp32 operand (hi = bf16(x), lo = bf16(x - hi)) as three
  * blocks, block b = lo when bit b of pattern is set (A: hi, lo, hi = 0b010; B: hi, hi, lo = 0b100), side
  * by side per row (along_cols, ldy >= 3C) or stacked (ldy >= C): one bf16 GEMM over K' = 3K then sums
- * hi*hi + lo*hi + hi*lo (replaces the reference's fp32 matmuls at ~16 significant bits per product). */
+ * hi*hi + lo*hi + hi*lo (replaces the reference's fp32 matmuls at ~16 significant bits per product).
+ * pattern | 16: two blocks (bits 0-1; ldy >= 2C side by side): the two-term images (hi, lo) . (hi, hi). */
 int b2p_split3_bf16(const float* x, int64_t R, int64_t C, int64_t ldx, uint16_t* y, int64_t ldy, int pattern,
                     int along_cols, b2p_stream_t stream);
 /* Per-member LayerDrop gates of a batched GEMM launch (nz1 members; the frozen weight gradients of several

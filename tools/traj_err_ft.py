@@ -130,8 +130,9 @@ print(f"  ({time.time() - t0:.1f} s)", flush=True)
 for v in variants:
     t0 = time.time()
     bo, sw, em, mode = (), (), None, "bf16"
-    if v.startswith("M:"):
-        mode = v[2:]
+    if v.startswith("M:"):   # M:<mode>[/switch+switch]
+        mode, _, xs = v[2:].partition("/")
+        sw = tuple(filter(None, xs.split("+")))
     elif v.startswith("E:"):
         _, bw, sc = v.split(":")
         em = (bw, float(sc))

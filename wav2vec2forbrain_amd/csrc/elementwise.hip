@@ -1284,7 +1284,8 @@ extern "C" int b2p_cast16_2d(const float* x, int64_t R, int64_t C, int64_t ldx, 
 // bf16(x - hi), written as three blocks (block b = lo when bit b of `pattern` is set, else hi), side by
 // side in every row (along_cols: y[r][b*C + c], the k-contiguous operands) or stacked (y[b*R + r][c]).
 // A GEMM over the 3x-deep K of an A image (hi, lo, hi) and a B image (hi, hi, lo) sums hi*hi + lo*hi +
-// hi*lo in one launch on the bf16 MFMA kernels, with its full epilogue.
+// hi*lo in one launch on the bf16 MFMA kernels, with its full epilogue. pattern & 16: two blocks (the
+// two-term images (hi, lo) . (hi, hi), one operand kept to ~16 bits, the other rounded to bf16).
 __global__ void __launch_bounds__(256) split3_bf16_k(const float* __restrict__ x, int64_t R, int64_t C, int64_t ldx,
                                                      uint16_t* __restrict__ y, int64_t ldy, int pattern, int along_cols) {
   const int64_t c4 = (C + 3) / 4;
@@ -1312,8 +1313,10 @@ __global__ void __launch_bounds__(256) split3_bf16_k(const float* __restrict__ x
   }
   const uint2 hv = make_uint2((uint32_t)hb[0] | ((uint32_t)hb[1] << 16), (uint32_t)hb[2] | ((uint32_t)hb[3] << 16));
   const uint2 lv = make_uint2((uint32_t)lb[0] | ((uint32_t)lb[1] << 16), (uint32_t)lb[2] | ((uint32_t)lb[3] << 16));
+  const int nb = (pattern & 16) ? 2 : 3;
 #pragma unroll
   for (int b = 0; b < 3; ++b) {
+    if (b >= nb) break;
     uint16_t* ys = along_cols ? y + r * ldy + b * C + c : y + (b * R + r) * ldy + c;
     const bool lo = (pattern >> b) & 1;
     if (nv == 4 && ((uintptr_t)ys & 7u) == 0) {
@@ -1329,7 +1332,8 @@ __global__ void __launch_bounds__(256) split3_bf16_k(const float* __restrict__ x
 extern "C" int b2p_split3_bf16(const float* x, int64_t R, int64_t C, int64_t ldx, uint16_t* y, int64_t ldy, int pattern,
                                int along_cols, b2p_stream_t stream) {
   B2P_CHECK_ARG(x && y, "split3_bf16: NULL pointer");
-  B2P_CHECK_ARG(R >= 0 && C >= 0 && ldx >= C && ldy >= (along_cols ? 3 * C : C), "split3_bf16: bad shape / strides");
+  B2P_CHECK_ARG(R >= 0 && C >= 0 && ldx >= C && ldy >= (along_cols ? ((pattern & 16) ? 2 : 3) * C : C),
+                "split3_bf16: bad shape / strides");
   if (R == 0 || C == 0) return 0;
   const int64_t n = R * ((C + 3) / 4);
   hipLaunchKernelGGL(split3_bf16_k, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, x, R, C, ldx,

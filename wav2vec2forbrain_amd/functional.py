@@ -40,6 +40,7 @@ class _State:
     sync_bn = None   # process group for synchronised BatchNorm statistics (sync_batchnorm())
     gate = None      # LayerDrop gate (device int32) of the layer being issued in a captured step
     block = None     # error attribution: the B2P_FP32_OPS block whose forward is being issued
+    x3forms = None   # x3_forms(): GEMM roles the bf16x3 mode runs single-pass / on two-term images
 
 
 _state = _State()
@@ -864,6 +865,15 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
          aux16=None, colsum_part=None, c16_fp16=False, C16b=None):
     """C may be None when only the bf16 copy C16 (same strides) is wanted. Both operands bf16
     (Operand.dtype 1) selects the LDS-DMA kernel (gemm16.hip)."""
+    if _state.prec == 3 and A.dtype == 0 and B.dtype == 0 and _x3_single(A, B):
+        # bf16x3 policy with a single-pass role (forward on fp16, see _x3_single): this GEMM as in bf16 mode
+        kw = dict(locals())
+        old = _state.prec
+        _state.prec = 0
+        try:
+            return gemm(**kw)
+        finally:
+            _state.prec = old
     d = GemmDesc()
     d.M, d.N, d.K = M, N, K
     d.nz1, d.nz2 = nz1, nz2
@@ -905,10 +915,15 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     if _X3_SPLIT[0] and _state.prec == 3 and A.dtype == 0 and B.dtype == 0 and _auto16_ok(M, N, K, A, B, nz1, nz2):
         # bf16x3: split-bf16 images of both operands over K' = 3K, one launch on the bf16 LDS-DMA kernels
         dev = (C if C is not None else C16).device
-        keep16 = (_split3_operand(A, M, K, 0b010, dev), _split3_operand(B, N, K, 0b100, dev))
+        form = _x3_form(A, B)
+        if form in ("2a", "2b"):   # two-term images over K' = 2K: (hi, lo) . (hi, hi) or the reverse
+            pa, pb = (0b10, 0b00) if form == "2a" else (0b00, 0b10)
+            keep16 = (_split3_operand(A, M, K, pa | _SPLIT2, dev), _split3_operand(B, N, K, pb | _SPLIT2, dev))
+        else:
+            keep16 = (_split3_operand(A, M, K, 0b010, dev), _split3_operand(B, N, K, 0b100, dev))
         A, B = keep16[0][1], keep16[1][1]
         d.A, d.B = A, B
-        K = 3 * K
+        K = (2 if form in ("2a", "2b") else 3) * K
         d.K = K
         d.precision = 0
     d.timing_family = timing or _GEMM_TIMING[0]
@@ -955,18 +970,88 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
     _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
 
 
+def _x3_role(A, B) -> str:
+    """The role of a bf16x3-mode fp32-operand GEMM by the operand layouts of a Linear: forward (inside
+    forward_f16), backward-data (A k-contiguous, B n-contiguous) or weight gradient (both m/n-contiguous)."""
+    if _state.fwd16:
+        return "fwd"
+    if A.inner_is_k and not B.inner_is_k:
+        return "dgrad"
+    if not A.inner_is_k and not B.inner_is_k:
+        return "wgrad"
+    return "other"
+
+
+def _x3_form(A, B) -> str:
+    """How the bf16x3 mode runs this GEMM (B2P_X3_SINGLE / the Trainer policy's role set, or the
+    diagnostic switches of tools/traj_err_ft.py): '' split-bf16 three-term images; '1' single pass as in
+    the bf16 mode (forward on fp16 operands); '2a' / '2b' two-term images (hi*hi + lo*hi: A kept to
+    ~16 bits, B rounded to bf16 / the reverse)."""
+    forms = _state.x3forms if _state.x3forms is not None else _X3_SINGLE
+    if not forms and not DIAG_SWITCHES:
+        return ""
+    role = _x3_role(A, B)
+    for form in ("1", "2a", "2b"):
+        if role + form in forms or role + form in DIAG_SWITCHES or (form == "1" and role in forms):
+            return form
+    return ""
+
+
+def _x3_single(A, B) -> bool:
+    return _x3_form(A, B) == "1"
+
+
+_X3_SINGLE = set(filter(None, os.environ.get("B2P_X3_SINGLE", "").split(",")))
+
+# The Trainer's bf16x3 policy (configs[4]: the w2v encoder trained) runs the weight-gradient GEMMs
+# single-pass (bf16) and the backward-data GEMMs on two-term images (the gradient rounded to bf16, the
+# weight kept to ~16 bits); forward GEMMs stay three-term. Measured on conformer_large_ft_bs8 against the
+# reference's trajectory (tools/ft_policy_ab.py, profiles/r06m_ft_policy_ab.txt): three-term everywhere
+# 8.1e-5 at step 3, 91.6 ms/step; this set 2.1e-4, 83.6 ms; forward single-pass (fp16) or two-term
+# 3.1e-3 .. 1.4e-2, backward-data single-pass 2.2e-3 (both past the 1e-3 gate).
+# B2P_X3_POLICY=<roles> overrides it ('none': three-term everywhere).
+X3_POLICY_FORMS = frozenset(filter(None, os.environ.get("B2P_X3_POLICY", "wgrad,dgrad2b").replace("none", "").split(",")))
+
+
+def x3_mfma_work(forms) -> float:
+    """bf16 MFMA products per algorithmic multiply-add of a bf16x3 step under `forms`, the three GEMM
+    roles (forward, backward-data, weight gradient) weighted equally (each ~1/3 of a Linear's FLOPs)."""
+    def terms(role):
+        for form, n in (("1", 1), ("2a", 2), ("2b", 2)):
+            if role + form in forms or (form == "1" and role in forms):
+                return n
+        return 3
+    return sum(terms(r) for r in ("fwd", "dgrad", "wgrad")) / 3.0
+
+
+@contextlib.contextmanager
+def x3_forms(forms):
+    """The bf16x3 mode's per-role GEMM forms inside (see _x3_form; None: B2P_X3_SINGLE)."""
+    old = _state.x3forms
+    _state.x3forms = None if forms is None else frozenset(forms)
+    try:
+        yield
+    finally:
+        _state.x3forms = old
+
+
 # bf16x3 mode: large plain fp32-operand GEMMs run as one bf16 GEMM over split-bf16 operand images
 # (B2P_X3_SPLIT=0: the fp32-operand kernel's three-MFMA form, csrc/gemm.hip precision 3)
 _X3_SPLIT = [os.environ.get("B2P_X3_SPLIT", "1") != "0"]
 
 
+_SPLIT2 = 0x10   # b2p_split3_bf16 pattern flag: two K-blocks instead of three
+
+
 def _split3_operand(o, mn, K, pattern, dev):
-    """The split-bf16 image of the logical (mn x K) fp32 operand o: three K-blocks (hi / lo per pattern
-    bit), along the rows of a k-contiguous operand, stacked for an m/n-contiguous one; (buffer, Operand)."""
+    """The split-bf16 image of the logical (mn x K) fp32 operand o: three (pattern & _SPLIT2: two)
+    K-blocks (hi / lo per pattern bit), along the rows of a k-contiguous operand, stacked for an
+    m/n-contiguous one; (buffer, Operand)."""
     rows, cols = (mn, K) if o.inner_is_k else (K, mn)
     along = bool(o.inner_is_k)
-    ld16 = -(-(3 * cols if along else cols) // 8) * 8
-    buf = torch.empty(rows if along else 3 * rows, ld16, device=dev, dtype=BF16)
+    nb = 2 if pattern & _SPLIT2 else 3
+    ld16 = -(-(nb * cols if along else cols) // 8) * 8
+    buf = torch.empty(rows if along else nb * rows, ld16, device=dev, dtype=BF16)
     _lib.call("b2p_split3_bf16", o.ptr, rows, cols, o.ld, buf.data_ptr(), ld16, pattern, int(along), _st())
     n = Operand()
     n.ptr = buf.data_ptr()

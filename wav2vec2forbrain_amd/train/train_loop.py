@@ -4,6 +4,7 @@ torch.distributed is initialised: gradients of the optimised parameters are all-
 train.ddp.GradBucketReducer overlapped with backward."""
 from __future__ import annotations
 
+import contextlib
 import dataclasses
 import os
 import uuid
@@ -244,11 +245,19 @@ class Trainer:
             Fn.set_deferred_wgrad(self._setup_dp(opt_ids), names=self._param_names())
             enc = getattr(self.model, "w2v_encoder", None)
             self.encoder_trained = enc is not None and any(id(p) in opt_ids for p in enc.parameters())
+        with self.precision_context():
+            return self._train_step(batch)
+
+    def precision_context(self):
+        """The precision mode of this Trainer's steps (step_precision) and, in the bf16x3 policy, its
+        per-role GEMM forms (functional.X3_POLICY_FORMS)."""
         mode = self.step_precision()
-        if mode is None:
-            return self._train_step(batch)
-        with Fn.precision(mode):
-            return self._train_step(batch)
+        stack = contextlib.ExitStack()
+        if mode is not None:
+            stack.enter_context(Fn.precision(mode))
+            if mode == "bf16x3":
+                stack.enter_context(Fn.x3_forms(Fn.X3_POLICY_FORMS))
+        return stack
 
     def _train_step(self, batch: SampleBatch):
         """One training step. The first `capture_after` steps of a batch shape run eagerly; then the
