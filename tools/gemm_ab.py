@@ -75,6 +75,7 @@ SHAPES = [
     (7968, 4096, 1024, "badh", True, True),   # Conformer-large FFN1 forward
     (7968, 1024, 4096, "bdrf", True, True),   # Conformer-large FFN2 forward
     (7968, 3072, 1024, "bh", True, True),     # Conformer-large QKV
+    (7968, 2048, 1024, "bh", True, True),     # Conformer-large pointwise conv 1
     (4096, 1024, 7968, "f", False, False),    # Conformer-large FFN weight gradient
 ]
 

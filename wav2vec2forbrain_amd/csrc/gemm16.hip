@@ -154,12 +154,15 @@ int b2p_gemm16_launch(const b2p_gemm_desc& d, hipStream_t st) {
     return run(d, st, G16_PP, ek, (unsigned)tiles_pp, tm, tn, gemm16_group(true));
   }
   // narrow ping-pong tiles, PBM x 128 (B2P_GEMM16_PN: 0 off, 1 (default) for k-contiguous launches with
-  // N <= 1024, 2 for every k-contiguous launch): 192 rows where fewer CU-rounds x tile rows come out of it
+  // N <= B2P_GEMM16_PN_MAX_N, 2 for every k-contiguous launch): 192 rows where fewer CU-rounds x tile rows come out of it
   // (N = 768: 252 tiles in one round), else 256 (N = 1024: 256 tiles); the LDS-staged (GENERIC) epilogue
   // stays on the other kernels
+  // N <= 2048 (round 6, tools/gemm_ab.py, profiles/r06o_pn_wide_ab.txt): the Conformer's pointwise conv 1
+  // (7968 x 2048 x 1024) 56.2 -> 49.8 us; the QKV projection (N = 2304) is slower on it (53.8 -> 57.2 us)
   static int pn_mode = getenv("B2P_GEMM16_PN") ? atoi(getenv("B2P_GEMM16_PN")) : 1;
+  static int pn_max_n = getenv("B2P_GEMM16_PN_MAX_N") ? atoi(getenv("B2P_GEMM16_PN_MAX_N")) : 2048;
   if (pn_mode && !(gemm16_variant_get() & 2) && nt && !d.A.conv && ek != EK_GENERIC && ext_ok(d.A, d.M) && ext_ok(d.B, d.N) &&
-      (ks == 1 || d.kchunk % 64 == 0) && (pn_mode == 2 || d.N <= 1024)) {
+      (ks == 1 || d.kchunk % 64 == 0) && (pn_mode == 2 || d.N <= pn_max_n)) {
     const int tn = (int)((d.N + 127) / 128), tm2 = (int)((d.M + 255) / 256), tm3 = (int)((d.M + 191) / 192);
     const int64_t t256 = (int64_t)tm2 * tn * nz, t192 = (int64_t)tm3 * tn * nz;
     const int64_t cost256 = (t256 + 255) / 256 * 256, cost192 = (t192 + 255) / 256 * 192;

@@ -81,7 +81,10 @@ __device__ __forceinline__ uint32_t ln_step(int d, int bg, int nbg, int T, int s
 // giL: LN(R=3) of x W_ih^T + b_ih + (b_hr, b_hz, 0) (b_hh's r/z parts folded by the caller: they
 // only ever appear summed with it); bhh [ndir][3H] (null = 0) is read for b_hn only; h0 [ndir][B][H]
 // or null. Outputs hL: LN(R=1) of h; savL: LN(R=4) of (r, z, n, W_hn h + b_hn).
-template <int H>
+// DIAG (tools/gru_probe.hip ablations only; 0 in the library): 1 no MFMAs, 2 no gate nonlinearities,
+// 4 no global stores, 8 no workgroup barrier, 16 no gi loads. SPLIT: the two unit blocks' K loops one
+// after the other, block 0's gate math and stores interleaved with block 1's MFMAs
+template <int H, int DIAG = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(H * 2) gru16_fwd(const float* __restrict__ giL, const float* __restrict__ whh,
                                                    const float* __restrict__ bhh, const float* __restrict__ h0,
                                                    float* __restrict__ hL, float* __restrict__ savL, int B, int T,
@@ -135,6 +138,13 @@ __global__ void __launch_bounds__(H * 2) gru16_fwd(const float* __restrict__ giL
   // gi is prefetched one time step ahead: its r/z parts become the MFMA accumulator inputs (they
   // are summed with W_h{r,z} h anyway), its n part waits for r
   auto load_gi = [&](int s, float4 (&g)[2][3]) {
+    if (DIAG & 16) {
+#pragma unroll
+      for (int ub = 0; ub < 2; ++ub)
+#pragma unroll
+        for (int q = 0; q < 3; ++q) g[ub][q] = make_float4(0.01f * s, 0.f, 0.f, 0.f);
+      return;
+    }
     const uint32_t o = ln_step(d, bg, nbg, T, s, H, 3) + 3 * wb + lo;
 #pragma unroll
     for (int ub = 0; ub < 2; ++ub)
@@ -157,10 +167,83 @@ __global__ void __launch_bounds__(H * 2) gru16_fwd(const float* __restrict__ giL
     const bf16x8* wnl = wn_lds + (w * 2) * KS * 64 + l;
     // LDS fragments one k-step ahead of the MFMAs; the sched barrier keeps the compiler from
     // hoisting every k-step's loads (that spills the VGPR-resident W_hh fragments)
+    uint16_t* hnxt = hb + ((s + 1) & 1) * BG * HP;
+    const uint32_t oh = ln_step(d, bg, nbg, T, s, H, 1) + lane_b;
+    const uint32_t osv = ln_step(d, bg, nbg, T, s, H, 4) + 4 * wb + lo;
+    // gate math, stores and h hand-off of unit block ub; part = -1: all of it, else the slice of it that
+    // rides along k-step `part` of the other block's MFMAs (elements 0-3, then the stores)
+    float rr[2][4], zz[2][4], nn[2][4], hh[2][4];
+    auto finish = [&](int ub, int part) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (part >= 0 && part != i) continue;
+        if (DIAG & 2) {
+          rr[ub][i] = acc[ub][0][i];
+          zz[ub][i] = acc[ub][1][i];
+          nn[ub][i] = comp(gc[ub][2], i) + rr[ub][i] * acc[ub][2][i];
+        } else {
+          rr[ub][i] = sigm(acc[ub][0][i]);
+          zz[ub][i] = sigm(acc[ub][1][i]);
+          nn[ub][i] = tanh_fast(comp(gc[ub][2], i) + rr[ub][i] * acc[ub][2][i]);
+        }
+        hh[ub][i] = bok ? (1.f - zz[ub][i]) * nn[ub][i] + zz[ub][i] * hp[ub][i] : 0.f;
+        hp[ub][i] = hh[ub][i];
+      }
+      const int j0 = (2 * w + ub) * 16 + 4 * lq;
+      const uint32_t o = osv + (uint32_t)ub * 4096u;
+      if (part < 0 || part == 4) {
+        *reinterpret_cast<uint2*>(hnxt + lr * HP + j0) =
+            b2p_pack_f16x4(make_float4(hh[ub][0], hh[ub][1], hh[ub][2], hh[ub][3]));
+        if (!(DIAG & 4) || s == T - 1)
+          bst4(h_r, oh + (uint32_t)ub * 1024u, make_float4(hh[ub][0], hh[ub][1], hh[ub][2], hh[ub][3]));
+      }
+      if ((part < 0 || part == 5) && (!(DIAG & 4) || s == T - 1)) {
+        bst4(sv_r, o, make_float4(rr[ub][0], rr[ub][1], rr[ub][2], rr[ub][3]));
+        bst4(sv_r, o + 1024u, make_float4(zz[ub][0], zz[ub][1], zz[ub][2], zz[ub][3]));
+      }
+      if ((part < 0 || part == 6) && (!(DIAG & 4) || s == T - 1)) {
+        bst4(sv_r, o + 2048u, make_float4(nn[ub][0], nn[ub][1], nn[ub][2], nn[ub][3]));
+        bst4(sv_r, o + 3072u, make_float4(acc[ub][2][0], acc[ub][2][1], acc[ub][2][2], acc[ub][2][3]));
+      }
+    };
     bf16x8 bf = *reinterpret_cast<const bf16x8*>(hcur);
     bf16x8 an0 = wnl[0], an1 = wnl[KS * 64];
+    if (SPLIT && !(DIAG & 1)) {
+      // block 0's K loop, then block 1's with block 0's gate math / stores interleaved one slice per
+      // k-step: the VALU work of one block runs while the other block's MFMAs occupy the matrix core
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 bfn = bf, an0n = an0;
+        if (ks + 1 < KS) {
+          bfn = *reinterpret_cast<const bf16x8*>(hcur + 32 * (ks + 1));
+          an0n = wnl[(ks + 1) * 64];
+        }
+        acc[0][0] = b2p_mfma_f16(wr[0][ks], bf, acc[0][0]);
+        acc[0][1] = b2p_mfma_f16(wz[0][ks], bf, acc[0][1]);
+        acc[0][2] = b2p_mfma_f16(an0, bf, acc[0][2]);
+        __builtin_amdgcn_sched_barrier(0);
+        bf = bfn; an0 = an0n;
+      }
+      bf = *reinterpret_cast<const bf16x8*>(hcur);
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 bfn = bf, an1n = an1;
+        if (ks + 1 < KS) {
+          bfn = *reinterpret_cast<const bf16x8*>(hcur + 32 * (ks + 1));
+          an1n = wnl[(KS + ks + 1) * 64];
+        }
+        acc[1][0] = b2p_mfma_f16(wr[1][ks], bf, acc[1][0]);
+        acc[1][1] = b2p_mfma_f16(wz[1][ks], bf, acc[1][1]);
+        acc[1][2] = b2p_mfma_f16(an1, bf, acc[1][2]);
+        if (KS >= 8) finish(0, ks);   // parts 0-6
+        __builtin_amdgcn_sched_barrier(0);
+        bf = bfn; an1 = an1n;
+      }
+      if (KS < 8) finish(0, -1);
+      finish(1, -1);
+    }
+#pragma unroll
+    for (int ks = 0; ks < ((DIAG & 1) || SPLIT ? 0 : KS); ++ks) {
       bf16x8 bfn = bf, an0n = an0, an1n = an1;
       if (ks + 1 < KS) {
         bfn = *reinterpret_cast<const bf16x8*>(hcur + 32 * (ks + 1));
@@ -176,30 +259,14 @@ __global__ void __launch_bounds__(H * 2) gru16_fwd(const float* __restrict__ giL
       __builtin_amdgcn_sched_barrier(0);
       bf = bfn; an0 = an0n; an1 = an1n;
     }
-    uint16_t* hnxt = hb + ((s + 1) & 1) * BG * HP;
-    const uint32_t oh = ln_step(d, bg, nbg, T, s, H, 1) + lane_b;
-    const uint32_t osv = ln_step(d, bg, nbg, T, s, H, 4) + 4 * wb + lo;
-#pragma unroll
-    for (int ub = 0; ub < 2; ++ub) {
-      const int j0 = (2 * w + ub) * 16 + 4 * lq;
-      float rr[4], zz[4], nn[4], hh[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        rr[i] = sigm(acc[ub][0][i]);
-        zz[i] = sigm(acc[ub][1][i]);
-        nn[i] = tanh_fast(comp(gc[ub][2], i) + rr[i] * acc[ub][2][i]);
-        hh[i] = bok ? (1.f - zz[i]) * nn[i] + zz[i] * hp[ub][i] : 0.f;
-        hp[ub][i] = hh[i];
-      }
-      bst4(h_r, oh + (uint32_t)ub * 1024u, make_float4(hh[0], hh[1], hh[2], hh[3]));
-      const uint32_t o = osv + (uint32_t)ub * 4096u;
-      bst4(sv_r, o, make_float4(rr[0], rr[1], rr[2], rr[3]));
-      bst4(sv_r, o + 1024u, make_float4(zz[0], zz[1], zz[2], zz[3]));
-      bst4(sv_r, o + 2048u, make_float4(nn[0], nn[1], nn[2], nn[3]));
-      bst4(sv_r, o + 3072u, make_float4(acc[ub][2][0], acc[ub][2][1], acc[ub][2][2], acc[ub][2][3]));
-      *reinterpret_cast<uint2*>(hnxt + lr * HP + j0) = b2p_pack_f16x4(make_float4(hh[0], hh[1], hh[2], hh[3]));
+    if (!SPLIT || (DIAG & 1)) {
+      finish(0, -1);
+      finish(1, -1);
     }
-    lds_barrier();
+    if (DIAG & 8)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    else
+      lds_barrier();
   };
   float4 ga[2][3], gb2[2][3];
   load_gi(0, ga);
