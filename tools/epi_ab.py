@@ -15,8 +15,11 @@ from wav2vec2forbrain_amd import functional as Fn  # noqa: E402
 
 BF = torch.bfloat16
 # letters: f fp32 C, h 16-bit C16 (H: fp16), B second bf16 copy, b bias, a GELU (+ pre16), d dropout,
-# g GELU' on aux16, c column sums, r residual
+# g GELU' on aux16, c column sums, r residual, s SiLU (+ pre16)
 VARIANTS = ["f", "h", "H", "bH", "bHB", "baH", "baHB", "bdH", "badH", "badHB", "gh", "gdh", "ghc", "gdhc", "rf", "bdrf"]
+# s: SiLU (+ pre16) instead of GELU (the Conformer's FFN); B2P_EPI_VARIANTS=bH,bsH,... picks a subset
+if os.environ.get("B2P_EPI_VARIANTS"):
+    VARIANTS = os.environ["B2P_EPI_VARIANTS"].split(",")
 
 
 def main():
@@ -39,8 +42,8 @@ def main():
             kw["C16b"] = torch.empty(M, N, device=dev, dtype=BF)
         if "b" in v:
             kw["bias"] = torch.randn(N, device=dev)
-        if "a" in v:
-            kw["act"] = Fn.ACT["gelu"]
+        if "a" in v or "s" in v:
+            kw["act"] = Fn.ACT["gelu" if "a" in v else "silu"]
             kw["pre16"] = torch.empty(M, N, device=dev, dtype=BF)
         if "d" in v:
             kw.update(drop_p=0.1, seed=7)
