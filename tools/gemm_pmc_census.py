@@ -42,7 +42,7 @@ def run(out):
     print(f"logged {len(Fn.GEMM_LOG)} gemm calls")
 
 
-GEMM_KERNELS = ("gemm_kernel<", "gemm16_kernel<", "gemm16_pp_kernel<")
+GEMM_KERNELS = ("gemm_kernel<", "gemm16_kernel<", "gemm16_pp_kernel<", "gemm16_pn_kernel<")
 
 
 def _dispatches(db):

@@ -19,7 +19,8 @@ def main():
     fetch = per_kernel(sys.argv[1], "FETCH_SIZE")
     write = per_kernel(sys.argv[2], "WRITE_SIZE")
     # our GEMM kernels
-    isg = lambda n: "gemm16_kernel<" in n or "gemm_kernel<" in n or "gemm16_pp_kernel<" in n or n.startswith("Cijk_")
+    isg = lambda n: ("gemm16_kernel<" in n or "gemm_kernel<" in n or "gemm16_pp_kernel<" in n or "gemm16_pn_kernel<" in n
+                     or n.startswith("Cijk_"))
     f = [v for _, n, v in fetch if isg(n)]
     w = [v for _, n, v in write if isg(n)]
     fb = 2.0 * 1024.0 * sum(f) / max(len(f), 1)
@@ -27,7 +28,8 @@ def main():
     out = {"kernel": "b2p_gemm (all GEMM launches of bench.py steps)", "launches_fetch": len(f),
            "launches_write": len(w), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
            "traffic_bytes_per_launch": fb + wb,
-           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction) + --pmc WRITE_SIZE, separate passes"}
+           "method": "rocprofv3 --pmc FETCH_SIZE (x2, gfx950 wide-read correction) + --pmc WRITE_SIZE, separate passes"
+                     + ("; side-stream work serialised (B2P_SERIAL_SIDE=1)" if __import__("os").environ.get("B2P_SERIAL_SIDE") == "1" else "")}
     json.dump(out, open(sys.argv[3], "w"), indent=1)
     print(json.dumps(out))
 

@@ -686,7 +686,7 @@ def flush_wgrad(after=None) -> None:
     if not _Deferred.sides:
         n = max(1, int(os.environ.get("B2P_SIDE_STREAMS", "1")))
         _Deferred.sides = [torch.cuda.Stream(device=main.device) for _ in range(n)]
-    sides = _Deferred.sides
+    sides = [main] if SERIAL_SIDE else _Deferred.sides
     for sd in sides:
         if after is not None:
             sd.wait_event(after)
@@ -729,6 +729,12 @@ def flush_wgrad(after=None) -> None:
         _state.nosplit = old
     _Deferred.queue.clear()
     _Deferred.pending = True
+
+
+# B2P_SERIAL_SIDE=1 (measurement only: PMC censuses, whose per-dispatch counters would otherwise mix the
+# concurrent side-stream kernels' bytes into the main stream's): the side-stream work runs on the main
+# stream, in issue order
+SERIAL_SIDE = os.environ.get("B2P_SERIAL_SIDE", "0") == "1"
 
 
 def _join_sides() -> None:
@@ -961,10 +967,12 @@ def gemm(M, N, K, A: Operand, B: Operand, C, ldc, c_off=0, cbs1=0, cbs2=0, nz1=1
                              aconv=int(A.conv), bconv=int(B.conv), ksplit=int(d.ksplit),
                              epi="".join(c for c, f in (("b", bias is not None), ("a", act != 0), ("g", act_bwd != 0),
                                                         ("d", drop_p > 0), ("r", residual is not None),
-                                                        ("h", C16 is not None), ("f", C is not None)) if f),
+                                                        ("h", C16 is not None), ("B", C16b is not None),
+                                                        ("f", C is not None)) if f),
                              # output-side bytes the epilogue must move once (writes + residual / aux / C reads)
                              out_bytes=M * N * nz1 * nz2 * (4 * (C is not None) + 4 * (pre_out is not None)
                                                             + 2 * (C16 is not None) + 2 * (pre16 is not None)
+                                                            + 2 * (C16b is not None)
                                                             + 4 * (residual is not None) + 4 * (beta != 0.0)
                                                             + (2 if aux16 is not None else 4 if aux is not None else 0))))
     _lib.check(_lib.load().b2p_gemm(ctypes.byref(d), _st()), "b2p_gemm")
@@ -2357,7 +2365,7 @@ class _KeepPlan:
         if not _Deferred.sides:
             n_side = max(1, int(os.environ.get("B2P_SIDE_STREAMS", "1")))
             _Deferred.sides = [torch.cuda.Stream(device=main.device) for _ in range(n_side)]
-        side = _Deferred.sides[0]
+        side = main if SERIAL_SIDE else _Deferred.sides[0]
         B, T, nh, p = self.key
         side.wait_stream(main)
         with torch.cuda.stream(side):
