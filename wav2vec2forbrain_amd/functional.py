@@ -75,26 +75,13 @@ def _gate_aware(cls):
     @functools.wraps(bwd)
     def backward(ctx, *grads):
         with _gated(ctx.gate):
-            res = bwd(ctx, *grads)
-            if _FLUSH_PER_BLOCK:   # the block's deferred weight gradients start now, beside the next block
-                _FLUSH_COUNT[0] += 1
-                if _FLUSH_COUNT[0] % _FLUSH_PER_BLOCK == 0:
-                    flush_wgrad()
-            return res
+            return bwd(ctx, *grads)
 
     cls.forward = staticmethod(forward)
     cls.backward = staticmethod(backward)
     return cls
 
 
-# B2P_WGRAD_FLUSH=block: the deferred frozen-weight gradient GEMMs of every encoder block go to the side
-# stream as soon as the block's backward is issued (they then overlap the rest of the backward); the
-# default ("gru") holds them until the GRU recurrence backward, whose few CUs leave the chip idle.
-# (block:N: after every N blocks). Round 6 with the flushed launches spanning only the flushed layers'
-# slots: see DESIGN.md section 5.
-_FLUSH_MODE = os.environ.get("B2P_WGRAD_FLUSH", "gru")
-_FLUSH_PER_BLOCK = (int(_FLUSH_MODE.split(":")[1]) if ":" in _FLUSH_MODE else 1) if _FLUSH_MODE.startswith("block") else 0
-_FLUSH_COUNT = [0]
 
 
 PRECISION_MODES = {"bf16": 0, "fp32": 1, "bf16x3": 3}   # GemmDesc.precision of each mode's fp32-operand GEMMs
@@ -635,8 +622,8 @@ def _run_wspecs(specs) -> bool:
     nslot = len(home.members)
     # every chunk's gathered operands first: a chunk that cannot be gathered (operands not 16-byte
     # aligned) makes the caller run ALL the specs one by one, so nothing may have been launched yet
-    # only the span of slots that holds present members: a flush of a few layers (B2P_WGRAD_FLUSH=block)
-    # launches those slots, not every slot of the home (whose absent members would run gated, += 0)
+    # only the span of slots that holds present members (slots of layers absent from this flush would
+    # run gated, += 0)
     lo, hi = min(at), max(at) + 1
     chunks = []
     for c0 in range(lo, hi, 64):
