@@ -13,6 +13,11 @@ int colsum_impl(const float* X, const float* Y, int64_t batch, int64_t M, int64_
 
 namespace {
 inline unsigned nblk(int64_t n, int bs = 256) { return (unsigned)((n + bs - 1) / bs); }
+// q = i / d, r = i - q * d in 32-bit arithmetic when the index space fits (the 64-bit division is a
+// ~40-instruction software sequence per thread); `fits` is wave-uniform
+__device__ __forceinline__ int64_t div_fit(int64_t i, int64_t d, bool fits) {
+  return fits ? (int64_t)((uint32_t)i / (uint32_t)d) : i / d;
+}
 
 // x rows (B*T) of H heads x D; cos/sin (T, D). out = x*cos + rotate_half(x)*sin
 // rotate_half(x) = cat(-x[D/2:], x[:D/2]); inverse (backward) applies the transpose.
@@ -96,10 +101,12 @@ __global__ void rotary4_k(const float* __restrict__ x, const float* __restrict__
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int D4 = D / 4;
   if (i4 >= rows * H * D4) return;
-  const int d = (int)(i4 % D4) * 4;
-  const int h = (int)((i4 / D4) % H);
-  const int64_t r = i4 / ((int64_t)D4 * H);
-  const int t = (int)(r % T);
+  const bool fits = rows * H * D4 < 0x100000000ll;
+  const int64_t q4 = div_fit(i4, D4, fits);
+  const int d = (int)(i4 - q4 * D4) * 4;
+  const int64_t r = div_fit(q4, H, fits);
+  const int h = (int)(q4 - r * H);
+  const int t = (int)(r - div_fit(r, T, fits) * T);
   const float* xr = x + r * ld + (int64_t)h * D;
   const int half = D / 2;
   const int od = d < half ? d + half : d - half;
@@ -134,7 +141,7 @@ __global__ void glu_fwd4_k(const float* __restrict__ a, float* __restrict__ out,
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t C4 = C / 4;
   if (i4 >= M * C4) return;
-  const int64_t m = i4 / C4, c = (i4 - m * C4) * 4;
+  const int64_t m = div_fit(i4, C4, M * C4 < 0x100000000ll), c = (i4 - m * C4) * 4;
   const float4 x = *reinterpret_cast<const float4*>(a + m * 2 * C + c);
   const float4 g = *reinterpret_cast<const float4*>(a + m * 2 * C + C + c);
   *reinterpret_cast<float4*>(out + m * C + c) =
@@ -160,7 +167,7 @@ __global__ void glu_bwd16_k(const float* __restrict__ a, const float* __restrict
   const int64_t i4 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t C4 = C / 4;
   if (i4 >= M * C4) return;
-  const int64_t m = i4 / C4, c = (i4 - m * C4) * 4;
+  const int64_t m = div_fit(i4, C4, M * C4 < 0x100000000ll), c = (i4 - m * C4) * 4;
   const float4 x = *reinterpret_cast<const float4*>(a + m * 2 * C + c);
   const float4 g = *reinterpret_cast<const float4*>(a + m * 2 * C + C + c);
   const float4 d = *reinterpret_cast<const float4*>(dout + m * C + c);
@@ -390,6 +397,11 @@ __global__ void bn_gxhat_k(const float* __restrict__ g, const float* __restrict_
   t[i] = g[i] * (x[i] - mean[c]) * rstd[c];
 }
 
+// channel group of float4 element i: a 32-bit modulo when the tensor allows (the 64-bit one is a ~40-
+// instruction software sequence, the largest VALU cost of these byte-bound passes); wave-uniform branch
+__device__ __forceinline__ int64_t chan4(int64_t i, int64_t n4, int64_t C4) {
+  return n4 < 0x100000000ll ? (int64_t)((uint32_t)i % (uint32_t)C4) : i % C4;
+}
 // float4 forms of the four BatchNorm elementwise passes above (C % 4 == 0, 16-B aligned tensors):
 // the same per-element expressions, 4 consecutive channels per thread, one index division per 4
 // elements (the scalar kernels' 64-bit modulo per element held them at ~60 % of HBM speed)
@@ -401,7 +413,7 @@ __global__ void bn_apply4_k(const float4* __restrict__ x, const float* __restric
                             int half = 0, uint2* __restrict__ y16b = nullptr) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  const int64_t c = 4 * (i % C4);
+  const int64_t c = 4 * chan4(i, n4, C4);
   const float4 xv = x[i];
   const float* xp = reinterpret_cast<const float*>(&xv);
   float v[4], o[4];
@@ -431,7 +443,7 @@ __global__ void bn_bwd_dx4_k(const float4* __restrict__ g, const float4* __restr
                              int64_t n4, int64_t C4, int64_t count) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  const int64_t c = 4 * (i % C4);
+  const int64_t c = 4 * chan4(i, n4, C4);
   const float4 gv = g[i], xv = x[i];
   const float* gp = reinterpret_cast<const float*>(&gv);
   const float* xp = reinterpret_cast<const float*>(&xv);
@@ -449,7 +461,7 @@ __global__ void bn_gxhat4_k(const float4* __restrict__ g, const float4* __restri
                             const float* __restrict__ rstd, float4* __restrict__ t, int64_t n4, int64_t C4) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n4) return;
-  const int64_t c = 4 * (i % C4);
+  const int64_t c = 4 * chan4(i, n4, C4);
   const float4 gv = g[i], xv = x[i];
   const float* gp = reinterpret_cast<const float*>(&gv);
   const float* xp = reinterpret_cast<const float*>(&xv);
