@@ -192,6 +192,22 @@ def test_implicit_unfold_views(mode):
         _close(dw, dy.t() @ u.view(B * T, -1), mode)
 
 
+@pytest.mark.parametrize("O,I,K", [(768, 256, 32), (40, 16, 8), (768, 48, 128), (6, 12, 5)])
+def test_conv_weight_permute_exact(O, I, K):
+    """b2p_conv_weight_permute (the tap-major GRU input / pos-conv weight copies and their gradients'
+    inverse) equals the torch permutation element for element, both directions: the 16-byte power-of-two
+    form (I, K powers of two) and the scalar tile form."""
+    Fn = _fn()
+    torch.manual_seed(6)
+    w = torch.randn(O, I, K, device="cuda")
+    wp = torch.empty(O, K, I, device="cuda")
+    Fn._lib.call("b2p_conv_weight_permute", w.data_ptr(), wp.data_ptr(), O, I, K, 0, Fn._st())
+    assert torch.equal(wp, w.permute(0, 2, 1))
+    back = torch.empty_like(w)
+    Fn._lib.call("b2p_conv_weight_permute", wp.data_ptr(), back.data_ptr(), O, I, K, 1, Fn._st())
+    assert torch.equal(back, w)
+
+
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
 def test_grouped_conv_view(mode):
     """positional conv: Conv1d(D, D, K, padding=K//2, groups=G) minus last frame as a grouped implicit GEMM."""

@@ -20,6 +20,20 @@ def _rel(a, b):
     return (a - b).abs().max().item() / (b.abs().max().item() + 1e-12)
 
 
+@pytest.mark.parametrize("n", [32 * 1024 * 256, 1001])
+def test_act_bwd_softsign_exact(n):
+    """b2p_act_bwd (the front end's softsign backward): the 16-byte form (n % 4 == 0) and the scalar form
+    both equal dy * (1 / (1 + |x|)^2) in fp32, element for element."""
+    Fn = _fn()
+    torch.manual_seed(8)
+    dy = torch.randn(n, device="cuda")
+    x = torch.randn(n, device="cuda") * 3
+    out = torch.empty_like(dy)
+    Fn._lib.call("b2p_act_bwd", dy.data_ptr(), x.data_ptr(), out.data_ptr(), n, Fn.ACT["softsign"], Fn._st())
+    d = 1.0 + x.abs()
+    assert torch.equal(out, dy * (1.0 / (d * d)))
+
+
 def test_layernorm_fwd_bwd():
     Fn = _fn()
     torch.manual_seed(0)

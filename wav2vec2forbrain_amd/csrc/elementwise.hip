@@ -846,16 +846,28 @@ __global__ void __launch_bounds__(256) softmax_bwd_k(const float* __restrict__ P
   }
 }
 
-__global__ void act_bwd_k(const float* __restrict__ dy, const float* __restrict__ pre, float* __restrict__ dx,
-                          int64_t n, int act) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float x = pre[i];
+__device__ __forceinline__ float act_bwd_one(float dy, float x, int act) {
   float g = 1.f;
   if (act == B2P_ACT_GELU) g = b2p_gelu_grad(x);
   else if (act == B2P_ACT_SOFTSIGN) { const float d = 1.f + fabsf(x); g = 1.f / (d * d); }
   else if (act == B2P_ACT_SILU) g = b2p_silu_grad(x);
-  dx[i] = dy[i] * g;
+  return dy * g;
+}
+__global__ void act_bwd_k(const float* __restrict__ dy, const float* __restrict__ pre, float* __restrict__ dx,
+                          int64_t n, int act) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  dx[i] = act_bwd_one(dy[i], pre[i], act);
+}
+// 4 elements per thread through 16-byte accesses (the front end's softsign' over B x L x 256: the scalar
+// form ran at ~1 TB/s), same expression per element
+__global__ void act_bwd4_k(const float4* __restrict__ dy, const float4* __restrict__ pre, float4* __restrict__ dx,
+                           int64_t n4, int act) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  const float4 d = dy[i], x = pre[i];
+  dx[i] = make_float4(act_bwd_one(d.x, x.x, act), act_bwd_one(d.y, x.y, act), act_bwd_one(d.z, x.z, act),
+                      act_bwd_one(d.w, x.w, act));
 }
 
 // ------------------------------------------------------------------ front-end
@@ -959,6 +971,46 @@ __global__ void __launch_bounds__(256) conv_perm_tile_k(const float* __restrict_
     for (int t = threadIdx.x; t < n; t += 256) {
       const int i = t / K, k = t - i * K;
       out[base + t] = tile[i * (K + 1) + k];
+    }
+  }
+}
+
+// conv_perm_tile_k for power-of-two I and K (>= 4; the GRU layer-0 input weight: I = 256 channels, K = 32
+// taps): 16-byte global loads and stores on both sides, index math by shifts (the scalar form's 4-byte
+// accesses and two runtime divisions per element ran it at ~0.7 TB/s)
+__global__ void __launch_bounds__(256) conv_perm_tile4_k(const float* __restrict__ in, float* __restrict__ out,
+                                                         int li, int lk, int inverse) {
+  extern __shared__ float tile[];   // I * (K + 1)
+  const int I = 1 << li, K = 1 << lk, K1 = K + 1;
+  const int64_t base = (int64_t)blockIdx.x * I * K;
+  const int n4 = (I * K) >> 2;
+  const float4* in4 = reinterpret_cast<const float4*>(in + base);
+  float4* out4 = reinterpret_cast<float4*>(out + base);
+  if (!inverse) {   // in (i, k) -> out (k, i)
+    for (int t = threadIdx.x; t < n4; t += 256) {
+      const int e = t << 2, i = e >> lk, k = e & (K - 1);
+      const float4 v = in4[t];
+      float* d = tile + i * K1 + k;
+      d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < n4; t += 256) {
+      const int e = t << 2, k = e >> li, i = e & (I - 1);
+      const float* sp = tile + i * K1 + k;
+      out4[t] = make_float4(sp[0], sp[K1], sp[2 * K1], sp[3 * K1]);
+    }
+  } else {          // in (k, i) -> out (i, k)
+    for (int t = threadIdx.x; t < n4; t += 256) {
+      const int e = t << 2, k = e >> li, i = e & (I - 1);
+      const float4 v = in4[t];
+      float* d = tile + i * K1 + k;
+      d[0] = v.x; d[K1] = v.y; d[2 * K1] = v.z; d[3 * K1] = v.w;
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < n4; t += 256) {
+      const int e = t << 2, i = e >> lk, k = e & (K - 1);
+      const float* sp = tile + i * K1 + k;
+      out4[t] = make_float4(sp[0], sp[1], sp[2], sp[3]);
     }
   }
 }
@@ -1572,7 +1624,12 @@ extern "C" int b2p_softmax_bwd(const float* P, const float* dPd, float* dS, int6
 extern "C" int b2p_act_bwd(const float* dy, const float* pre, float* dx, int64_t n, int act, b2p_stream_t stream) {
   B2P_CHECK_ARG(dy && pre && dx, "act_bwd: NULL pointer");
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(act_bwd_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, dy, pre, dx, n, act);
+  if (n % 4 == 0 && (((uintptr_t)dy | (uintptr_t)pre | (uintptr_t)dx) & 15u) == 0)
+    hipLaunchKernelGGL(act_bwd4_k, dim3(nblocks(n / 4)), dim3(256), 0, (hipStream_t)stream,
+                       reinterpret_cast<const float4*>(dy), reinterpret_cast<const float4*>(pre),
+                       reinterpret_cast<float4*>(dx), n / 4, act);
+  else
+    hipLaunchKernelGGL(act_bwd_k, dim3(nblocks(n)), dim3(256), 0, (hipStream_t)stream, dy, pre, dx, n, act);
   B2P_CHECK_LAUNCH();
   return 0;
 }
@@ -1617,7 +1674,12 @@ extern "C" int b2p_conv_weight_permute(const float* in, float* out, int64_t O, i
   const int64_t n = O * I * ntaps;
   if (n <= 0) return 0;
   const size_t lds = (size_t)I * (ntaps + 1) * sizeof(float);
-  if (lds <= 64 * 1024 && O < (1ll << 31))
+  auto pow2 = [](int64_t v) { return v >= 4 && (v & (v - 1)) == 0; };
+  if (lds <= 64 * 1024 && O < (1ll << 31) && pow2(I) && pow2(ntaps) && ((uintptr_t)in & 15u) == 0 &&
+      ((uintptr_t)out & 15u) == 0)
+    hipLaunchKernelGGL(conv_perm_tile4_k, dim3((unsigned)O), dim3(256), lds, (hipStream_t)stream, in, out,
+                       __builtin_ctzll((unsigned long long)I), __builtin_ctzll((unsigned long long)ntaps), inverse);
+  else if (lds <= 64 * 1024 && O < (1ll << 31))
     hipLaunchKernelGGL(conv_perm_tile_k, dim3((unsigned)O), dim3(256), lds, (hipStream_t)stream, in, out, (int)I,
                        (int)ntaps, inverse);
   else
