@@ -674,7 +674,8 @@ int b2p_layerdrop_select(const float* skip_val, const float* keep_val, float* ou
                          const uint16_t* skip16, const uint16_t* keep16, uint16_t* out16, int64_t n,
                          float p, uint64_t seed, b2p_stream_t stream);
 /* b2p_layerdrop_select plus the fp16 copy (outh from skiph / keeph, or packed from the selected values
- * when the chosen one is NULL): the next post-LN layer's fp16 forward operand, so it needs no cast. */
+ * when the chosen one is NULL): the next post-LN layer's fp16 forward operand, so it needs no cast.
+ * out == keep_val with out16 == keep16 and outh == keeph selects in place: a kept layer moves no bytes. */
 int b2p_layerdrop_select_h(const float* skip_val, const float* keep_val, float* out, const uint16_t* skip16,
                            const uint16_t* keep16, uint16_t* out16, const uint16_t* skiph, const uint16_t* keeph,
                            uint16_t* outh, int64_t n, float p, uint64_t seed, b2p_stream_t stream);

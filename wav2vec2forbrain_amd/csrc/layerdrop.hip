@@ -42,8 +42,10 @@ __global__ void __launch_bounds__(256) ld_select_k(const float4* skipv, const fl
                                                    const uint2* skip16, const uint2* keep16, uint2* out16,
                                                    int64_t n4, uint32_t thr, uint64_t seed,
                                                    const uint64_t* __restrict__ epoch, const uint2* skiph = nullptr,
-                                                   const uint2* keeph = nullptr, uint2* outh = nullptr) {
+                                                   const uint2* keeph = nullptr, uint2* outh = nullptr,
+                                                   int inplace = 0) {
   const bool keep = dev_keep(seed, epoch, thr);
+  if (keep && inplace) return;   // out (and its 16-bit copies) IS the kept tensor: nothing to move
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
     const float4 v = keep ? keepv[i] : skipv[i];
     out[i] = v;
@@ -114,7 +116,7 @@ extern "C" int b2p_layerdrop_select_h(const float* skip_val, const float* keep_v
   hipLaunchKernelGGL(ld_select_k, dim3(grid_for(n4)), dim3(256), 0, (hipStream_t)stream, (const float4*)skip_val,
                      (const float4*)keep_val, (float4*)out, (const uint2*)skip16, (const uint2*)keep16, (uint2*)out16,
                      n4, b2p_dropout_threshold(p), seed, b2p_seed_epoch(), (const uint2*)skiph, (const uint2*)keeph,
-                     (uint2*)outh);
+                     (uint2*)outh, (int)(out == keep_val && out16 == keep16 && outh == keeph));
   B2P_CHECK_LAUNCH();
   return 0;
 }

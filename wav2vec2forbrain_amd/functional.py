@@ -2030,12 +2030,21 @@ class _LayerDropSelect(torch.autograd.Function):
         y = y.contiguous()
         _chk(x, "layerdrop.x")
         _chk(y, "layerdrop.y")
-        out = torch.empty_like(y)
-        out16 = torch.empty(y.shape, device=y.device, dtype=BF16) if bf16_mode() else None
-        x16, y16 = (_b16_of(x), _b16_of(y)) if out16 is not None else (None, None)
+        b16 = bf16_mode()
+        x16, y16 = (_b16_of(x), _b16_of(y)) if b16 else (None, None)
         # the fp16 copy too when the layer made one (post-LN forward_f16): the next layer reads it uncast
-        yh = _h16_of(y) if out16 is not None and _LD_SELECT_H else None
-        outh = torch.empty(y.shape, device=y.device, dtype=torch.float16) if yh is not None else None
+        yh = _h16_of(y) if b16 and _LD_SELECT_H else None
+        if _LD_INPLACE and (not b16 or y16 is not None):
+            # in place: the output is a fresh tensor over y's storage (and y's 16-bit copies), overwritten
+            # by x only when the replay's draw skips the layer, so a kept layer's select moves no bytes.
+            # Nothing reads y's old values after a skip: the layer's own backward is gated off then.
+            out = torch.empty(0, device=y.device, dtype=y.dtype).set_(y.untyped_storage(), y.storage_offset(),
+                                                                       y.shape, y.stride())
+            out16, outh = y16, yh
+        else:
+            out = torch.empty_like(y)
+            out16 = torch.empty(y.shape, device=y.device, dtype=BF16) if b16 else None
+            outh = torch.empty(y.shape, device=y.device, dtype=torch.float16) if yh is not None else None
         _lib.call("b2p_layerdrop_select_h", _p(x), _p(y), _p(out), _p(x16), _p(y16), _p(out16),
                   _p(_h16_of(x)) if outh is not None else None, _p(yh), _p(outh), y.numel(), float(p), seed, _st())
         ctx.p, ctx.seed, ctx.slot = p, seed, slot
@@ -2058,6 +2067,7 @@ class _LayerDropSelect(torch.autograd.Function):
 
 
 _LD_SELECT_H = os.environ.get("B2P_LD_SELECT_H", "1") != "0"   # 0: no fp16 copy from the select (A/B)
+_LD_INPLACE = os.environ.get("B2P_LD_INPLACE", "1") != "0"     # 0: the select writes a new tensor (A/B)
 LAYERDROP_LOG = None   # tests: when a list, layerdrop_layer appends each layer's draw seed
 # diagnostic only (B2P_GRAPH_LAYERDROP=0): a captured step keeps the host draw made at capture time
 GRAPH_LAYERDROP = os.environ.get("B2P_GRAPH_LAYERDROP", "1") != "0"
