@@ -192,6 +192,23 @@ def test_implicit_unfold_views(mode):
         _close(dw, dy.t() @ u.view(B * T, -1), mode)
 
 
+@pytest.mark.parametrize("mode", ["fp32", "bf16"])
+@pytest.mark.parametrize("M,N", [(7968, 32), (1000, 48), (20000, 32)])
+def test_narrow_n_fp32_operands(mode, M, N):
+    """fp32-operand GEMMs with N <= 64 (the CTC lm_head, 768 -> 32 classes): 64 x 64 tiles when the 128-row
+    grid leaves most CUs idle, 128 x 64 otherwise; both against torch fp32, with the head's bias epilogue."""
+    Fn = _fn()
+    torch.manual_seed(9)
+    K = 768
+    a = torch.randn(M, K, device="cuda")
+    w = torch.randn(N, K, device="cuda") / 16
+    bias = torch.randn(N, device="cuda")
+    with Fn.precision(mode):
+        out = torch.empty(M, N, device="cuda")
+        Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(w, 0, K, True), out, N, bias=bias)
+    _close(out, a @ w.t() + bias, mode)
+
+
 @pytest.mark.parametrize("O,I,K", [(768, 256, 32), (40, 16, 8), (768, 48, 128), (6, 12, 5)])
 def test_conv_weight_permute_exact(O, I, K):
     """b2p_conv_weight_permute (the tap-major GRU input / pos-conv weight copies and their gradients'
