@@ -65,18 +65,29 @@ def test_step_matches_reference_golden(name, mode):
         ltol = 4e-2 if CFG[name].get("layers", 0) >= 24 else 2e-2
         assert np.linalg.norm(lg - fx["logits"]) <= ltol * np.linalg.norm(fx["logits"])
     gmax = max(float(fx["gnorm/" + n]) for n in fx["param_names"])
-    # bf16: 5e-2 relative L2 on gradients; 1.2e-1 for the 24-layer Conformer (bf16 rounding of every
-    # backward GEMM operand compounds over 24 x 4 sub-blocks, and the BatchNorm backward of the conv
-    # module subtracts means of bf16-rounded gradients: worst parameter measured 8.2e-2)
-    # (12-layer plumbing_base: worst parameter 5.3e-2 -> 6e-2)
+    # bf16 gates on the gradient norms and the relative L2 of the sampled entries, ~1.8x the worst values
+    # measured at the end of round 6 (profiles/r06z_golden_grad_errors.txt: worst norm error / sampled relL2):
+    # tiny fixtures 4.7e-3 / 9.6e-3 -> 2.5e-2; 12 layers (plumbing_base, base_L1280, base_bs32) 3.5e-3 /
+    # 4.6e-2 -> 6e-2 (plumbing_base's worst entry set is at 4.6e-2); 24-layer Conformers 9.0e-3 / 2.2e-2 ->
+    # 4e-2; the 24-layer post-LN wav2vec2-large (large960_bs32) 1.5e-2 / 1.38e-1 on a small-norm parameter
+    # whose entries the absolute 1e-5 * gmax term covers -> 1.2e-1 (bf16 rounding of every backward GEMM
+    # operand compounds over 24 post-LN blocks)
     nl = CFG[name].get("layers", 0)
-    gtol = 2e-3 if mode == "fp32" else (1.2e-1 if nl >= 24 else 6e-2 if nl >= 12 else 5e-2)
+    if mode == "fp32":
+        gtol = 2e-3
+    elif nl >= 24:
+        gtol = 4e-2 if "conformer" in name else 1.2e-1
+    else:
+        gtol = 6e-2 if nl >= 12 else 2.5e-2
     params = dict(model.named_parameters())
+    worst_norm = worst_l2 = 0.0
     for n in fx["param_names"]:
         p = params[n]
         g = p.grad if p.grad is not None else torch.zeros_like(p)
         ref_norm = float(fx["gnorm/" + n])
         got = float(g.double().norm())
+        if ref_norm >= 1e-6 * gmax:
+            worst_norm = max(worst_norm, abs(got - ref_norm) / ref_norm)
         assert abs(got - ref_norm) <= gtol * ref_norm + 1e-4 * gmax, (n, got, ref_norm)
         if "grad/" + n in fx:
             r = fx["grad/" + n]
@@ -94,7 +105,10 @@ def test_step_matches_reference_golden(name, mode):
         else:
             # bf16 MFMA through 12+ layers: element errors are a few % of the entry scale, so the
             # check is on the relative L2 error of the stored (sampled) gradient entries
+            worst_l2 = max(worst_l2, float(np.linalg.norm(v - r) / max(np.linalg.norm(r), 1e-30)))
             assert np.linalg.norm(v - r) <= gtol * np.linalg.norm(r) + 1e-5 * gmax, n
+    print(f"{name} [{mode}]: worst gradient-norm error {worst_norm:.3e}, worst sampled-gradient relL2 "
+          f"{worst_l2:.3e} (gate {gtol:g})")
 
 
 def test_full_size_loss_vs_oracle():
