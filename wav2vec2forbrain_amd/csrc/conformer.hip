@@ -449,10 +449,15 @@ __global__ void bn_bwd_dx4_k(const float4* __restrict__ g, const float4* __restr
   const float* xp = reinterpret_cast<const float*>(&xv);
   const float inv = 1.f / (float)count;
   float o[4];
+  // the scalar kernel's operation sequence spelled out (its contraction: g - inv * sum_g as one fma, the
+  // rest rounded per operation), so both forms write the same bits
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
+#pragma clang fp contract(off)
     const float xh = (xp[q] - mean[c + q]) * rstd[c + q];
-    o[q] = gamma[c + q] * rstd[c + q] * (gp[q] - sum_g[c + q] * inv - xh * sum_gx[c + q] * inv);
+    const float t = __builtin_fmaf(-inv, sum_g[c + q], gp[q]);
+    const float u = inv * (xh * sum_gx[c + q]);
+    o[q] = (gamma[c + q] * rstd[c + q]) * (t - u);
   }
   dx[i] = make_float4(o[0], o[1], o[2], o[3]);
 }
@@ -668,10 +673,10 @@ static void bn_gxhat_launch(const float* g, const float* x, const float* mean, c
 static void bn_bwd_dx_launch(const float* g, const float* x, const float* mean, const float* rstd, const float* gamma,
                              const float* sum_g, const float* sum_gx, float* dx, int64_t M, int64_t C, int64_t count,
                              hipStream_t st) {
-  // the float4 form differs from the scalar one in the last bit for some elements (measured,
-  // tests/test_kernels_gpu.py::test_conv_module_vector_paths_bitwise_equal_scalar_paths): off until
-  // that is understood, so the Conformer's input gradient keeps its bits
-  if (getenv("B2P_BN_DX4") && bn_vec(C, {g, x, dx}))
+  // the float4 form spells out the scalar form's contraction (bitwise equal:
+  // tests/test_kernels_gpu.py::test_conv_module_vector_paths_bitwise_equal_scalar_paths); B2P_BN_DX4=0: scalar
+  static const bool dx4 = !getenv("B2P_BN_DX4") || atoi(getenv("B2P_BN_DX4")) != 0;
+  if (dx4 && bn_vec(C, {g, x, dx}))
     hipLaunchKernelGGL(bn_bwd_dx4_k, dim3(nblk(M * C / 4)), dim3(256), 0, st, reinterpret_cast<const float4*>(g),
                        reinterpret_cast<const float4*>(x), mean, rstd, gamma, sum_g, sum_gx, reinterpret_cast<float4*>(dx),
                        M * C / 4, C / 4, count);
