@@ -299,6 +299,18 @@ def _nccl_world1_worker(port, out_dir, graphs, in_graph):
         dist.destroy_process_group()
 
 
+def _single_process_ref_worker(out_dir):
+    """The single-process reference steps of the RCCL world-1 test in a fresh process, like the workers
+    (state earlier tests left in the pytest process, e.g. consumed dropout seeds, cannot reach it)."""
+    torch.cuda.set_device(0)
+    cfg = _cfg("tiny_conf")
+    ref = build_model(cfg)
+    ref.train()
+    losses, _, _ = _trainer_steps(ref, [_batch(cfg, (0, cfg["B"]))] * 3, graphs=False, unfreeze="brain_encoder+w2v")
+    torch.save({"losses": losses, "params": {n: p.detach().cpu() for n, p in _optimised(ref, "brain_encoder+w2v")}},
+               os.path.join(out_dir, "single_process_ref.pt"))
+
+
 def test_rccl_world1_captured_collectives(tmp_path):
     """BASELINE configs[3]/[4] run over RCCL on 8 GPUs, which this box cannot: a one-rank RCCL process
     group with the data-parallel machinery forced on (B2P_DP_FORCE=1) runs the Conformer's SyncBN
@@ -307,13 +319,13 @@ def test_rccl_world1_captured_collectives(tmp_path):
     graph (the RCCL default, train.ddp.collectives_in_graph) and replayed with the segmented capture,
     leave the same parameters as the single-process steps (one rank: the all-reduces are identities)."""
     import torch.multiprocessing as mp
-    name, unfreeze = "tiny_conf", "brain_encoder+w2v"
-    cfg = _cfg(name)
-    ref = build_model(cfg)
-    ref.train()
-    ref_losses, _, _ = _trainer_steps(ref, [_batch(cfg, (0, cfg["B"]))] * 3, graphs=False, unfreeze=unfreeze)
-    params = {n: p.detach().cpu() for n, p in _optimised(ref, unfreeze)}
     ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_single_process_ref_worker, args=(str(tmp_path),))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0, p.exitcode
+    ref = torch.load(tmp_path / "single_process_ref.pt", weights_only=True)
+    ref_losses, params = ref["losses"], ref["params"]
     res = {}
     for graphs, in_graph in ((False, True), (True, True), (True, False)):
         p = ctx.Process(target=_nccl_world1_worker, args=(_free_port(), str(tmp_path), graphs, in_graph))
