@@ -4,6 +4,7 @@ train.ddp.GradBucketReducer, produce the single-process global-batch loss (mean 
 and gradients (bucket average). For the Conformer this holds because BatchNorm statistics are
 synchronised over the ranks (functional.sync_batchnorm); its running statistics match too.
 Deterministic mode (dropout / LayerDrop 0), exact-fp32 MFMA, so only the reduction order differs."""
+import math
 import os
 import socket
 
@@ -507,3 +508,48 @@ def test_dp_trainer_param_group_added_between_steps(tmp_path):
             d = float((r["params"][n] - p).norm())
             assert d <= 1e-4 * float(p.norm()) + 1e-6, (n, d)
         assert torch.equal(res[0]["params"][n], res[1]["params"][n]), n
+
+
+def _capture_fallback_worker(port, out_dir):
+    """One gloo rank with the data-parallel machinery forced on; every step capture raises."""
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), B2P_DP_FORCE="1")
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=0, world_size=1)
+    try:
+        from wav2vec2forbrain_amd import functional as Fn
+        from wav2vec2forbrain_amd.train.train_loop import Trainer
+        from wav2vec2forbrain_amd.workloads import SyntheticStepExperiment
+        cfg = _cfg("tiny_a")
+        model = build_model(cfg)
+        model.train()
+        model.sync_metrics = False
+        b = _batch(cfg, (0, cfg["B"]))
+        with Fn.precision("fp32"):
+            trainer = Trainer(SyntheticStepExperiment(model, lr=1e-3))
+            trainer.capture_after = 1
+
+            def fail(batch):
+                raise RuntimeError("capture refused (test)")
+            trainer._capture = fail
+            losses = [float(trainer.train_step(b).loss) for _ in range(3)]
+        torch.save({"losses": losses, "counts": (trainer.eager_steps, trainer.graph_steps),
+                    "failed": list(trainer._capture_failed.values())}, os.path.join(out_dir, "fallback.pt"))
+        Fn.set_deferred_wgrad([])
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dp_capture_failure_falls_back_to_eager_steps(tmp_path):
+    """A data-parallel step capture that raises leaves that batch shape on eager steps (the same update)
+    instead of ending the run: every step eager, the capture tried once, finite losses."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    p = ctx.Process(target=_capture_fallback_worker, args=(_free_port(), str(tmp_path)))
+    p.start()
+    p.join(timeout=240)
+    assert p.exitcode == 0, p.exitcode
+    r = torch.load(tmp_path / "fallback.pt", weights_only=True)
+    assert tuple(r["counts"]) == (3, 0), r["counts"]
+    assert len(r["failed"]) == 1 and "capture refused" in r["failed"][0], r["failed"]
+    assert all(math.isfinite(v) for v in r["losses"]), r["losses"]

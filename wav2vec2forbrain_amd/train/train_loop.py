@@ -7,6 +7,7 @@ from __future__ import annotations
 import contextlib
 import dataclasses
 import os
+import sys
 import uuid
 from typing import Literal, cast
 
@@ -66,6 +67,7 @@ class Trainer:
         self._graphs: dict = {}
         self._opt_generation = getattr(self.optimizer, "generation", 0)
         self._shape_seen: dict = {}
+        self._capture_failed: dict = {}   # batch shape -> the capture error (data-parallel fallback)
         self._epoch_counter = None
         self.graph_steps = 0
         self.eager_steps = 0
@@ -271,8 +273,20 @@ class Trainer:
             if g is None:
                 n = self._shape_seen.get(key, 0)
                 self._shape_seen[key] = n + 1
-                if n >= self.capture_after and len(self._graphs) < self.graph_cache_size:
-                    g = self._graphs[key] = self._capture(batch)
+                if (n >= self.capture_after and len(self._graphs) < self.graph_cache_size
+                        and key not in self._capture_failed):
+                    try:
+                        g = self._graphs[key] = self._capture(batch)
+                    except Exception as e:   # noqa: BLE001
+                        # a data-parallel capture that fails (the in-graph RCCL form has run at world size 1
+                        # only, on the boxes this was built on) leaves this batch shape on eager steps, which
+                        # compute the same update, instead of ending the run; B2P_CAPTURE_FALLBACK=0 raises
+                        if self.reducer is None or os.environ.get("B2P_CAPTURE_FALLBACK", "1") == "0":
+                            raise
+                        self._capture_failed[key] = repr(e)
+                        print(f"Trainer: step capture failed for batch shape {key[0]} ({e!r}); eager steps",
+                              file=sys.stderr, flush=True)
+                        g = None
             if g is not None:
                 self.graph_steps += 1
                 return self._replay(g, batch)
