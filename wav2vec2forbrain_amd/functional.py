@@ -144,6 +144,9 @@ def _fp32_if(name: str):
 _BWD_FOLLOWS_FWD = [os.environ.get("B2P_FP32_BWD", "0") == "1"]
 _FP32_BWD_OPS: set = set()   # blocks whose backward follows their forward's precision regardless
 _FP32_BWD_ONLY: set = set()  # blocks whose backward runs in exact fp32 (forward unchanged)
+# blocks whose backward always runs in the precision their forward ran in: the GRU layer, whose bf16-mode
+# forward (persistent recurrences, lane-native saved state) only its bf16-mode backward can consume
+_BWD_FOLLOWS_BLOCKS = frozenset({"gru"})
 
 
 def _prec_follow(cls):
@@ -163,7 +166,8 @@ def _prec_follow(cls):
         if ctx.block in _FP32_BWD_ONLY and _state.prec != 1:
             with precision("fp32"):
                 return bwd(ctx, *grads)
-        if (_BWD_FOLLOWS_FWD[0] or ctx.block in _FP32_BWD_OPS) and ctx.prec_fwd != _state.prec:
+        if (_BWD_FOLLOWS_FWD[0] or ctx.block in _FP32_BWD_OPS or ctx.block in _BWD_FOLLOWS_BLOCKS) \
+                and ctx.prec_fwd != _state.prec:
             with precision({v: k for k, v in PRECISION_MODES.items()}[ctx.prec_fwd]):
                 return bwd(ctx, *grads)
         return bwd(ctx, *grads)
@@ -1657,8 +1661,12 @@ class _GRULayer(torch.autograd.Function):
         gi = torch.empty(B, T, ndir * G3, device=dev)
         # bf16 mode: persistent MFMA recurrence (csrc/gru16.hip), which wants b_hh's r/z parts folded
         # into the input projection bias
-        use16 = bf16_mode() and _GRU16[0] and bool(_lib.load().b2p_gru16_supported(H))
-        usemc = bf16_mode() and not use16 and _GRUMC[0] and bool(_lib.load().b2p_gru_mc_supported(H))
+        # the bf16x3 mode's 'grurec1' form (X3_POLICY_FORMS): the persistent recurrences (fp16 / bf16 MFMA on
+        # W_hh h) with the input-projection and weight-gradient GEMMs kept in the mode's split-bf16 form
+        fast = bf16_mode() or (_state.prec == 3 and "grurec1" in (_state.x3forms if _state.x3forms is not None
+                                                                     else _X3_SINGLE))
+        use16 = fast and _GRU16[0] and bool(_lib.load().b2p_gru16_supported(H))
+        usemc = fast and not use16 and _GRUMC[0] and bool(_lib.load().b2p_gru_mc_supported(H))
         # the step's stacked recurrent weights / biases and the concatenated input-projection bias (with
         # b_hh's r/z parts folded in for gru16), assembled by ONE launch (b2p_gather_recs)
         whh_s = torch.empty(ndir, G3, H, device=dev)
@@ -1894,11 +1902,17 @@ def _view_off(t, off):
 
 def gru_layer(x, H, ndir, weights, h0=None):
     """One nn.GRU layer (both directions) — brain_feature_extractor.py:39-47,61-65.
-    x: (B,T,IN) tensor or Unfolded; weights: [w_ih, w_hh, b_ih, b_hh] per direction."""
+    x: (B,T,IN) tensor or Unfolded; weights: [w_ih, w_hh, b_ih, b_hh] per direction.
+    In the bf16x3 mode with the 'gru1' form (the Trainer policy, X3_POLICY_FORMS) the layer runs as in the
+    bf16 mode (persistent MFMA recurrences, fp16 forward operands) and its backward follows it
+    (_prec_follow: block 'gru'), instead of the fp32 operators' per-time-step recurrence kernels."""
     with _fp32_if("gru"):
-        if isinstance(x, Unfolded):
-            return _GRULayer.apply(x.src, (x.kernel, x.stride), H, ndir, h0, *weights)
-        return _GRULayer.apply(x, None, H, ndir, h0, *weights)
+        forms = _state.x3forms if _state.x3forms is not None else _X3_SINGLE
+        ctxm = precision("bf16") if (_state.prec == 3 and "gru1" in forms) else contextlib.nullcontext()
+        with ctxm:
+            if isinstance(x, Unfolded):
+                return _GRULayer.apply(x.src, (x.kernel, x.stride), H, ndir, h0, *weights)
+            return _GRULayer.apply(x, None, H, ndir, h0, *weights)
 
 
 # =====================================================================================
