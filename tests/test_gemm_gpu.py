@@ -192,6 +192,31 @@ def test_implicit_unfold_views(mode):
         _close(dw, dy.t() @ u.view(B * T, -1), mode)
 
 
+def test_bf16x3_role_forms():
+    """The bf16x3 mode's per-role GEMM forms (functional._x3_form) on a backward-data layout (A k-contiguous,
+    B n-contiguous): three-term split images (~16 bits per product), the two-term images of
+    b2p_split3_bf16's pattern | 16 (one operand ~16 bits, the other bf16) and single-pass bf16, against an
+    fp64 product: the error grows as terms are dropped, and the two-term forms sit between. (GEMMs under
+    2 GFLOP keep the fp32-operand kernel's three-MFMA form whatever the role's form: this one is 4.3.)"""
+    Fn = _fn()
+    torch.manual_seed(12)
+    M, N, K = 2048, 1024, 1024
+    a = torch.randn(M, K, device="cuda")
+    b = torch.randn(K, N, device="cuda")
+    ref = (a.double() @ b.double())
+
+    def run(forms):
+        out = torch.empty(M, N, device="cuda")
+        with Fn.precision("bf16x3"), Fn.x3_forms(forms):
+            Fn.gemm(M, N, K, Fn.op(a, 0, K, True), Fn.op(b, 0, N, False), out, N)
+        return float(((out.double() - ref).norm() / ref.norm()).item())
+    e3, e2a, e2b, e1 = run(()), run(("dgrad2a",)), run(("dgrad2b",)), run(("dgrad1",))
+    print("bf16x3 role forms relL2: three-term", e3, "2a", e2a, "2b", e2b, "single", e1)
+    assert e3 < 2e-5, e3
+    assert e3 < e2a < e1 and e3 < e2b < e1, (e3, e2a, e2b, e1)
+    assert e1 > 1e-3, e1
+
+
 @pytest.mark.parametrize("mode", ["fp32", "bf16"])
 @pytest.mark.parametrize("M,N", [(7968, 32), (1000, 48), (20000, 32)])
 def test_narrow_n_fp32_operands(mode, M, N):
