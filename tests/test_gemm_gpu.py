@@ -234,11 +234,13 @@ def test_narrow_n_fp32_operands(mode, M, N):
     _close(out, a @ w.t() + bias, mode)
 
 
-@pytest.mark.parametrize("O,I,K", [(768, 256, 32), (40, 16, 8), (768, 48, 128), (6, 12, 5)])
+@pytest.mark.parametrize("O,I,K", [(768, 256, 32), (1536, 256, 32), (3, 64, 64), (5, 4, 1024), (40, 16, 8),
+                                    (768, 48, 128), (6, 12, 5)])
 def test_conv_weight_permute_exact(O, I, K):
     """b2p_conv_weight_permute (the tap-major GRU input / pos-conv weight copies and their gradients'
     inverse) equals the torch permutation element for element, both directions: the 16-byte power-of-two
-    form (I, K powers of two) and the scalar tile form."""
+    form (I, K powers of two; the base / Conformer GRU weights, square and one-channel-wide shapes) and
+    the scalar tile form."""
     Fn = _fn()
     torch.manual_seed(6)
     w = torch.randn(O, I, K, device="cuda")
